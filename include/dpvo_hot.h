@@ -1,0 +1,161 @@
+/*
+ * dpvo_hot.h -- C ABI of the MI355X-native DPVO patch-graph hot path.
+ *
+ * One shared library (libdpvo_hot.so, built from
+ * the HIP sources in wild-video-3d-reconstruction_amd/csrc, for gfx950) exports the entry
+ * points below.  They replace the three PyTorch extensions the reference
+ * builds in setup.py:43-66 (cuda_corr, cuda_ba, lietorch_backends); the
+ * Python modules of the same names in wild-video-3d-reconstruction_amd/ bind
+ * them with ctypes and keep the reference's call signatures.
+ *
+ * Conventions
+ *  - All data pointers are DEVICE pointers (HIP, gfx950) unless stated.
+ *  - Sizes/strides are in ELEMENTS, int64, outermost first (torch order).
+ *  - `stream` is a hipStream_t passed as void*; NULL = the null stream.
+ *    Nothing here synchronises the host; every call only enqueues work.
+ *  - Return value: 0 on success, <0 on error (dpvo_hot_last_error() gives
+ *    the message; the Python shims raise RuntimeError with it, matching the
+ *    reference's TORCH_CHECK behaviour).
+ *  - Outputs are caller-allocated (the shims allocate them with torch so the
+ *    caching allocator owns them), as are workspaces (size via *_bytes()).
+ */
+#ifndef DPVO_HOT_H
+#define DPVO_HOT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { DPVO_F16 = 0, DPVO_F32 = 1, DPVO_F64 = 2 };
+
+#define DPVO_HOT_ABI_VERSION 1
+
+int dpvo_hot_abi_version(void);
+const char* dpvo_hot_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * altcorr -- replaces cuda_corr (reference dpvo/altcorr/correlation.cpp:57-62)
+ * --------------------------------------------------------------------- */
+
+/* cuda_corr.forward(fmap1, fmap2, coords, ii, jj, radius)
+ * (correlation.cpp:28-35 -> correlation_kernel.cu:193-233).
+ * gmap  [B][N1][C][P][P]   (the reference's "fmap1": per-patch features)
+ * fmap  [B][N2][C][H2][W2] (one pyramid level; any strides -- channel-last
+ *                           storage, stride(C)==1, takes the fast path)
+ * coords[B][E][2][P][P] float; ii, jj [E] int64.
+ * corr  contiguous [B][E][2r+1 (y)][2r+1 (x)][P][P] of `dtype`: the memory
+ *       of the reference's pre-permute tensor (the shim returns the same
+ *       .permute(0,1,3,2,4,5) view).
+ * fp16 results are bit-identical to the reference's c10::Half arithmetic. */
+int dpvo_corr_forward(int dtype, const void* gmap, const int64_t* gmap_size, const int64_t* gmap_stride,
+                      const void* fmap, const int64_t* fmap_size, const int64_t* fmap_stride, const float* coords,
+                      const int64_t* coords_size, const int64_t* coords_stride, const int64_t* ii, const int64_t* jj,
+                      int radius, void* corr, void* stream);
+
+/* Fused DPVO.corr (reference dpvo/dpvo.py:326-333): both pyramid levels of
+ * one gmap against `nlev` fmaps with coords scaled by 1/level_scale[l],
+ * written directly in the stacked layout the update operator consumes:
+ * corr [B][E][2r+1 (x)][2r+1 (y)][P][P][nlev] of `dtype`
+ * (= torch.stack([corr1, corr2], -1).view(1, E, -1)). */
+int dpvo_corr_forward_pyramid(int dtype, const void* gmap, const int64_t* gmap_size, const int64_t* gmap_stride,
+                              int nlev, const void* const* fmaps, const int64_t* fmap_sizes /* nlev*5 */,
+                              const int64_t* fmap_strides /* nlev*5 */, const float* level_scale,
+                              const float* coords, const int64_t* coords_size, const int64_t* coords_stride,
+                              const int64_t* ii, const int64_t* jj, int radius, void* corr, void* stream);
+
+/* cuda_corr.backward (correlation_kernel.cu:236-286): grad is the returned
+ * (permuted) view's gradient given as contiguous [B][E][2r+1 (x)][2r+1 (y)][P][P]
+ * float; gmap_grad / fmap_grad (contiguous, dtype, zero-filled by caller)
+ * are accumulated with atomics. */
+int dpvo_corr_backward(int dtype, const void* gmap, const int64_t* gmap_size, const void* fmap,
+                       const int64_t* fmap_size, const float* coords, const int64_t* coords_size, const int64_t* ii,
+                       const int64_t* jj, const float* grad, int radius, void* gmap_grad, void* fmap_grad,
+                       void* stream);
+
+/* cuda_corr.patchify_forward(net[B][C][H][W], coords[B][M][2] f32, radius)
+ * (correlation_kernel.cu:17-47,288-308): patches contiguous [B][M][C][D][D],
+ * D = 2r+2; out-of-image taps are written as zero. */
+int dpvo_patchify_forward(int dtype, const void* net, const int64_t* net_size, const int64_t* net_stride,
+                          const float* coords, int64_t M, int radius, void* patches, void* stream);
+
+/* cuda_corr.patchify_backward (correlation_kernel.cu:50-80,310-333):
+ * grad contiguous [B][M][C][D][D]; net_grad contiguous [B][C][H][W], zeroed
+ * by the caller, accumulated with atomics (f32/f64 only). */
+int dpvo_patchify_backward(int dtype, const int64_t* net_size, const float* coords, int64_t M, int radius,
+                           const void* grad, void* net_grad, void* stream);
+
+/* ------------------------------------------------------------------------
+ * fastba -- replaces cuda_ba (reference dpvo/fastba/ba.cpp:236-241)
+ * --------------------------------------------------------------------- */
+
+/* Workspace bytes for dpvo_ba_forward. */
+size_t dpvo_ba_workspace_bytes(int64_t num_edges, int64_t num_patches, int num_opt_poses);
+
+/* cuda_ba.forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj,
+ * kk, t0, t1, iterations) (ba.cpp:31-43 -> ba_cuda.cu:422-540).
+ * poses [*][7] and patches [num_patches][3][P][P] (contiguous float) are
+ * updated IN PLACE; intrinsics row 0 is used; target, weight [E][2];
+ * lmbda [1]; ii, jj, kk [E] int64.
+ * status (device int, may be NULL) receives 0, or the order of the leading
+ * minor at which the Cholesky factorisation failed (the reference raises
+ * there); iterations after a failure are skipped. */
+int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
+                    const float* target, const float* weight, const float* lmbda, const int64_t* ii,
+                    const int64_t* jj, const int64_t* kk, int64_t num_edges, int t0, int t1, int iterations,
+                    void* workspace, size_t workspace_bytes, int* status, void* stream);
+
+/* cuda_ba.reproject (ba_cuda.cu:368-418,543-575): coords [E][2][P][P]. */
+int dpvo_reproject(const float* poses, const float* patches, int P, const float* intrinsics, const int64_t* ii,
+                   const int64_t* jj, const int64_t* kk, int64_t num_edges, float* coords, void* stream);
+
+/* cuda_ba.neighbors(ii, jj) (ba.cpp:113-158), on the device: for every edge
+ * the previous / next edge of the same ii in stable jj order, -1 at ends. */
+size_t dpvo_neighbors_workspace_bytes(int64_t num_edges);
+int dpvo_neighbors(const int64_t* ii, const int64_t* jj, int64_t num_edges, int64_t* ix, int64_t* jx,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * lietorch -- replaces lietorch_backends (reference lietorch.cpp:286-316)
+ * group: 1 = SO3, 3 = SE3 (dispatch.h:16-31); dtype F32 or F64.
+ * All arrays are flat [n][dim] contiguous (already broadcast).
+ * --------------------------------------------------------------------- */
+enum {
+    DPVO_LIE_EXP = 0, DPVO_LIE_LOG, DPVO_LIE_INV, DPVO_LIE_MUL, DPVO_LIE_ADJ, DPVO_LIE_ADJT,
+    DPVO_LIE_ACT, DPVO_LIE_ACT4, DPVO_LIE_MATRIX, DPVO_LIE_PROJECTOR, DPVO_LIE_JINV
+};
+/* forward: out = op(X[, Y]) -- expm, logm, inv, mul, adj, adjT, act, act4,
+ * as_matrix, projector, Jinv (lietorch_gpu.cu:21-296). */
+int dpvo_lie_forward(int op, int group, int dtype, const void* X, const void* Y, void* out, int64_t n,
+                     void* stream);
+/* backward of expm/logm/inv/mul/adj/adjT/act/act4: dX (and dY for binary
+ * ops), caller-allocated and zero-filled with the shapes the reference
+ * returns (lietorch_gpu.cu:298-601). */
+int dpvo_lie_backward(int op, int group, int dtype, const void* grad, const void* X, const void* Y, void* dX,
+                      void* dY, int64_t n, void* stream);
+
+/* ------------------------------------------------------------------------
+ * projective ops -- fused forms of dpvo/projective_ops.py
+ * --------------------------------------------------------------------- */
+enum { DPVO_TF_DEPTH = 1, DPVO_TF_TONLY = 2, DPVO_TF_CHW = 4 };
+/* projective_ops.transform (projective_ops.py:53-68): per edge
+ * Gij = poses[jj] * poses[ii]^-1, X1 = Gij * iproj(patches[kk], K[ii]),
+ * x = K[jj] proj(X1) with Z clamped to >= 0.1.
+ * coords: [E][P][P][2|3] (default) or [E][2|3][P][P] (DPVO_TF_CHW);
+ * valid (optional) [E][P][P] float = (Z > 0.2). */
+int dpvo_transform(const float* poses, const float* patches, int P, const float* intrinsics, const int64_t* ii,
+                   const int64_t* jj, const int64_t* kk, int64_t num_edges, int flags, float* coords, float* valid,
+                   void* stream);
+
+/* projective_ops.point_cloud (projective_ops.py:106-108) of patches[0..m):
+ * centre_only=1 -> out [m][3] = xyz/w of the centre pixel (what
+ * DPVO.update stores in pg.points_, dpvo.py:747-749); else out [m][P][P][4]. */
+int dpvo_point_cloud(const float* poses, const float* patches, int P, const float* intrinsics, const int64_t* ix,
+                     int64_t m, int centre_only, float* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPVO_HOT_H */

@@ -1,0 +1,123 @@
+"""fastba / neighbors / reproject on the GPU (through the C ABI) vs the oracle.
+
+Bars: BA poses and depths within 1e-3 relative of the oracle (the reference
+itself sums with unordered float atomics, so it is not bit-reproducible);
+neighbors bit-exact (index work); reproject within fp32 rounding.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-3
+
+
+def T(a, d="cuda:0"):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(d)
+
+
+def run_gpu_ba(poses, patches, intr, target, weight, ii, jj, kk, t0, t1, iters):
+    import cuda_ba
+    p = T(poses)
+    q = T(patches)[None]
+    cuda_ba.forward(p, q, T(intr), T(target), T(weight), torch.tensor([1e-4], device="cuda:0"), T(ii), T(jj), T(kk),
+                    t0, t1, iters)
+    return p.cpu().numpy(), q[0].cpu().numpy()
+
+
+def assert_close_rel(got, ref, rtol=RTOL, floor=1e-5):
+    """norm-wise per tensor, and per element where |ref| > floor."""
+    assert np.linalg.norm(got - ref) <= rtol * max(np.linalg.norm(ref), floor)
+    big = np.abs(ref) > 1e-3
+    assert np.all(np.abs(got[big] - ref[big]) <= rtol * np.abs(ref[big]) + floor)
+
+
+@pytest.mark.parametrize("case", ["window", "full", "structure"])
+def test_ba_golden_cases(case):
+    g = np.load(os.path.join(GOLDEN, "ba_python_ref.npz"))
+    f = lambda k: g[f"{case}_{k}"]
+    args = (f("poses"), f("patches"), f("intrinsics"), f("target"), f("weight"), f("ii"), f("jj"), f("kk"),
+            int(f("t0")), int(f("t1")), int(f("iters")))
+    gp, gq = run_gpu_ba(*args)
+    rp, rq, st = oracle.ba_forward(*args[:5], 1e-4, *args[5:])
+    assert st == 0
+    assert_close_rel(gp, rp)
+    assert_close_rel(gq[:, 2], rq[:, 2])
+    # and against the reference's own Python BA output
+    assert_close_rel(gp, f("poses_out").reshape(-1, 7), rtol=2e-3)
+
+
+def synth_dpvo_state(seed, n=40, M=16, lifetime=13, removal=22):
+    """Tracker-shaped state: random-walk poses, DPVO edge rules."""
+    from tests_helpers import dpvo_state
+    return dpvo_state(seed, n=n, M=M, lifetime=lifetime, removal=removal)
+
+
+@pytest.mark.parametrize("seed,iters", [(0, 2), (1, 8)])
+def test_ba_dpvo_window(seed, iters):
+    st = synth_dpvo_state(seed)
+    n = st["n"]
+    t0, t1 = n - 10, n
+    args = (st["poses"], st["patches"], st["intrinsics"], st["target"], st["weight"], st["ii"], st["jj"], st["kk"],
+            t0, t1, iters)
+    gp, gq = run_gpu_ba(*args)
+    rp, rq, status = oracle.ba_forward(*args[:5], 1e-4, *args[5:])
+    assert status == 0
+    assert_close_rel(gp, rp)
+    assert_close_rel(gq[:, 2], rq[:, 2])
+    assert np.abs(gp - st["poses"]).max() > 1e-5  # the window moved
+
+
+def test_ba_fails_like_reference_on_non_spd():
+    import cuda_ba
+    g = np.load(os.path.join(GOLDEN, "ba_python_ref.npz"))
+    f = lambda k: g[f"window_{k}"]
+    w = np.full_like(f("weight"), np.nan)
+    p = T(f("poses"))
+    with pytest.raises(RuntimeError, match="positive-definite"):
+        cuda_ba.forward(p, T(f("patches"))[None], T(f("intrinsics")), T(f("target")), T(w),
+                        torch.tensor([1e-4], device="cuda:0"), T(f("ii")), T(f("jj")), T(f("kk")), int(f("t0")),
+                        int(f("t1")), 2)
+
+
+def test_ba_empty_edges_is_noop():
+    import cuda_ba
+    p = torch.zeros(4, 7, device="cuda:0"); p[:, 6] = 1
+    q = torch.rand(1, 8, 3, 3, 3, device="cuda:0")
+    q0 = q.clone()
+    e = torch.zeros(0, dtype=torch.long, device="cuda:0")
+    cuda_ba.forward(p, q, torch.ones(4, 4, device="cuda:0"), torch.zeros(1, 0, 2, device="cuda:0"),
+                    torch.zeros(1, 0, 2, device="cuda:0"), torch.tensor([1e-4], device="cuda:0"), e, e, e, 1, 4, 2)
+    assert torch.equal(q, q0)
+
+
+@pytest.mark.parametrize("pre", ["", "r_"])
+def test_neighbors_golden(pre):
+    import cuda_ba
+    g = np.load(os.path.join(GOLDEN, "neighbors_ref.npz"))
+    ix, jx = cuda_ba.neighbors(T(g[pre + "kk"]), T(g[pre + "jj"]))
+    assert np.array_equal(ix.cpu().numpy(), g[pre + "ix"])
+    assert np.array_equal(jx.cpu().numpy(), g[pre + "jx"])
+
+
+def test_neighbors_large_matches_oracle():
+    import cuda_ba
+    st = synth_dpvo_state(3, n=60, M=32)
+    ix, jx = cuda_ba.neighbors(T(st["kk"]), T(st["jj"]))
+    rix, rjx = oracle.neighbors(st["kk"], st["jj"])
+    assert np.array_equal(ix.cpu().numpy(), rix)
+    assert np.array_equal(jx.cpu().numpy(), rjx)
+
+
+def test_reproject_matches_oracle():
+    import cuda_ba
+    st = synth_dpvo_state(4)
+    out = cuda_ba.reproject(T(st["poses"])[None], T(st["patches"])[None], T(st["intrinsics"])[None], T(st["ii"]),
+                            T(st["jj"]), T(st["kk"]))
+    ref = oracle.reproject(st["poses"], st["patches"], st["intrinsics"], st["ii"], st["jj"], st["kk"])
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-5, atol=1e-3)

@@ -1,0 +1,54 @@
+"""Synthetic DPVO patch-graph states for tests (seeded, numpy only)."""
+import numpy as np
+
+from oracle import oracle
+
+
+def dpvo_edges(n, M, lifetime=13, removal=None):
+    """Edge construction of dpvo.py:756-769 replayed frame by frame, with the
+    removal rule of dpvo.py:657 (patch frame < n - REMOVAL_WINDOW) applied
+    after every frame when `removal` is given."""
+    ii = np.zeros(0, np.int64)
+    jj = np.zeros(0, np.int64)
+    kk = np.zeros(0, np.int64)
+    for t in range(1, n + 1):
+        k_f = np.arange(M * max(t - lifetime, 0), M * max(t - 1, 0))
+        j_f = np.full(len(k_f), t - 1)
+        kb = np.arange(M * (t - 1), M * t)
+        jb = np.arange(max(t - lifetime, 0), t)
+        k_b = np.repeat(kb, len(jb))
+        j_b = np.tile(jb, len(kb))
+        kk = np.concatenate([kk, k_f, k_b])
+        jj = np.concatenate([jj, j_f, j_b])
+        ii = np.concatenate([ii, k_f // M, k_b // M])
+        if removal is not None:
+            keep = ii >= t - removal
+            ii, jj, kk = ii[keep], jj[keep], kk[keep]
+    return ii.astype(np.int64), jj.astype(np.int64), kk.astype(np.int64)
+
+
+def dpvo_state(seed, n=40, M=16, lifetime=13, removal=22, wd=128, ht=96, intr=(80.0, 80.0, 80.0, 60.0)):
+    g = np.random.default_rng(seed)
+    poses = np.zeros((n, 7))
+    poses[:, 6] = 1.0
+    for i in range(1, n):
+        xi = np.concatenate([g.normal(0, 0.05, 3), g.normal(0, 0.01, 3)])
+        dq = oracle.lie_forward("exp", oracle.SE3, xi[None])
+        poses[i] = oracle.lie_forward("mul", oracle.SE3, dq, poses[i - 1:i])[0]
+    xs = g.integers(1, wd - 1, size=(n, M)).astype(np.float64)
+    ys = g.integers(1, ht - 1, size=(n, M)).astype(np.float64)
+    d = g.uniform(0.2, 1.0, size=(n, M))
+    patches = np.zeros((n, M, 3, 3, 3))
+    off = np.arange(3) - 1
+    patches[:, :, 0] = xs[:, :, None, None] + off[None, None, None, :]
+    patches[:, :, 1] = ys[:, :, None, None] + off[None, None, :, None]
+    patches[:, :, 2] = d[:, :, None, None]
+    patches = patches.reshape(n * M, 3, 3, 3)
+    intrinsics = np.tile(np.asarray(intr), (n, 1))
+    ii, jj, kk = dpvo_edges(n, M, lifetime, removal)
+    coords = oracle.transform(poses, patches, intrinsics, ii, jj, kk)[0]
+    target = coords[:, 1, 1, :] + g.normal(0, 1.0, size=(len(ii), 2))
+    weight = g.uniform(0.0, 1.0, size=(len(ii), 2))
+    return dict(n=n, M=M, poses=poses.astype(np.float32), patches=patches.astype(np.float32),
+                intrinsics=intrinsics.astype(np.float32), ii=ii, jj=jj, kk=kk,
+                target=target.astype(np.float32)[None], weight=weight.astype(np.float32)[None])

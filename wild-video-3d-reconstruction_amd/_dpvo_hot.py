@@ -1,0 +1,113 @@
+"""ctypes binding of libdpvo_hot.so (the C ABI declared in include/dpvo_hot.h).
+
+This is the only place that loads the native library.  There is no CPU or
+Python fallback: if the library is missing or a tensor is not on the GPU the
+call raises, so a silently-degraded run cannot pass for the HIP path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("DPVO_HOT_LIB", os.path.join(HERE, "libdpvo_hot.so"))
+
+F16, F32, F64 = 0, 1, 2
+_DTYPES = {torch.float16: F16, torch.float32: F32, torch.float64: F64}
+
+_i64 = ctypes.c_int64
+_vp = ctypes.c_void_p
+_ip = ctypes.c_int
+_fp = ctypes.c_float
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes)
+_SIGNATURES = {
+    "dpvo_hot_abi_version": (_ip, []),
+    "dpvo_hot_last_error": (ctypes.c_char_p, []),
+    "dpvo_corr_forward": (_ip, [_ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip, _vp, _vp]),
+    "dpvo_corr_forward_pyramid": (_ip, [_ip, _vp, _vp, _vp, _ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip,
+                                        _vp, _vp]),
+    "dpvo_corr_backward": (_ip, [_ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip, _vp, _vp, _vp]),
+    "dpvo_patchify_forward": (_ip, [_ip, _vp, _vp, _vp, _vp, _i64, _ip, _vp, _vp]),
+    "dpvo_patchify_backward": (_ip, [_ip, _vp, _vp, _i64, _ip, _vp, _vp, _vp]),
+    "dpvo_ba_workspace_bytes": (_sz, [_i64, _i64, _ip]),
+    "dpvo_ba_forward": (_ip, [_vp, _vp, _i64, _ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _ip, _ip, _ip, _vp, _sz,
+                              _vp, _vp]),
+    "dpvo_reproject": (_ip, [_vp, _vp, _ip, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "dpvo_neighbors_workspace_bytes": (_sz, [_i64]),
+    "dpvo_neighbors": (_ip, [_vp, _vp, _i64, _vp, _vp, _vp, _sz, _vp]),
+    "dpvo_lie_forward": (_ip, [_ip, _ip, _ip, _vp, _vp, _vp, _i64, _vp]),
+    "dpvo_lie_backward": (_ip, [_ip, _ip, _ip, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "dpvo_transform": (_ip, [_vp, _vp, _ip, _vp, _vp, _vp, _vp, _i64, _ip, _vp, _vp, _vp]),
+    "dpvo_point_cloud": (_ip, [_vp, _vp, _ip, _vp, _vp, _i64, _ip, _vp, _vp]),
+}
+EXPORTED = tuple(_SIGNATURES)
+
+_lib = None
+
+
+def lib():
+    """Load libdpvo_hot.so once; raise if it was not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libdpvo_hot.so not found at {LIB_PATH}; build it with `python -c \"import __graft_entry__ as g; "
+                f"g.build()\"` (hipcc, --offload-arch=gfx950)")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().dpvo_hot_last_error().decode(errors="replace")
+        raise RuntimeError(msg or f"dpvo_hot error {rc}")
+
+
+def on_gpu(*tensors):
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("MI355X build: operands must be GPU (HIP) tensors; this library has no CPU backend")
+
+
+def dtype_code(t):
+    try:
+        return _DTYPES[t.dtype]
+    except KeyError:
+        raise RuntimeError(f"unsupported dtype {t.dtype}") from None
+
+
+def stream_of(t):
+    return _vp(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def ptr(t):
+    return _vp(t.data_ptr()) if t is not None else _vp(0)
+
+
+def i64arr(vals):
+    vals = [int(v) for v in vals]
+    return (ctypes.c_int64 * max(len(vals), 1))(*vals)
+
+
+def sizes(t):
+    return i64arr(t.shape)
+
+
+def strides(t):
+    return i64arr(t.stride())
+
+
+def idx64(t):
+    """int64, contiguous, on the GPU (the reference passes torch.long)."""
+    if t.dtype != torch.int64:
+        t = t.long()
+    return t.contiguous()

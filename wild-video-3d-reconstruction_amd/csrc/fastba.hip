@@ -1,0 +1,752 @@
+// fastba.hip -- sparse Gauss-Newton bundle adjustment over SE(3) poses and
+// patch inverse depths, for gfx950.
+//
+// Replaces the reference's cuda_ba extension (dpvo/fastba/ba.cpp:236-241,
+// ba_cuda.cu).  Same normal equations and update as ba_cuda.cu:214-540:
+//   per edge (patch centre only): residual, mask, Jacobians Ji, Jj, Jz;
+//   B (6N x 6N pose block), E (6N x Mu), C, v, u; Q = 1/(C + lmbda);
+//   S = B - E Q E^T, y = v - E Q u, S += diag(1e-4 S + 1);
+//   dX = chol_solve(S, y); dZ = Q (u - E^T dX); left retraction of the poses,
+//   clamped additive update of the depths.
+//
+// MI355X structure (no host synchronisation inside the call):
+//   mark    -- bitmap of the referenced patches                (grid over E)
+//   scan    -- popcount prefix -> sorted unique ids kx, counts  (1 workgroup)
+//   zero    -- clear the Mu-sized accumulators                  (grid)
+//   per iteration:
+//     hessian -- per edge; B and v reduced in LDS (ds_add_f32), flushed
+//                once per workgroup; E/C/u with device atomics   (grid over E)
+//     schur   -- E Q E^T and E Q u over patch chunks             (grid over Mu)
+//     solve   -- Cholesky (fp64, LDS) + solve + pose retraction  (1 workgroup)
+//     patch   -- dZ, depth retraction, re-zero accumulators      (grid over Mu)
+// The unique-id inverse (the reference's torch::_unique, ba_cuda.cu:435) is
+// recomputed per edge from the bitmap instead of being stored.
+#include <algorithm>
+
+#include <hipcub/hipcub.hpp>
+
+#include "common.hpp"
+
+namespace dpvo {
+
+// ---------------------------------------------------------------------------
+// device SE3 helpers, float (restating ba_cuda.cu:18-156)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void actSO3(const float* q, const float* X, float* Y)
+{
+    float uv[3];
+    uv[0] = 2.0f * (q[1] * X[2] - q[2] * X[1]);
+    uv[1] = 2.0f * (q[2] * X[0] - q[0] * X[2]);
+    uv[2] = 2.0f * (q[0] * X[1] - q[1] * X[0]);
+    Y[0] = X[0] + q[3] * uv[0] + (q[1] * uv[2] - q[2] * uv[1]);
+    Y[1] = X[1] + q[3] * uv[1] + (q[2] * uv[0] - q[0] * uv[2]);
+    Y[2] = X[2] + q[3] * uv[2] + (q[0] * uv[1] - q[1] * uv[0]);
+}
+__device__ __forceinline__ void actSE3(const float* t, const float* q, const float* X, float* Y)
+{
+    actSO3(q, X, Y);
+    Y[3] = X[3];
+    Y[0] += X[3] * t[0];
+    Y[1] += X[3] * t[1];
+    Y[2] += X[3] * t[2];
+}
+__device__ __forceinline__ void adjSE3(const float* t, const float* q, const float* X, float* Y)
+{
+    const float qinv[4] = {-q[0], -q[1], -q[2], q[3]};
+    actSO3(qinv, &X[0], &Y[0]);
+    actSO3(qinv, &X[3], &Y[3]);
+    float u[3], v[3];
+    u[0] = t[2] * X[1] - t[1] * X[2];
+    u[1] = t[0] * X[2] - t[2] * X[0];
+    u[2] = t[1] * X[0] - t[0] * X[1];
+    actSO3(qinv, u, v);
+    Y[3] += v[0];
+    Y[4] += v[1];
+    Y[5] += v[2];
+}
+__device__ __forceinline__ void relSE3(const float* ti, const float* qi, const float* tj, const float* qj,
+                                       float* tij, float* qij)
+{
+    qij[0] = -qj[3] * qi[0] + qj[0] * qi[3] - qj[1] * qi[2] + qj[2] * qi[1];
+    qij[1] = -qj[3] * qi[1] + qj[1] * qi[3] - qj[2] * qi[0] + qj[0] * qi[2];
+    qij[2] = -qj[3] * qi[2] + qj[2] * qi[3] - qj[0] * qi[1] + qj[1] * qi[0];
+    qij[3] = qj[3] * qi[3] + qj[0] * qi[0] + qj[1] * qi[1] + qj[2] * qi[2];
+    actSO3(qij, ti, tij);
+    tij[0] = tj[0] - tij[0];
+    tij[1] = tj[1] - tij[1];
+    tij[2] = tj[2] - tij[2];
+}
+__device__ __forceinline__ void expSO3(const float* phi, float* q)
+{
+    const float theta_sq = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+    const float theta_p4 = theta_sq * theta_sq;
+    const float theta = sqrtf(theta_sq);
+    float imag, real;
+    if (theta_sq < 1e-8f) {
+        imag = 0.5f - (1.0f / 48.0f) * theta_sq + (1.0f / 3840.0f) * theta_p4;
+        real = 1.0f - (1.0f / 8.0f) * theta_sq + (1.0f / 384.0f) * theta_p4;
+    } else {
+        imag = sinf(0.5f * theta) / theta;
+        real = cosf(0.5f * theta);
+    }
+    q[0] = imag * phi[0];
+    q[1] = imag * phi[1];
+    q[2] = imag * phi[2];
+    q[3] = real;
+}
+__device__ __forceinline__ void cross_inplace(const float* a, float* b)
+{
+    const float x0 = a[1] * b[2] - a[2] * b[1], x1 = a[2] * b[0] - a[0] * b[2], x2 = a[0] * b[1] - a[1] * b[0];
+    b[0] = x0;
+    b[1] = x1;
+    b[2] = x2;
+}
+__device__ __forceinline__ void expSE3(const float* xi, float* t, float* q)
+{
+    expSO3(xi + 3, q);
+    float tau[3] = {xi[0], xi[1], xi[2]};
+    const float phi[3] = {xi[3], xi[4], xi[5]};
+    const float theta_sq = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+    const float theta = sqrtf(theta_sq);
+    t[0] = tau[0];
+    t[1] = tau[1];
+    t[2] = tau[2];
+    if (theta > 1e-4f) {
+        const float a = (1.0f - cosf(theta)) / theta_sq;
+        cross_inplace(phi, tau);
+        t[0] += a * tau[0];
+        t[1] += a * tau[1];
+        t[2] += a * tau[2];
+        const float b = (theta - sinf(theta)) / (theta * theta_sq);
+        cross_inplace(phi, tau);
+        t[0] += b * tau[0];
+        t[1] += b * tau[1];
+        t[2] += b * tau[2];
+    }
+}
+__device__ __forceinline__ void retrSE3(const float* xi, const float* t, const float* q, float* t1, float* q1)
+{
+    float dt[3] = {0, 0, 0}, dq[4] = {0, 0, 0, 1};
+    expSE3(xi, dt, dq);
+    q1[0] = dq[3] * q[0] + dq[0] * q[3] + dq[1] * q[2] - dq[2] * q[1];
+    q1[1] = dq[3] * q[1] + dq[1] * q[3] + dq[2] * q[0] - dq[0] * q[2];
+    q1[2] = dq[3] * q[2] + dq[2] * q[3] + dq[0] * q[1] - dq[1] * q[0];
+    q1[3] = dq[3] * q[3] - dq[0] * q[0] - dq[1] * q[1] - dq[2] * q[2];
+    actSO3(dq, t, t1);
+    t1[0] += dt[0];
+    t1[1] += dt[1];
+    t1[2] += dt[2];
+}
+
+// ---------------------------------------------------------------------------
+// workspace layout
+// ---------------------------------------------------------------------------
+constexpr int BA_LDS_NMAX = 12;  // optimised poses whose B fits in LDS (72x72 fp32)
+constexpr int BA_SOLVE_NMAX = 64;  // up to 384 x 384 (fp64 Cholesky in global scratch beyond BA_LDS_NMAX)
+constexpr int HDR_MU = 0, HDR_STATUS = 1, HDR_WORDS = 16;
+
+struct BaLayout {
+    size_t hdr, bits, wordbase, kx, B, v, C, u, E, S, y, dX, Sd, yd, total;
+    int64_t nwords, mu_max;
+    int n6;
+};
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static BaLayout ba_layout(int64_t E, int64_t num_patches, int N)
+{
+    BaLayout L{};
+    L.nwords = (num_patches + 31) / 32;
+    L.mu_max = E < num_patches ? E : num_patches;
+    if (L.mu_max < 1) L.mu_max = 1;
+    L.n6 = 6 * N;
+    const size_t n6 = (size_t)(L.n6 > 0 ? L.n6 : 1);
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += align256(bytes); return o; };
+    L.hdr = take(HDR_WORDS * 4);
+    L.bits = take((size_t)L.nwords * 4);
+    L.wordbase = take((size_t)L.nwords * 4);
+    L.kx = take((size_t)L.mu_max * 4);
+    L.B = take(n6 * n6 * 4);
+    L.v = take(n6 * 4);
+    L.C = take((size_t)L.mu_max * 4);
+    L.u = take((size_t)L.mu_max * 4);
+    L.E = take((size_t)L.mu_max * n6 * 4);
+    L.S = take(n6 * n6 * 4);
+    L.y = take(n6 * 4);
+    L.dX = take(n6 * 4);
+    // fp64 Cholesky scratch, only for systems too large for the LDS solver
+    const bool big = L.n6 > 6 * 12;
+    L.Sd = take(big ? n6 * (n6 + 1) * 8 : 8);
+    L.yd = take(big ? n6 * 8 : 8);
+    L.total = off;
+    return L;
+}
+
+struct BaParams {
+    float* poses;
+    float* patches;
+    const float* intrinsics;
+    const float* target;
+    const float* weight;
+    const float* lmbda;
+    const int64_t* ii;
+    const int64_t* jj;
+    const int64_t* kk;
+    int64_t E, num_patches;
+    int P, t0, N, n6;
+    int* hdr;
+    int* status;
+    uint32_t* bits;
+    int* wordbase;
+    int* kx;
+    float *B, *v, *C, *u, *Em, *S, *y, *dX;
+    double* Sd;
+    double* yd;
+};
+
+__device__ __forceinline__ bool failed(const BaParams& p) { return *(volatile int*)p.status != 0; }
+
+// ---------------------------------------------------------------------------
+// unique(kk): bitmap + popcount prefix
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ba_mark_kernel(BaParams p)
+{
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < p.E; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = p.kk[e];
+        if (k < 0 || k >= p.num_patches) {
+            atomicExch(p.status, -1);  // patch index out of range
+            continue;
+        }
+        atomicOr(&p.bits[k >> 5], 1u << (k & 31));
+    }
+}
+
+__global__ __launch_bounds__(1024) void ba_scan_kernel(BaParams p, int64_t nwords)
+{
+    __shared__ int part[1024];
+    const int tid = threadIdx.x;
+    const int64_t per = (nwords + 1023) / 1024;
+    const int64_t w0 = tid * per, w1 = min(nwords, w0 + per);
+    int cnt = 0;
+    for (int64_t w = w0; w < w1; w++) cnt += __popc(p.bits[w]);
+    part[tid] = cnt;
+    __syncthreads();
+    // inclusive Hillis-Steele scan over 1024 partials
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int add = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += add;
+        __syncthreads();
+    }
+    int base = part[tid] - cnt;
+    for (int64_t w = w0; w < w1; w++) {
+        uint32_t m = p.bits[w];
+        p.wordbase[w] = base;
+        while (m) {
+            const int bit = __ffs(m) - 1;
+            m &= m - 1;
+            p.kx[base++] = (int)(w * 32 + bit);
+        }
+    }
+    if (tid == 1023) p.hdr[HDR_MU] = part[1023];
+}
+
+__device__ __forceinline__ int unique_rank(const BaParams& p, int64_t k)
+{
+    const uint32_t w = p.bits[k >> 5];
+    return p.wordbase[k >> 5] + __popc(w & ((1u << (k & 31)) - 1u));
+}
+
+__global__ __launch_bounds__(256) void ba_zero_kernel(BaParams p)
+{
+    const int Mu = p.hdr[HDR_MU];
+    const int64_t nE = (int64_t)Mu * p.n6, nB = (int64_t)p.n6 * p.n6;
+    const int64_t total = nE + 2 * (int64_t)Mu + nB + p.n6 + nB + p.n6;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t j = i;
+        if (j < nE) { p.Em[j] = 0.f; continue; } j -= nE;
+        if (j < Mu) { p.C[j] = 0.f; continue; } j -= Mu;
+        if (j < Mu) { p.u[j] = 0.f; continue; } j -= Mu;
+        if (j < nB) { p.B[j] = 0.f; continue; } j -= nB;
+        if (j < p.n6) { p.v[j] = 0.f; continue; } j -= p.n6;
+        if (j < nB) { p.S[j] = 0.f; continue; } j -= nB;
+        p.y[j] = 0.f;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// residuals + normal equations (ba_cuda.cu:214-365)
+// ---------------------------------------------------------------------------
+template <bool LDS_B>
+__global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
+{
+    extern __shared__ __attribute__((aligned(16))) float sB[];  // [n6*n6] B upper triangle + [n6] v
+    const int n6 = p.n6;
+    if (failed(p)) return;
+    float* Bacc = LDS_B ? sB : p.B;
+    float* vacc = LDS_B ? sB + n6 * n6 : p.v;
+    if (LDS_B) {
+        for (int i = threadIdx.x; i < n6 * n6 + n6; i += blockDim.x) sB[i] = 0.f;
+        __syncthreads();
+    }
+    const float fx = p.intrinsics[0], fy = p.intrinsics[1], cx = p.intrinsics[2], cy = p.intrinsics[3];
+    const int64_t PP = (int64_t)p.P * p.P, centre = (p.P / 2) * p.P + p.P / 2;
+
+    for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < p.E; n += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t kxn = p.kk[n];
+        if (kxn < 0 || kxn >= p.num_patches) continue;
+        const int k = unique_rank(p, kxn);
+        const int64_t i_abs = p.ii[n], j_abs = p.jj[n];
+        const float* Pi = p.poses + i_abs * 7;
+        const float* Pj = p.poses + j_abs * 7;
+        const float ti[3] = {Pi[0], Pi[1], Pi[2]}, tj[3] = {Pj[0], Pj[1], Pj[2]};
+        const float qi[4] = {Pi[3], Pi[4], Pi[5], Pi[6]}, qj[4] = {Pj[3], Pj[4], Pj[5], Pj[6]};
+        const float* pa = p.patches + kxn * 3 * PP + centre;
+        float Xi[4], Xj[4], tij[3], qij[4];
+        Xi[0] = (pa[0] - cx) / fx;
+        Xi[1] = (pa[PP] - cy) / fy;
+        Xi[2] = 1.0f;
+        Xi[3] = pa[2 * PP];
+        relSE3(ti, qi, tj, qj, tij, qij);
+        actSE3(tij, qij, Xi, Xj);
+        const float X = Xj[0], Y = Xj[1], Z = Xj[2], W = Xj[3];
+        const float d = (Z >= 0.2f) ? 1.0f / Z : 0.0f;
+        const float d2 = d * d;
+        const float x1 = fx * (X / Z) + cx, y1 = fy * (Y / Z) + cy;
+        const float rx = p.target[n * 2 + 0] - x1, ry = p.target[n * 2 + 1] - y1;
+        const bool in_bounds = (sqrtf(rx * rx + ry * ry) < 128.f) && (Z > 0.2f) && (x1 > -64.f) && (y1 > -64.f) &&
+                               (x1 < 2.f * cx + 64.f) && (y1 < 2.f * cy + 64.f);
+        const float mask = in_bounds ? 1.0f : 0.0f;
+        const int ix = (int)(i_abs - p.t0), jx = (int)(j_abs - p.t0);
+        const bool iv = ix >= 0 && ix < p.N, jv = jx >= 0 && jx < p.N;
+
+        // both residual rows, summed per destination
+        float Ji[2][6], Jj[2][6], Jz[2], w[2], r[2];
+        w[0] = mask * p.weight[n * 2 + 0];
+        w[1] = mask * p.weight[n * 2 + 1];
+        r[0] = rx;
+        r[1] = ry;
+        Jz[0] = fx * (tij[0] * d - tij[2] * (X * d2));
+        Jz[1] = fy * (tij[1] * d - tij[2] * (Y * d2));
+        {
+            const float a[6] = {fx * W * d, 0.f, fx * -X * W * d2, fx * -X * Y * d2, fx * (1.f + X * X * d2), fx * -Y * d};
+            const float b[6] = {0.f, fy * W * d, fy * -Y * W * d2, fy * (-1.f - Y * Y * d2), fy * (X * Y * d2), fy * X * d};
+#pragma unroll
+            for (int t = 0; t < 6; t++) { Jj[0][t] = a[t]; Jj[1][t] = b[t]; }
+        }
+        adjSE3(tij, qij, Jj[0], Ji[0]);
+        adjSE3(tij, qij, Jj[1], Ji[1]);
+
+        // patch terms: E rows (device atomics), C, u
+        float Ei[6], Ej[6], Ck = 0.f, uk = 0.f;
+#pragma unroll
+        for (int t = 0; t < 6; t++) { Ei[t] = 0.f; Ej[t] = 0.f; }
+#pragma unroll
+        for (int row = 0; row < 2; row++) {
+#pragma unroll
+            for (int t = 0; t < 6; t++) {
+                Ei[t] += -w[row] * Jz[row] * Ji[row][t];
+                Ej[t] += w[row] * Jz[row] * Jj[row][t];
+            }
+            Ck += w[row] * Jz[row] * Jz[row];
+            uk += w[row] * r[row] * Jz[row];
+        }
+        atomicAdd(&p.C[k], Ck);
+        atomicAdd(&p.u[k], uk);
+        float* Erow = p.Em + (int64_t)k * n6;
+        if (iv) {
+#pragma unroll
+            for (int t = 0; t < 6; t++) atomicAdd(&Erow[6 * ix + t], Ei[t]);
+        }
+        if (jv) {
+#pragma unroll
+            for (int t = 0; t < 6; t++) atomicAdd(&Erow[6 * jx + t], Ej[t]);
+        }
+        // pose terms: v, and the upper triangle of B
+        if (iv) {
+#pragma unroll
+            for (int t = 0; t < 6; t++) atomicAdd(&vacc[6 * ix + t], -w[0] * r[0] * Ji[0][t] - w[1] * r[1] * Ji[1][t]);
+        }
+        if (jv) {
+#pragma unroll
+            for (int t = 0; t < 6; t++) atomicAdd(&vacc[6 * jx + t], w[0] * r[0] * Jj[0][t] + w[1] * r[1] * Jj[1][t]);
+        }
+        if (iv && jv && ix == jx) {
+            // self edge: Bii + Bjj - Bij - Bji land in one diagonal block
+#pragma unroll
+            for (int a = 0; a < 6; a++)
+#pragma unroll
+                for (int b = a; b < 6; b++) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int row = 0; row < 2; row++)
+                        s += w[row] * (Ji[row][a] * Ji[row][b] + Jj[row][a] * Jj[row][b] - Ji[row][a] * Jj[row][b] -
+                                       Jj[row][a] * Ji[row][b]);
+                    atomicAdd(&Bacc[(6 * ix + a) * n6 + 6 * ix + b], s);
+                }
+            continue;
+        }
+        if (iv) {
+#pragma unroll
+            for (int a = 0; a < 6; a++)
+#pragma unroll
+                for (int b = a; b < 6; b++)
+                    atomicAdd(&Bacc[(6 * ix + a) * n6 + 6 * ix + b],
+                              w[0] * Ji[0][a] * Ji[0][b] + w[1] * Ji[1][a] * Ji[1][b]);
+        }
+        if (jv) {
+#pragma unroll
+            for (int a = 0; a < 6; a++)
+#pragma unroll
+                for (int b = a; b < 6; b++)
+                    atomicAdd(&Bacc[(6 * jx + a) * n6 + 6 * jx + b],
+                              w[0] * Jj[0][a] * Jj[0][b] + w[1] * Jj[1][a] * Jj[1][b]);
+        }
+        if (iv && jv) {
+            // off-diagonal block stored once, in the upper triangle
+            const bool up = ix < jx;
+            const int r0 = up ? ix : jx, c0 = up ? jx : ix;
+#pragma unroll
+            for (int a = 0; a < 6; a++)
+#pragma unroll
+                for (int b = 0; b < 6; b++) {
+                    const float s = up ? -(w[0] * Ji[0][a] * Jj[0][b] + w[1] * Ji[1][a] * Jj[1][b])
+                                       : -(w[0] * Jj[0][a] * Ji[0][b] + w[1] * Jj[1][a] * Ji[1][b]);
+                    atomicAdd(&Bacc[(6 * r0 + a) * n6 + 6 * c0 + b], s);
+                }
+        }
+    }
+    if (LDS_B) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < n6 * n6 + n6; i += blockDim.x) {
+            const float s = sB[i];
+            if (s != 0.f) atomicAdd(i < n6 * n6 ? &p.B[i] : &p.v[i - n6 * n6], s);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Schur complement terms: S_acc += Q_k e_k e_k^T (upper), y_acc += Q_k u_k e_k
+// ---------------------------------------------------------------------------
+constexpr int SCHUR_CHUNK = 64;
+
+__global__ __launch_bounds__(256) void ba_schur_kernel(BaParams p)
+{
+    extern __shared__ __attribute__((aligned(16))) float sE[];  // [SCHUR_CHUNK][n6] rows + [SCHUR_CHUNK] Q
+    if (failed(p)) return;
+    const int Mu = p.hdr[HDR_MU];
+    const int n6 = p.n6;
+    const int nup = n6 * (n6 + 1) / 2;
+    const float lm = p.lmbda[0];
+    float* sQ = sE + SCHUR_CHUNK * n6;
+    for (int64_t k0 = (int64_t)blockIdx.x * SCHUR_CHUNK; k0 < Mu; k0 += (int64_t)gridDim.x * SCHUR_CHUNK) {
+        const int cnt = (int)min((int64_t)SCHUR_CHUNK, Mu - k0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt * n6; i += blockDim.x) sE[i] = p.Em[k0 * n6 + i];
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) sQ[i] = 1.0f / (p.C[k0 + i] + lm);
+        __syncthreads();
+        // upper triangle of sum_k (E_ak Q_k) E_bk, i.e. the reference's matmul(E*Q, E^T)
+        for (int idx = threadIdx.x; idx < nup; idx += blockDim.x) {
+            int a = 0, rem = idx;
+            while (rem >= n6 - a) { rem -= n6 - a; a++; }
+            const int b = a + rem;
+            float s = 0.f;
+            for (int kk = 0; kk < cnt; kk++) s += (sE[kk * n6 + a] * sQ[kk]) * sE[kk * n6 + b];
+            if (s != 0.f) atomicAdd(&p.S[a * n6 + b], s);
+        }
+        for (int a = threadIdx.x; a < n6; a += blockDim.x) {
+            float s = 0.f;
+            for (int kk = 0; kk < cnt; kk++) s += (sE[kk * n6 + a] * sQ[kk]) * p.u[k0 + kk];
+            if (s != 0.f) atomicAdd(&p.y[a], s);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// dense solve (fp64 Cholesky) + pose retraction; one workgroup
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ba_solve_kernel(BaParams p)
+{
+    extern __shared__ __attribute__((aligned(16))) double sA[];  // [n6][n6+1] + [n6]
+    __shared__ int s_fail;
+    if (failed(p)) return;
+    const int n = p.n6, ld = n + 1;
+    const bool in_lds = n <= 6 * BA_LDS_NMAX;
+    double* A = in_lds ? sA : p.Sd;
+    double* yv = in_lds ? sA + n * ld : p.yd;
+    const int tid = threadIdx.x;
+    if (tid == 0) s_fail = 0;
+    // S = B - E Q E^T (upper, mirrored), y = v - E Q u; damping S += diag(1e-4 S + 1)
+    for (int i = tid; i < n * n; i += blockDim.x) {
+        const int a = i / n, b = i - a * n;
+        const int r0 = a < b ? a : b, c0 = a < b ? b : a;
+        double s = (double)(p.B[r0 * n + c0] - p.S[r0 * n + c0]);
+        if (a == b) s += 1e-4 * s + 1.0;
+        A[a * ld + b] = s;
+    }
+    for (int i = tid; i < n; i += blockDim.x) yv[i] = (double)(p.v[i] - p.y[i]);
+    __syncthreads();
+    // right-looking Cholesky, lower triangle in place
+    for (int j = 0; j < n; j++) {
+        const double djj = A[j * ld + j];
+        if (!(djj > 0.0)) {
+            if (tid == 0) s_fail = j + 1;
+            break;
+        }
+        const double ljj = sqrt(djj);
+        __syncthreads();
+        for (int i = j + 1 + tid; i < n; i += blockDim.x) A[i * ld + j] /= ljj;
+        __syncthreads();
+        if (tid == 0) A[j * ld + j] = ljj;
+        const int m = n - j - 1;
+        for (int t = tid; t < m * m; t += blockDim.x) {
+            const int r = j + 1 + t / m, c = j + 1 + t % m;
+            if (c <= r) A[r * ld + c] -= A[r * ld + j] * A[c * ld + j];
+        }
+        __syncthreads();
+    }
+    __syncthreads();
+    if (s_fail) {
+        if (tid == 0) atomicExch(p.status, s_fail);
+        return;
+    }
+    // forward then backward substitution: L z = y, L^T x = z
+    for (int j = 0; j < n; j++) {
+        const double yj = yv[j] / A[j * ld + j];
+        __syncthreads();
+        if (tid == 0) yv[j] = yj;
+        for (int i = j + 1 + tid; i < n; i += blockDim.x) yv[i] -= A[i * ld + j] * yj;
+        __syncthreads();
+    }
+    for (int j = n - 1; j >= 0; j--) {
+        const double yj = yv[j] / A[j * ld + j];
+        __syncthreads();
+        if (tid == 0) yv[j] = yj;
+        for (int i = tid; i < j; i += blockDim.x) yv[i] -= A[j * ld + i] * yj;
+        __syncthreads();
+    }
+    for (int i = tid; i < n; i += blockDim.x) p.dX[i] = (float)yv[i];
+    __syncthreads();
+    // pose retraction (ba_cuda.cu:160-188)
+    for (int i = tid; i < p.N; i += blockDim.x) {
+        float* P = p.poses + (int64_t)(p.t0 + i) * 7;
+        const float t0v[3] = {P[0], P[1], P[2]}, q0v[4] = {P[3], P[4], P[5], P[6]};
+        float xi[6], t1v[3], q1v[4];
+        for (int k = 0; k < 6; k++) xi[k] = (float)yv[6 * i + k];
+        retrSE3(xi, t0v, q0v, t1v, q1v);
+        P[0] = t1v[0]; P[1] = t1v[1]; P[2] = t1v[2];
+        P[3] = q1v[0]; P[4] = q1v[1]; P[5] = q1v[2]; P[6] = q1v[3];
+    }
+    // reset the pose accumulators for the next iteration
+    for (int i = tid; i < n * n; i += blockDim.x) { p.B[i] = 0.f; p.S[i] = 0.f; }
+    for (int i = tid; i < n; i += blockDim.x) { p.v[i] = 0.f; p.y[i] = 0.f; }
+}
+
+// ---------------------------------------------------------------------------
+// depth update (ba_cuda.cu:191-211, :523) and accumulator reset
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void ba_patch_kernel(BaParams p, int structure_only, int reset)
+{
+    if (failed(p)) return;
+    const int Mu = p.hdr[HDR_MU];
+    const int n6 = p.n6;
+    const float lm = p.lmbda[0];
+    const int64_t PP = (int64_t)p.P * p.P;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < Mu; k += (int64_t)gridDim.x * blockDim.x) {
+        const float Q = 1.0f / (p.C[k] + lm);
+        float dZ;
+        float* Erow = p.Em + k * n6;
+        if (structure_only) {
+            dZ = Q * p.u[k];
+        } else {
+            float s = 0.f;
+            for (int a = 0; a < n6; a++) s += Erow[a] * p.dX[a];
+            dZ = Q * (p.u[k] - s);
+        }
+        float* pd = p.patches + ((int64_t)p.kx[k] * 3 + 2) * PP;
+        float d = pd[0] + dZ;
+        d = (d > 20.f) ? 1.0f : d;
+        d = fmaxf(d, 1e-4f);
+        for (int64_t q = 0; q < PP; q++) pd[q] = d;
+        if (reset) {
+            p.C[k] = 0.f;
+            p.u[k] = 0.f;
+            for (int a = 0; a < n6; a++) Erow[a] = 0.f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// fastba.reproject (ba_cuda.cu:368-418)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void reproject_kernel(const float* poses, const float* patches, int P,
+                                                       const float* intrinsics, const int64_t* ii, const int64_t* jj,
+                                                       const int64_t* kk, int64_t E, float* coords)
+{
+    const float fx = intrinsics[0], fy = intrinsics[1], cx = intrinsics[2], cy = intrinsics[3];
+    const int64_t PP = (int64_t)P * P;
+    for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < E; n += (int64_t)gridDim.x * blockDim.x) {
+        const float* Pi = poses + ii[n] * 7;
+        const float* Pj = poses + jj[n] * 7;
+        const float ti[3] = {Pi[0], Pi[1], Pi[2]}, tj[3] = {Pj[0], Pj[1], Pj[2]};
+        const float qi[4] = {Pi[3], Pi[4], Pi[5], Pi[6]}, qj[4] = {Pj[3], Pj[4], Pj[5], Pj[6]};
+        float tij[3], qij[4], Xi[4], Xj[4];
+        relSE3(ti, qi, tj, qj, tij, qij);
+        const float* pa = patches + kk[n] * 3 * PP;
+        for (int64_t q = 0; q < PP; q++) {
+            Xi[0] = (pa[q] - cx) / fx;
+            Xi[1] = (pa[PP + q] - cy) / fy;
+            Xi[2] = 1.0f;
+            Xi[3] = pa[2 * PP + q];
+            actSE3(tij, qij, Xi, Xj);
+            coords[(n * 2 + 0) * PP + q] = fx * (Xj[0] / Xj[2]) + cx;
+            coords[(n * 2 + 1) * PP + q] = fy * (Xj[1] / Xj[2]) + cy;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// neighbors on the device: stable sort by (ii, jj, edge), then prev/next
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void nb_keys_kernel(const int64_t* ii, const int64_t* jj, int64_t E, uint64_t* keys,
+                                                     int* vals)
+{
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+        // order-preserving map of signed 32-bit values to unsigned
+        const uint32_t hi = (uint32_t)(int32_t)ii[e] ^ 0x80000000u, lo = (uint32_t)(int32_t)jj[e] ^ 0x80000000u;
+        keys[e] = ((uint64_t)hi << 32) | lo;
+        vals[e] = (int)e;
+    }
+}
+
+__global__ __launch_bounds__(256) void nb_link_kernel(const uint64_t* keys, const int* vals, int64_t E, int64_t* ix,
+                                                     int64_t* jx)
+{
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < E; s += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t g = (uint32_t)(keys[s] >> 32);
+        const bool first = s == 0 || (uint32_t)(keys[s - 1] >> 32) != g;
+        const bool last = s == E - 1 || (uint32_t)(keys[s + 1] >> 32) != g;
+        const int e = vals[s];
+        ix[e] = first ? -1 : vals[s - 1];
+        jx[e] = last ? -1 : vals[s + 1];
+    }
+}
+
+static size_t nb_sort_temp_bytes(int64_t E)
+{
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (int*)nullptr,
+                                       (int*)nullptr, (int)E);
+    return bytes;
+}
+
+}  // namespace dpvo
+
+using namespace dpvo;
+
+extern "C" size_t dpvo_ba_workspace_bytes(int64_t num_edges, int64_t num_patches, int num_opt_poses)
+{
+    return ba_layout(num_edges, num_patches, num_opt_poses < 0 ? 0 : num_opt_poses).total;
+}
+
+extern "C" int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
+                               const float* target, const float* weight, const float* lmbda, const int64_t* ii,
+                               const int64_t* jj, const int64_t* kk, int64_t num_edges, int t0, int t1,
+                               int iterations, void* workspace, size_t workspace_bytes, int* status, void* stream)
+{
+    const int N = t1 - t0;
+    DPVO_CHECK_ARG(N >= 0, "t1 must be >= t0");
+    DPVO_CHECK_ARG(N <= BA_SOLVE_NMAX, "more than 64 optimised poses is not supported by the dense solver");
+    DPVO_CHECK_ARG(P >= 1 && num_patches >= 0 && iterations >= 0, "bad sizes");
+    const BaLayout L = ba_layout(num_edges, num_patches, N);
+    DPVO_CHECK_ARG(workspace && workspace_bytes >= L.total, "workspace too small");
+    hipStream_t s = as_stream(stream);
+    char* ws = (char*)workspace;
+    BaParams p{};
+    p.poses = poses; p.patches = patches; p.intrinsics = intrinsics; p.target = target; p.weight = weight;
+    p.lmbda = lmbda; p.ii = ii; p.jj = jj; p.kk = kk; p.E = num_edges; p.num_patches = num_patches;
+    p.P = P; p.t0 = t0; p.N = N; p.n6 = 6 * N;
+    p.hdr = (int*)(ws + L.hdr);
+    p.status = status ? status : p.hdr + HDR_STATUS;
+    p.bits = (uint32_t*)(ws + L.bits);
+    p.wordbase = (int*)(ws + L.wordbase);
+    p.kx = (int*)(ws + L.kx);
+    p.B = (float*)(ws + L.B); p.v = (float*)(ws + L.v); p.C = (float*)(ws + L.C); p.u = (float*)(ws + L.u);
+    p.Em = (float*)(ws + L.E); p.S = (float*)(ws + L.S); p.y = (float*)(ws + L.y); p.dX = (float*)(ws + L.dX);
+    p.Sd = (double*)(ws + L.Sd);
+    p.yd = (double*)(ws + L.yd);
+    if (num_edges == 0 || iterations == 0) {
+        if (status) DPVO_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
+        return 0;
+    }
+    DPVO_CHECK_HIP(hipMemsetAsync(ws + L.hdr, 0, L.wordbase - L.hdr, s));  // header + bitmap
+    if (status) DPVO_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
+    const unsigned gE = grid_for(num_edges, 256, 2048);
+    hipLaunchKernelGGL(ba_mark_kernel, dim3(gE), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(ba_scan_kernel, dim3(1), dim3(1024), 0, s, p, L.nwords);
+    hipLaunchKernelGGL(ba_zero_kernel, dim3(256), dim3(256), 0, s, p);
+    DPVO_CHECK_LAUNCH();
+    const bool lds_b = N <= BA_LDS_NMAX;
+    const size_t lds_h = lds_b ? (size_t)(p.n6 * p.n6 + p.n6) * 4 : 0;
+    const unsigned gH = grid_for(num_edges, 256, 1024);
+    const unsigned gP = grid_for(L.mu_max, 256, 1024);
+    const unsigned gS = (unsigned)std::min<int64_t>((L.mu_max + SCHUR_CHUNK - 1) / SCHUR_CHUNK, 512);
+    const size_t lds_s = (size_t)(SCHUR_CHUNK * p.n6 + SCHUR_CHUNK) * 4;
+    const size_t lds_v = lds_b ? (size_t)(p.n6 * (p.n6 + 1) + p.n6) * 8 : 0;
+    for (int it = 0; it < iterations; it++) {
+        if (lds_b)
+            hipLaunchKernelGGL(ba_hessian_kernel<true>, dim3(gH), dim3(256), lds_h, s, p);
+        else
+            hipLaunchKernelGGL(ba_hessian_kernel<false>, dim3(gH), dim3(256), 0, s, p);
+        if (N > 0) {
+            hipLaunchKernelGGL(ba_schur_kernel, dim3(gS), dim3(256), lds_s, s, p);
+            hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), lds_v, s, p);
+        }
+        hipLaunchKernelGGL(ba_patch_kernel, dim3(gP), dim3(256), 0, s, p, N == 0 ? 1 : 0, it + 1 < iterations ? 1 : 0);
+        DPVO_CHECK_LAUNCH();
+    }
+    return 0;
+}
+
+extern "C" int dpvo_reproject(const float* poses, const float* patches, int P, const float* intrinsics,
+                              const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t num_edges,
+                              float* coords, void* stream)
+{
+    DPVO_CHECK_ARG(P >= 1, "bad patch size");
+    if (num_edges == 0) return 0;
+    hipLaunchKernelGGL(reproject_kernel, dim3(grid_for(num_edges, 256)), dim3(256), 0, as_stream(stream), poses,
+                       patches, P, intrinsics, ii, jj, kk, num_edges, coords);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" size_t dpvo_neighbors_workspace_bytes(int64_t num_edges)
+{
+    const size_t n = (size_t)(num_edges > 0 ? num_edges : 1);
+    return align256(n * 8) * 2 + align256(n * 4) * 2 + align256(nb_sort_temp_bytes(num_edges > 0 ? num_edges : 1));
+}
+
+extern "C" int dpvo_neighbors(const int64_t* ii, const int64_t* jj, int64_t num_edges, int64_t* ix, int64_t* jx,
+                              void* workspace, size_t workspace_bytes, void* stream)
+{
+    if (num_edges == 0) return 0;
+    DPVO_CHECK_ARG(num_edges < 0x7fffffff, "too many edges");
+    DPVO_CHECK_ARG(workspace && workspace_bytes >= dpvo_neighbors_workspace_bytes(num_edges), "workspace too small");
+    hipStream_t s = as_stream(stream);
+    const size_t n = (size_t)num_edges;
+    char* ws = (char*)workspace;
+    uint64_t* k_in = (uint64_t*)ws;
+    uint64_t* k_out = (uint64_t*)(ws + align256(n * 8));
+    int* v_in = (int*)(ws + 2 * align256(n * 8));
+    int* v_out = (int*)(ws + 2 * align256(n * 8) + align256(n * 4));
+    void* tmp = ws + 2 * align256(n * 8) + 2 * align256(n * 4);
+    size_t tmp_bytes = nb_sort_temp_bytes(num_edges);
+    const unsigned g = grid_for(num_edges, 256, 2048);
+    hipLaunchKernelGGL(nb_keys_kernel, dim3(g), dim3(256), 0, s, ii, jj, num_edges, k_in, v_in);
+    DPVO_CHECK_LAUNCH();
+    DPVO_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k_in, k_out, v_in, v_out, (int)num_edges, 0, 64, s));
+    hipLaunchKernelGGL(nb_link_kernel, dim3(g), dim3(256), 0, s, k_out, v_out, num_edges, ix, jx);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}

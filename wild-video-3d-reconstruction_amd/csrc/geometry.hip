@@ -1,0 +1,114 @@
+// geometry.hip -- fused projective ops of dpvo/projective_ops.py for gfx950,
+// plus the library's runtime entry points (ABI version, error string).
+//
+// The reference composes transform() from ~30 ATen/lietorch launches and
+// materialises E*9 broadcast pose copies (lietorch/broadcasting.py:21-29);
+// here one thread handles one edge: Gij = poses[jj] * poses[ii]^-1 once, then
+// the P*P patch pixels, with lietorch's normalise-on-load semantics.
+#include <string>
+
+#include "common.hpp"
+#include "liegroups.hpp"
+
+namespace dpvo {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+using G3 = lie::SE3<float>;
+
+__global__ __launch_bounds__(256) void transform_kernel(const float* poses, const float* patches, int P,
+                                                       const float* intr, const int64_t* ii, const int64_t* jj,
+                                                       const int64_t* kk, int64_t E, int flags, float* coords,
+                                                       float* valid)
+{
+    const bool depth = flags & DPVO_TF_DEPTH, tonly = flags & DPVO_TF_TONLY, chw = flags & DPVO_TF_CHW;
+    const int od = depth ? 3 : 2;
+    const int64_t PP = (int64_t)P * P;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = ii[e], j = jj[e];
+        // Gij = poses[jj] * poses[ii].inv()   (projective_ops.py:60)
+        G3 g = G3::load(poses + j * 7).mul(G3::load(poses + i * 7).inv());
+        if (tonly) { g.so3.q.x = 0.f; g.so3.q.y = 0.f; g.so3.q.z = 0.f; g.so3.q.w = 1.f; }
+        const float *ki = intr + i * 4, *kj = intr + j * 4;
+        const float* pa = patches + kk[e] * 3 * PP;
+        for (int64_t q = 0; q < PP; q++) {
+            // iproj (projective_ops.py:19-29)
+            const float X0[4] = {(pa[q] - ki[2]) / ki[0], (pa[PP + q] - ki[3]) / ki[1], 1.0f, pa[2 * PP + q]};
+            float X1[4];
+            g.act4(X0, X1);
+            // proj with Z clamped to >= 0.1 (projective_ops.py:32-50)
+            const float d = 1.0f / fmaxf(X1[2], 0.1f);
+            const float x = kj[0] * (d * X1[0]) + kj[2];
+            const float y = kj[1] * (d * X1[1]) + kj[3];
+            if (chw) {
+                coords[(e * od + 0) * PP + q] = x;
+                coords[(e * od + 1) * PP + q] = y;
+                if (depth) coords[(e * od + 2) * PP + q] = d;
+            } else {
+                coords[(e * PP + q) * od + 0] = x;
+                coords[(e * PP + q) * od + 1] = y;
+                if (depth) coords[(e * PP + q) * od + 2] = d;
+            }
+            if (valid) valid[e * PP + q] = X1[2] > 0.2f ? 1.0f : 0.0f;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void point_cloud_kernel(const float* poses, const float* patches, int P,
+                                                         const float* intr, const int64_t* ix, int64_t m,
+                                                         int centre_only, float* out)
+{
+    const int64_t PP = (int64_t)P * P, centre = (P / 2) * P + P / 2;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t f = ix[k];
+        const G3 g = G3::load(poses + f * 7).inv();
+        const float* K = intr + f * 4;
+        const float* pa = patches + k * 3 * PP;
+        if (centre_only) {
+            const float X0[4] = {(pa[centre] - K[2]) / K[0], (pa[PP + centre] - K[3]) / K[1], 1.0f, pa[2 * PP + centre]};
+            float X1[4];
+            g.act4(X0, X1);
+            out[k * 3 + 0] = X1[0] / X1[3];
+            out[k * 3 + 1] = X1[1] / X1[3];
+            out[k * 3 + 2] = X1[2] / X1[3];
+        } else {
+            for (int64_t q = 0; q < PP; q++) {
+                const float X0[4] = {(pa[q] - K[2]) / K[0], (pa[PP + q] - K[3]) / K[1], 1.0f, pa[2 * PP + q]};
+                g.act4(X0, out + (k * PP + q) * 4);
+            }
+        }
+    }
+}
+
+}  // namespace dpvo
+
+using namespace dpvo;
+
+extern "C" int dpvo_hot_abi_version(void) { return DPVO_HOT_ABI_VERSION; }
+extern "C" const char* dpvo_hot_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" int dpvo_transform(const float* poses, const float* patches, int P, const float* intrinsics,
+                              const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t num_edges, int flags,
+                              float* coords, float* valid, void* stream)
+{
+    DPVO_CHECK_ARG(P >= 1, "bad patch size");
+    if (num_edges == 0) return 0;
+    DPVO_CHECK_ARG(poses && patches && intrinsics && ii && jj && kk && coords, "null operand");
+    hipLaunchKernelGGL(transform_kernel, dim3(grid_for(num_edges, 256)), dim3(256), 0, as_stream(stream), poses,
+                       patches, P, intrinsics, ii, jj, kk, num_edges, flags, coords, valid);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_point_cloud(const float* poses, const float* patches, int P, const float* intrinsics,
+                                const int64_t* ix, int64_t m, int centre_only, float* out, void* stream)
+{
+    DPVO_CHECK_ARG(P >= 1, "bad patch size");
+    if (m == 0) return 0;
+    DPVO_CHECK_ARG(poses && patches && intrinsics && ix && out, "null operand");
+    hipLaunchKernelGGL(point_cloud_kernel, dim3(grid_for(m, 256)), dim3(256), 0, as_stream(stream), poses, patches,
+                       P, intrinsics, ix, m, centre_only, out);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}

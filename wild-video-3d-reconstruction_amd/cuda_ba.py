@@ -1,0 +1,87 @@
+"""Drop-in replacement for the reference's ``cuda_ba`` extension.
+
+Same module name, functions and argument meaning as dpvo/fastba/ba.cpp:236-241
+(imported by dpvo/fastba/ba.py:2); the work runs in libdpvo_hot.so
+(csrc/fastba.hip) on the current HIP stream.
+
+``CHECK_CHOLESKY`` (default True) keeps the reference's behaviour of raising
+when the Schur system is not positive definite (torch::linalg::cholesky in
+ba_cuda.cu:521 raises); it costs one device->host read of a status word per
+call.  Set it to False for fully asynchronous / graph-captured use; the
+status is then left in ``last_status`` (a device tensor).
+"""
+import torch
+
+import _dpvo_hot as H
+
+CHECK_CHOLESKY = True
+last_status = None
+
+
+def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, iterations):
+    """ba.cpp:31-43 -> ba_cuda.cu:422-540.  Updates poses and patches in place; returns []."""
+    global last_status
+    H.on_gpu(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk)
+    for name, t in (("poses", poses), ("patches", patches), ("intrinsics", intrinsics), ("target", target),
+                    ("weight", weight)):
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"{name} must be float32")
+        if not t.is_contiguous():
+            raise RuntimeError(f"{name} must be contiguous (the reference views it, ba_cuda.cu:446-451)")
+    P = patches.shape[3] if patches.dim() == 5 else patches.shape[-1]
+    num_patches = patches.numel() // (3 * P * P)
+    ii, jj, kk = H.idx64(ii), H.idx64(jj), H.idx64(kk)
+    lmbda = lmbda.to(device=poses.device, dtype=torch.float32).contiguous()
+    E = ii.numel()
+    N = int(t1) - int(t0)
+    nbytes = H.lib().dpvo_ba_workspace_bytes(E, num_patches, max(N, 0))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=poses.device)
+    status = torch.zeros(1, dtype=torch.int32, device=poses.device)
+    H.check(H.lib().dpvo_ba_forward(
+        H.ptr(poses), H.ptr(patches), num_patches, P, H.ptr(intrinsics), H.ptr(target), H.ptr(weight), H.ptr(lmbda),
+        H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(t0), int(t1), int(iterations), H.ptr(ws), nbytes, H.ptr(status),
+        H.stream_of(poses)))
+    last_status = status
+    if CHECK_CHOLESKY:
+        s = int(status.item())
+        if s > 0:
+            raise RuntimeError(
+                "linalg.cholesky: The factorization could not be completed because the input is not positive-"
+                f"definite (the leading minor of order {s} is not positive-definite).")
+        if s < 0:
+            raise RuntimeError("cuda_ba.forward: patch index out of range")
+    return []
+
+
+def neighbors(ii, jj):
+    """ba.cpp:113-158, GPU-resident: -> [ix, jx] (int64)."""
+    H.on_gpu(ii, jj)
+    ii, jj = H.idx64(ii), H.idx64(jj)
+    E = ii.numel()
+    ix = torch.empty(E, dtype=torch.int64, device=ii.device)
+    jx = torch.empty(E, dtype=torch.int64, device=ii.device)
+    if E:
+        nbytes = H.lib().dpvo_neighbors_workspace_bytes(E)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=ii.device)
+        H.check(H.lib().dpvo_neighbors(H.ptr(ii), H.ptr(jj), E, H.ptr(ix), H.ptr(jx), H.ptr(ws), nbytes,
+                                       H.stream_of(ii)))
+    return [ix, jx]
+
+
+def reproject(poses, patches, intrinsics, ii, jj, kk):
+    """ba.cpp:53-61 / ba_cuda.cu:543-575 -> coords [1, E, 2, P, P]."""
+    H.on_gpu(poses, patches, intrinsics, ii, jj, kk)
+    poses, patches, intrinsics = poses.contiguous(), patches.contiguous(), intrinsics.contiguous()
+    P = patches.shape[-1]
+    ii, jj, kk = H.idx64(ii), H.idx64(jj), H.idx64(kk)
+    E = ii.numel()
+    out = torch.empty((E, 2, P, P), dtype=torch.float32, device=poses.device)
+    H.check(H.lib().dpvo_reproject(H.ptr(poses), H.ptr(patches), P, H.ptr(intrinsics), H.ptr(ii), H.ptr(jj),
+                                   H.ptr(kk), E, H.ptr(out), H.stream_of(poses)))
+    return out.view(1, E, 2, P, P)
+
+
+def solve_system(J_Ginv_i, J_Ginv_j, ii, jj, res, ep, lm, freen):
+    """ba.cpp:181-241 (loop-closure PGO, Eigen sparse Cholesky) -- not built yet
+    for MI355X (a later-round item)."""
+    raise NotImplementedError("cuda_ba.solve_system is not implemented in the MI355X build yet")

@@ -1,0 +1,94 @@
+"""Drop-in replacement for the reference's ``cuda_corr`` extension.
+
+Same module name, functions and argument meaning as
+dpvo/altcorr/correlation.cpp:57-62 (imported by dpvo/altcorr/correlation.py:2);
+the work runs in libdpvo_hot.so (csrc/altcorr.hip) on the current HIP stream.
+"""
+import torch
+
+import _dpvo_hot as H
+
+
+def _check_corr_args(fmap1, fmap2, coords, ii, jj):
+    H.on_gpu(fmap1, fmap2, coords, ii, jj)
+    if fmap1.dtype != fmap2.dtype:
+        raise RuntimeError("fmap1 and fmap2 must have the same dtype")
+    if coords.dtype != torch.float32:
+        raise RuntimeError("coords must be float32")
+    if fmap1.dim() != 5 or fmap2.dim() != 5 or coords.dim() != 5:
+        raise RuntimeError("expected fmap1 [B,N1,C,P,P], fmap2 [B,N2,C,H,W], coords [B,E,2,P,P]")
+
+
+def forward(fmap1, fmap2, coords, ii, jj, radius):
+    """correlation.cpp:28-35 -> [corr]; corr is the reference's permuted view
+    [B, E, 2r+1 (x), 2r+1 (y), P, P] (correlation_kernel.cu:232)."""
+    _check_corr_args(fmap1, fmap2, coords, ii, jj)
+    B, E, _, Hh, W = coords.shape
+    Do = 2 * radius + 1
+    out = torch.empty((B, E, Do, Do, Hh, W), dtype=fmap1.dtype, device=fmap1.device)
+    ii, jj = H.idx64(ii), H.idx64(jj)
+    H.check(H.lib().dpvo_corr_forward(
+        H.dtype_code(fmap1), H.ptr(fmap1), H.sizes(fmap1), H.strides(fmap1), H.ptr(fmap2), H.sizes(fmap2),
+        H.strides(fmap2), H.ptr(coords), H.sizes(coords), H.strides(coords), H.ptr(ii), H.ptr(jj), int(radius),
+        H.ptr(out), H.stream_of(fmap1)))
+    return [out.permute(0, 1, 3, 2, 4, 5)]
+
+
+def forward_pyramid(fmap1, pyramid, coords, ii, jj, radius, scales):
+    """Fused form of DPVO.corr (dpvo/dpvo.py:326-333): all levels in one
+    launch, returned in the stacked layout torch.stack([...], -1).view(B, E, -1)."""
+    for f in pyramid:
+        _check_corr_args(fmap1, f, coords, ii, jj)
+    B, E, _, Hh, W = coords.shape
+    L = len(pyramid)
+    Do = 2 * radius + 1
+    out = torch.empty((B, E, Do * Do * Hh * W * L), dtype=fmap1.dtype, device=fmap1.device)
+    ii, jj = H.idx64(ii), H.idx64(jj)
+    ptrs = (H._vp * L)(*[f.data_ptr() for f in pyramid])
+    fs = H.i64arr([s for f in pyramid for s in f.shape])
+    fst = H.i64arr([s for f in pyramid for s in f.stride()])
+    sc = (H._fp * L)(*[float(s) for s in scales])
+    H.check(H.lib().dpvo_corr_forward_pyramid(
+        H.dtype_code(fmap1), H.ptr(fmap1), H.sizes(fmap1), H.strides(fmap1), L, ptrs, fs, fst, sc, H.ptr(coords),
+        H.sizes(coords), H.strides(coords), H.ptr(ii), H.ptr(jj), int(radius), H.ptr(out), H.stream_of(fmap1)))
+    return out
+
+
+def backward(fmap1, fmap2, coords, ii, jj, grad, radius):
+    """correlation.cpp:37-45 / correlation_kernel.cu:236-286 -> [fmap1_grad, fmap2_grad]."""
+    _check_corr_args(fmap1, fmap2, coords, ii, jj)
+    g1 = torch.zeros_like(fmap1).contiguous()
+    g2 = torch.zeros_like(fmap2).contiguous()
+    f1, f2, c = fmap1.contiguous(), fmap2.contiguous(), coords.contiguous()
+    grad = grad.float().contiguous()
+    ii, jj = H.idx64(ii), H.idx64(jj)
+    H.check(H.lib().dpvo_corr_backward(
+        H.dtype_code(f1), H.ptr(f1), H.sizes(f1), H.ptr(f2), H.sizes(f2), H.ptr(c), H.sizes(c), H.ptr(ii), H.ptr(jj),
+        H.ptr(grad), int(radius), H.ptr(g1), H.ptr(g2), H.stream_of(f1)))
+    return [g1, g2]
+
+
+def patchify_forward(net, coords, radius):
+    """correlation.cpp:47-50 / correlation_kernel.cu:288-308 -> [patches [B,M,C,D,D]]."""
+    H.on_gpu(net, coords)
+    if coords.dtype != torch.float32:
+        raise RuntimeError("coords must be float32")
+    B, C = net.shape[0], net.shape[1]
+    coords = coords.contiguous()
+    M = coords.shape[1]
+    D = 2 * radius + 2
+    out = torch.empty((B, M, C, D, D), dtype=net.dtype, device=net.device)
+    H.check(H.lib().dpvo_patchify_forward(H.dtype_code(net), H.ptr(net), H.sizes(net), H.strides(net), H.ptr(coords),
+                                          M, int(radius), H.ptr(out), H.stream_of(net)))
+    return [out]
+
+
+def patchify_backward(net, coords, gradient, radius):
+    """correlation.cpp:52-55 / correlation_kernel.cu:310-333 -> [net_gradient]."""
+    H.on_gpu(net, coords, gradient)
+    coords = coords.contiguous()
+    grad = gradient.contiguous()
+    out = torch.zeros(net.shape, dtype=net.dtype, device=net.device)
+    H.check(H.lib().dpvo_patchify_backward(H.dtype_code(net), H.sizes(net), H.ptr(coords), coords.shape[1],
+                                           int(radius), H.ptr(grad), H.ptr(out), H.stream_of(net)))
+    return [out]
