@@ -1,0 +1,397 @@
+"""DPVO tracker (reference dpvo/dpvo.py:22-875), hot path on MI355X.
+
+Public API kept: DPVO(cfg, network, ht, wd, ...), __call__(tstamp, image,
+depth, mask, intrinsics), update(), keyframe(), terminate(),
+terminate_keyframe(), get_pts_clr_intri(), global_bundle_adjustment().
+Visualisation (rerun/viewer), inlier-ratio records, SuperPoint and loop
+closure are out of scope.
+
+MI355X-specific choices (all behind the same API):
+  * the fmap rings are stored channel-last ([pmem, H, W, C], exposed through
+    the reference's [1, pmem, C, H, W] shape) so altcorr streams 256-byte
+    pixel rows; both pyramid levels run in one fused launch;
+  * reproject / point cloud are single fused launches;
+  * fastba.neighbors and BA stay on the device (no host round trip).
+"""
+import torch
+import torch.nn.functional as F
+
+from . import altcorr, fastba
+from . import projective_ops as pops
+from .lietorch import SE3, stack
+from .net import VONet
+from .patchgraph import PatchGraph
+from .utils import Timer, flatmeshgrid
+
+
+def _ring(pmem, C, h, w, channel_last, **kw):
+    if channel_last:
+        return torch.zeros(1, pmem, h, w, C, **kw).permute(0, 1, 4, 2, 3)
+    return torch.zeros(1, pmem, C, h, w, **kw)
+
+
+class DPVO:
+    def __init__(self, cfg, network, ht=480, wd=640, viz=False, path="", nvlad_db=None, rerun=False,
+                 device="cuda"):
+        if viz or rerun:
+            raise NotImplementedError("visualisation is out of scope for the MI355X hot-path build")
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.load_weights(network)
+        self.is_initialized = False
+        self.enable_timing = False
+        self.M = cfg.PATCHES_PER_FRAME
+        self.N = cfg.BUFFER_SIZE
+        self.enable_global_ba = cfg.ENABLE_GLOBAL_BA
+        self.distance_thresh = cfg.DISTANCE_THRESH
+        self.use_distance_edges = cfg.USE_DISTANCE_EDGES
+        self.ht, self.wd = ht, wd
+        self.tlist = []
+        self.counter = 0
+        self.viewer = None
+        self.path = path
+
+        self.pmem = self.mem = 36
+        if self.enable_global_ba:
+            self.pmem = self.N  # every frame's features kept for the global pass
+        dt = torch.half if cfg.MIXED_PRECISION else torch.float
+        self.kwargs = kw = {"device": self.device, "dtype": dt}
+        DIM, P, RES = self.DIM, self.P, self.RES
+        self.imap_ = torch.zeros(self.pmem, self.M, DIM, **kw)
+        self.gmap_ = torch.zeros(self.pmem, self.M, 128, P, P, **kw)
+        self.image_buffer_ = torch.zeros(self.mem, 3, ht, wd, dtype=torch.uint8, device=self.device)
+        h, w = ht // RES, wd // RES
+        cl = getattr(cfg, "CHANNEL_LAST_FMAPS", True)
+        self.fmap1_ = _ring(self.pmem, 128, h, w, cl, **kw)
+        self.fmap2_ = _ring(self.pmem, 128, h // 4, w // 4, cl, **kw)
+        self.pyramid = (self.fmap1_, self.fmap2_)
+        self.pg = PatchGraph(cfg, P, DIM, self.pmem, self.M, h, w, RES, device=self.device, **kw)
+        self.warm_up = 10
+        self._lmbda = torch.as_tensor([1e-4], device=self.device)
+        self._identity = SE3.Identity(1, device=self.device)
+
+    # ------------------------------------------------------------------ state views
+    @property
+    def poses(self):
+        return self.pg.poses_.view(1, self.N, 7)
+
+    @property
+    def patches(self):
+        return self.pg.patches_.view(1, self.N * self.M, 3, 3, 3)
+
+    @property
+    def patches_est(self):
+        return self.pg.patches_est_.view(1, self.N * self.M, 3, 3, 3)
+
+    @property
+    def intrinsics(self):
+        return self.pg.intrinsics_.view(1, self.N, 4)
+
+    @property
+    def ix(self):
+        return self.pg.index_.view(-1)
+
+    @property
+    def imap(self):
+        return self.imap_.view(1, self.pmem * self.M, self.DIM)
+
+    @property
+    def gmap(self):
+        return self.gmap_.view(1, self.pmem * self.M, 128, 3, 3)
+
+    @property
+    def n(self):
+        return self.pg.n
+
+    @n.setter
+    def n(self, v):
+        self.pg.n = v
+
+    @property
+    def m(self):
+        return self.pg.m
+
+    @m.setter
+    def m(self, v):
+        self.pg.m = v
+
+    # ------------------------------------------------------------------ weights
+    def load_weights(self, network):
+        if isinstance(network, str):
+            from collections import OrderedDict
+            state = torch.load(network, map_location="cpu", weights_only=True)
+            clean = OrderedDict((k.replace("module.", ""), v) for k, v in state.items() if "update.lmbda" not in k)
+            self.network = VONet()
+            self.network.load_state_dict(clean)
+        else:
+            self.network = network
+        self.DIM, self.RES, self.P = self.network.DIM, self.network.RES, self.network.P
+        self.network.to(self.device).eval()
+
+    # ------------------------------------------------------------------ outputs
+    def get_pts_clr_intri(self, inlier=False):
+        m = self.pg.m
+        pts = pops.point_cloud_centre(SE3(self.poses), self.patches[:, :m], self.intrinsics, self.ix[:m])
+        points = pts.cpu().numpy()
+        colors = self.pg.colors_.view(-1, 3)[:m].cpu().numpy() * 255.0
+        d = self.pg.patches_[:self.n][..., self.P // 2, self.P // 2]
+        med = d[:, :, 2].median(dim=1).values
+        mask = ((d[:, :, -1] > med[:, None]) & (d[:, :, -1] < 4.0 * med[:, None])).view(-1).cpu().numpy()
+        intrinsic = self.pg.intrinsics_[0].cpu().numpy() * self.RES
+        return points[mask], colors[mask], (intrinsic, self.ht, self.wd)
+
+    def get_pose(self, t):
+        if t in self.traj:
+            return SE3(self.traj[t])
+        t0, dP = self.pg.delta[t]
+        return dP * self.get_pose(t0)
+
+    def terminate(self):
+        if self.enable_global_ba:
+            self.global_bundle_adjustment()
+        self.traj = {self.pg.tstamps_[i].item(): self.pg.poses_[i] for i in range(self.n)}
+        poses = stack([self.get_pose(t) for t in range(self.counter)], dim=0)
+        poses = poses.inv().data.cpu().numpy()
+        return poses, torch.as_tensor(self.tlist, dtype=torch.float64).numpy()
+
+    def terminate_keyframe(self):
+        self.traj = {self.pg.tstamps_[i].item(): self.pg.poses_[i] for i in range(self.n)}
+        poses = stack([SE3(self.pg.poses_[i]) for i in range(self.n)], dim=0).inv().data.cpu().numpy()
+        return poses, torch.as_tensor([self.pg.tstamps_[i] for i in range(self.n)], dtype=torch.float64).numpy()
+
+    # ------------------------------------------------------------------ hot path
+    def corr(self, coords, indicies=None):
+        """2-level local correlation -> [1, E, 882] (dpvo.py:326-333), one fused launch."""
+        ii, jj = indicies if indicies is not None else (self.pg.kk, self.pg.jj)
+        ii1 = ii % (self.M * self.pmem)
+        jj1 = jj % self.pmem
+        return altcorr.corr_pyramid(self.gmap, self.pyramid, coords, ii1, jj1, 3, (1, 4)).view(1, len(ii), -1)
+
+    def reproject(self, indicies=None):
+        """patch kk from frame ii into frame jj -> [1, E, 2, P, P] (dpvo.py:335-339)."""
+        ii, jj, kk = indicies if indicies is not None else (self.pg.ii, self.pg.jj, self.pg.kk)
+        return pops.transform_fused(SE3(self.poses), self.patches, self.intrinsics, ii, jj, kk, chw=True)
+
+    def append_factors(self, kk, jj):
+        self.pg.jj = torch.cat([self.pg.jj, jj])
+        self.pg.kk = torch.cat([self.pg.kk, kk])
+        self.pg.ii = torch.cat([self.pg.ii, self.ix[kk]])
+        self.pg.net = torch.cat([self.pg.net, torch.zeros(1, len(kk), self.DIM, **self.kwargs)], dim=1)
+
+    def remove_factors(self, m, store: bool):
+        assert self.pg.ii.numel() == self.pg.weight.shape[1]
+        if store:
+            self.pg.ii_inac = torch.cat((self.pg.ii_inac, self.pg.ii[m]))
+            self.pg.jj_inac = torch.cat((self.pg.jj_inac, self.pg.jj[m]))
+            self.pg.kk_inac = torch.cat((self.pg.kk_inac, self.pg.kk[m]))
+            self.pg.weight_inac = torch.cat((self.pg.weight_inac, self.pg.weight[:, m]), dim=1)
+            self.pg.target_inac = torch.cat((self.pg.target_inac, self.pg.target[:, m]), dim=1)
+        keep = ~m
+        self.pg.weight = self.pg.weight[:, keep]
+        self.pg.target = self.pg.target[:, keep]
+        self.pg.ii, self.pg.jj, self.pg.kk = self.pg.ii[keep], self.pg.jj[keep], self.pg.kk[keep]
+        self.pg.net = self.pg.net[:, keep]
+
+    def motion_probe(self):
+        """median flow of a trial update on the newest frame (dpvo.py:366-381)."""
+        kk = torch.arange(self.pg.m - self.M, self.pg.m, device=self.device)
+        jj = self.n * torch.ones_like(kk)
+        ii = self.ix[kk]
+        net = torch.zeros(1, len(ii), self.DIM, **self.kwargs)
+        coords = self.reproject(indicies=(ii, jj, kk))
+        with torch.autocast("cuda", enabled=self.cfg.MIXED_PRECISION):
+            corr = self.corr(coords, indicies=(kk, jj))
+            ctx = self.imap[:, kk % (self.M * self.pmem)]
+            net, (delta, weight, _) = self.network.update(net, ctx, corr, None, ii, jj, kk)
+        return torch.quantile(delta.norm(dim=-1).float(), 0.5)
+
+    def motionmag(self, i, j):
+        k = (self.pg.ii == i) & (self.pg.jj == j)
+        flow = pops.flow_mag(SE3(self.poses), self.patches, self.intrinsics, self.pg.ii[k], self.pg.jj[k],
+                             self.pg.kk[k], beta=0.5)
+        return flow.mean().item()
+
+    def update(self):
+        """One keyframe of the hot loop (dpvo.py:711-749)."""
+        with Timer("other", enabled=self.enable_timing):
+            coords = self.reproject()
+            with torch.autocast("cuda", enabled=True):
+                corr = self.corr(coords)
+                ctx = self.imap[:, self.pg.kk % (self.M * self.pmem)]
+                self.pg.net, (delta, weight, _) = self.network.update(self.pg.net, ctx, corr, None, self.pg.ii,
+                                                                      self.pg.jj, self.pg.kk)
+            weight = weight.float()
+            target = coords[..., self.P // 2, self.P // 2] + delta.float()
+        self.pg.target = target
+        self.pg.weight = weight
+        with Timer("BA", enabled=self.enable_timing):
+            t0 = self.n - self.cfg.OPTIMIZATION_WINDOW if self.is_initialized else 1
+            t0 = max(t0, 1)
+            fastba.BA(self.poses, self.patches, self.intrinsics, target, weight, self._lmbda, self.pg.ii, self.pg.jj,
+                      self.pg.kk, t0, self.n, getattr(self.cfg, "BA_ITERATIONS", 2))
+            m = self.pg.m
+            pops.point_cloud_centre(SE3(self.poses), self.patches[:, :m], self.intrinsics, self.ix[:m],
+                                    out=self.pg.points_[:m])
+
+    def keyframe(self):
+        """drop a redundant keyframe, retire old edges (dpvo.py:605-658)."""
+        k = self.n - self.cfg.KEYFRAME_INDEX
+        i, j = k - 1, k + 1
+        m = self.motionmag(i, j) + self.motionmag(j, i)
+        if m / 2 < self.cfg.KEYFRAME_THRESH:
+            t0, t1 = self.pg.tstamps_[k - 1].item(), self.pg.tstamps_[k].item()
+            dP = SE3(self.pg.poses_[k]) * SE3(self.pg.poses_[k - 1]).inv()
+            self.pg.delta[t1] = (t0, dP)
+            self.remove_factors((self.pg.ii == k) | (self.pg.jj == k), store=False)
+            self.pg.kk[self.pg.ii > k] -= self.M
+            self.pg.ii[self.pg.ii > k] -= 1
+            self.pg.jj[self.pg.jj > k] -= 1
+            for f in range(k, self.n - 1):
+                g = f + 1
+                self.pg.tstamps_[f] = self.pg.tstamps_[g]
+                for buf in (self.pg.colors_, self.pg.poses_, self.pg.patches_, self.pg.patches_est_,
+                            self.pg.intrinsics_):
+                    buf[f] = buf[g]
+                self.imap_[f % self.pmem] = self.imap_[g % self.pmem]
+                self.gmap_[f % self.pmem] = self.gmap_[g % self.pmem]
+                self.fmap1_[0, f % self.pmem] = self.fmap1_[0, g % self.pmem]
+                self.fmap2_[0, f % self.pmem] = self.fmap2_[0, g % self.pmem]
+                self.image_buffer_[f % self.mem] = self.image_buffer_[g % self.mem]
+            self.n -= 1
+            self.pg.m -= self.M
+        elif torch.isnan(self.pg.poses_[k]).any():
+            raise Exception("Error: the estimated pose is nan!")
+        self.remove_factors(self.ix[self.pg.kk] < self.n - self.cfg.REMOVAL_WINDOW, store=True)
+
+    # ------------------------------------------------------------------ global BA (C4)
+    def compute_keyframe_distance(self, i, j, beta=0.5):
+        if i >= self.n or j >= self.n:
+            return float("inf")
+        M, d = self.M, self.device
+        fi = lambda a, b: pops.flow_mag(SE3(self.poses), self.patches, self.intrinsics,
+                                        torch.full((M,), a, device=d, dtype=torch.long),
+                                        torch.full((M,), b, device=d, dtype=torch.long),
+                                        torch.arange(M * a, M * (a + 1), device=d), beta=beta)
+        return (0.5 * (fi(i, j).mean() + fi(j, i).mean())).item()
+
+    def get_distance_based_edges(self):
+        if not self.use_distance_edges or self.n < 2:
+            return [], []
+        ii = list(range(self.n - 1))
+        jj = list(range(1, self.n))
+        for i in range(self.n):
+            for j in range(i + 2, self.n):
+                if self.compute_keyframe_distance(i, j) < self.distance_thresh:
+                    ii.append(i)
+                    jj.append(j)
+        return ii, jj
+
+    def global_corr(self, coords, ii, jj, kk):
+        return self.corr(coords, (kk, jj))
+
+    def global_bundle_adjustment(self):
+        """one fastba pass over every keyframe (dpvo.py:436-505)."""
+        if not self.enable_global_ba or self.n < 2:
+            return
+        if self.use_distance_edges:
+            ii_e, jj_e = self.get_distance_based_edges()
+        else:
+            ii_e, jj_e = list(range(self.n - 1)), list(range(1, self.n))
+            for i in range(0, self.n, 5):
+                for j in range(i + 10, min(i + 20, self.n)):
+                    ii_e.append(i)
+                    jj_e.append(j)
+        if not ii_e:
+            return
+        d, M = self.device, self.M
+        ie = torch.as_tensor(ii_e, device=d)
+        je = torch.as_tensor(jj_e, device=d)
+        ii = ie.repeat_interleave(M)
+        jj = je.repeat_interleave(M)
+        kk = (ie[:, None] * M + torch.arange(M, device=d)[None]).reshape(-1)
+        coords = self.reproject((ii, jj, kk))
+        with torch.autocast("cuda", enabled=True):
+            corr = self.global_corr(coords, ii, jj, kk)
+            ctx = self.imap[:, kk]
+            net = torch.zeros(1, len(ii), self.DIM, **self.kwargs)
+            net, (delta, weight, _) = self.network.update(net, ctx, corr, None, ii, jj, kk)
+        target = coords[..., self.P // 2, self.P // 2] + delta.float()
+        try:
+            fastba.BA(self.poses, self.patches, self.intrinsics, target, weight.float(), self._lmbda, ii, jj, kk, 1,
+                      self.n, 2)
+        except Exception as e:  # the reference logs and carries on (dpvo.py:499-501)
+            print(f"Global BA failed: {e}")
+
+    # ------------------------------------------------------------------ ingest
+    def _edges_forw(self):
+        r = self.cfg.PATCH_LIFETIME
+        t0, t1 = self.M * max(self.n - r, 0), self.M * max(self.n - 1, 0)
+        return flatmeshgrid(torch.arange(t0, t1, device=self.device),
+                            torch.arange(self.n - 1, self.n, device=self.device), indexing="ij")
+
+    def _edges_back(self):
+        r = self.cfg.PATCH_LIFETIME
+        t0, t1 = self.M * max(self.n - 1, 0), self.M * max(self.n, 0)
+        return flatmeshgrid(torch.arange(t0, t1, device=self.device),
+                            torch.arange(max(self.n - r, 0), self.n, device=self.device), indexing="ij")
+
+    def __call__(self, tstamp, image, depth, mask, intrinsics):
+        """track one frame (dpvo.py:771-875)."""
+        if self.pg.n + 1 >= self.pg.N:
+            raise Exception(f'The buffer size is too small. You can increase it using "--buffer {self.N * 2}"')
+        with torch.autocast("cuda", enabled=self.cfg.MIXED_PRECISION):
+            fmap, gmap, imap, patches, _, clr = self.network.patchify(
+                image, patches_per_image=self.cfg.PATCHES_PER_FRAME, gradient_bias=self.cfg.GRADIENT_BIAS,
+                return_color=True, mask=mask)
+        n = self.n
+        self.tlist.append(tstamp)
+        self.pg.tstamps_[n] = self.counter
+        self.pg.intrinsics_[n] = intrinsics / self.RES
+        self.pg.colors_[n] = ((clr[0, :, [2, 1, 0]] + 0.5) * (255.0 / 2)).to(torch.uint8)
+        self.pg.index_[n + 1] = n + 1
+        self.pg.index_map_[n + 1] = self.pg.m + self.pg.M
+        if n > 1:
+            if self.cfg.MOTION_MODEL == "DAMPED_LINEAR":
+                P1, P2 = SE3(self.pg.poses_[n - 1]), SE3(self.pg.poses_[n - 2])
+                *_, a, b, c = [1] * 3 + self.tlist
+                xi = self.cfg.MOTION_DAMPING * ((c - b) / (b - a)) * (P1 * P2.inv()).log()
+                self.pg.poses_[n] = (SE3.exp(xi) * P1).data
+            else:
+                self.pg.poses_[n] = self.pg.poses_[n - 1]
+        patches[:, :, 2] = torch.rand_like(patches[:, :, 2, 0, 0, None, None])
+        ref_depth = None
+        if self.is_initialized:
+            if depth is not None and mask is not None:
+                s = torch.median(self.pg.patches_[n - 3:n, :, 2])
+                ref_depth = (1 / s) / torch.median(depth[mask]) * depth
+                patches[:, :, 2] = ref_depth[mask].median()
+            elif depth is not None:
+                ref_depth = depth
+        elif depth is not None:
+            ref_depth = depth
+        self.pg.patches_[n] = patches
+        if ref_depth is not None:
+            self.pg.set_prior_depth(n, ref_depth)
+
+        slot = n % self.pmem
+        self.imap_[slot] = imap.squeeze()
+        self.gmap_[slot] = gmap.squeeze()
+        self.fmap1_[:, slot] = F.avg_pool2d(fmap[0], 1, 1)
+        self.fmap2_[:, slot] = F.avg_pool2d(fmap[0], 4, 4)
+        self.image_buffer_[n % self.mem] = image
+        self.counter += 1
+        if n > 0 and not self.is_initialized:
+            if self.motion_probe() < 2.0:
+                self.pg.delta[self.counter - 1] = (self.counter - 2, self._identity[0])
+                return
+        self.pg.n += 1
+        self.pg.m += self.M
+        self.append_factors(*self._edges_forw())
+        self.append_factors(*self._edges_back())
+        if self.n == self.warm_up and not self.is_initialized:
+            self.is_initialized = True
+            for _ in range(12):
+                self.update()
+        elif self.is_initialized:
+            self.update()
+            self.keyframe()
