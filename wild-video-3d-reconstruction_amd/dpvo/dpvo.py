@@ -65,7 +65,7 @@ class DPVO:
         self.fmap1_ = _ring(self.pmem, 128, h, w, cl, **kw)
         self.fmap2_ = _ring(self.pmem, 128, h // 4, w // 4, cl, **kw)
         self.pyramid = (self.fmap1_, self.fmap2_)
-        self.pg = PatchGraph(cfg, P, DIM, self.pmem, self.M, h, w, RES, device=self.device, **kw)
+        self.pg = PatchGraph(cfg, P, DIM, self.pmem, self.M, h, w, RES, device=self.device, dtype=dt)
         self.warm_up = 10
         self._lmbda = torch.as_tensor([1e-4], device=self.device)
         self._identity = SE3.Identity(1, device=self.device)
