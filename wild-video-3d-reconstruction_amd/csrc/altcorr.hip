@@ -49,152 +49,231 @@ struct CorrFastParams {
 };
 
 __device__ __forceinline__ half2_t as_h2(uint32_t v) { return __builtin_bit_cast(half2_t, v); }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // exact binary16 ops (contraction is off for this file)
 __device__ __forceinline__ half_t hmul(half_t a, half_t b) { return a * b; }
 __device__ __forceinline__ half_t hadd(half_t a, half_t b) { return a + b; }
 
+// Block -> edge map that gives each XCD a contiguous run of edges (blocks
+// b, b+8, ... share an XCD under round-robin dispatch), so consecutive edges --
+// which mostly share a target frame -- reuse that XCD's L2 (speed only).
+__device__ __forceinline__ int xcd_swizzle(int b, int nblk)
+{
+    const int main = nblk & ~7;
+    if (b >= main) return b;
+    return (b & 7) * (main >> 3) + (b >> 3);
+}
+
 template <int NLEV>
-__global__ __launch_bounds__(128 * NLEV) void corr_fast_kernel(CorrFastParams p)
+struct FastThreads {
+    static constexpr int value = NLEV == 2 ? 192 : 128;
+};
+
+// per-level metadata, uniform over the workgroup (kept in LDS so that runtime
+// level / pixel indices never force register arrays to scratch)
+struct LevelMeta {
+    int fy[corr::NP], fx[corr::NP];
+    float xs[corr::NP], ys[corr::NP];
+    int fast, oy, ox, bw, bh, nslots, first_slot, pad;
+};
+
+template <int NLEV, int C8>
+__global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_fast_kernel(CorrFastParams p)
 {
     using namespace corr;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // LDS carve: f1 pairs [C][8] dwords (5 used) | raw tiles [NLEV][NP][BOX*BOX] half
-    uint32_t* f1pk = reinterpret_cast<uint32_t*>(smem);
-    half_t* raw_all = reinterpret_cast<half_t*>(smem + (size_t)p.C * 8 * 4);
+    constexpr int NT = FastThreads<NLEV>::value;
+    constexpr int C = C8 * 8;
+    __shared__ __attribute__((aligned(16))) uint32_t f1pk[C * 8];   // (p0,p1)(p2,p3)(p4,p5)(p6,p7)(p8,0) per channel
+    __shared__ half_t raw[NLEV][NP][BOX * BOX];                      // raw 8x8 tiles (inside the shared box)
+    __shared__ LevelMeta meta[NLEV];
 
-    const int be = blockIdx.x;
-    const int b = be / p.E, e = be - b * p.E;
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int b = bid / p.E, e = bid - b * p.E;
     const int tid = threadIdx.x;
-    const int lev = tid >> 7;
-    const int t = tid & 127;
-    const int C = p.C;
-
     const int ix = (int)p.ii[e];
     const int jx = (int)p.jj[e];
     const bool ix_ok = ix >= 0 && ix < p.N1;
 
-    // ---- patch features -> packed pairs (p0,p1) (p2,p3) (p4,p5) (p6,p7) (p8,0)
-    {
-        const half_t* g = p.gmap + b * p.g_s[0] + (int64_t)ix * p.g_s[1];
-        for (int i = tid; i < C * NPAIR; i += 128 * NLEV) {
-            const int c = i / NPAIR, q = i - c * NPAIR;
-            const int pa = 2 * q, pb = 2 * q + 1;
-            half_t lo = (half_t)0, hi = (half_t)0;
-            if (ix_ok) {
-                lo = g[c * p.g_s[2] + (pa / PS) * p.g_s[3] + (pa % PS) * p.g_s[4]];
-                if (pb < NP) hi = g[c * p.g_s[2] + (pb / PS) * p.g_s[3] + (pb % PS) * p.g_s[4]];
-            }
-            half2_t v = {lo, hi};
-            f1pk[c * 8 + q] = __builtin_bit_cast(uint32_t, v);
+    // ---- per-level floors and shared-box geometry (one thread per level)
+    if (tid < NLEV) {
+        LevelMeta& m = meta[tid];
+        const float sc = p.scale[tid];
+        const float* cb = p.coords + b * p.c_s[0] + (int64_t)e * p.c_s[1];
+        int ymin = 0x7fffffff, ymax = (int)0x80000000u, xmin = 0x7fffffff, xmax = (int)0x80000000u;
+        for (int q = 0; q < NP; q++) {
+            const int64_t o = (q / PS) * p.c_s[3] + (q % PS) * p.c_s[4];
+            const float x = cb[o] / sc, y = cb[p.c_s[2] + o] / sc;
+            m.xs[q] = x; m.ys[q] = y;
+            m.fy[q] = floor_to_int_sat(y);
+            m.fx[q] = floor_to_int_sat(x);
+            ymin = min(ymin, m.fy[q]); ymax = max(ymax, m.fy[q]);
+            xmin = min(xmin, m.fx[q]); xmax = max(xmax, m.fx[q]);
         }
+        m.fast = ((int64_t)ymax - ymin) <= 2 && ((int64_t)xmax - xmin) <= 2;
+        m.oy = wrap_add(ymin, -R);
+        m.ox = wrap_add(xmin, -R);
+        m.bh = m.fast ? (ymax - ymin) + D : D;
+        m.bw = m.fast ? (xmax - xmin) + D : D;
+        m.nslots = m.fast ? m.bh * m.bw : NP * D * D;
     }
-
-    // ---- this level's coordinates (uniform per wave)
-    const float sc = p.scale[lev];
-    const int N2 = p.N2[lev], H2 = p.H2[lev], W2 = p.W2[lev];
-    const bool idx_ok = ix_ok && jx >= 0 && jx < N2;
-    float xs[NP], ys[NP];
-    int fy[NP], fx[NP];
-    int ymin = 0x7fffffff, ymax = (int)0x80000000u, xmin = 0x7fffffff, xmax = (int)0x80000000u;
-    const float* cb = p.coords + b * p.c_s[0] + (int64_t)e * p.c_s[1];
-#pragma unroll
-    for (int q = 0; q < NP; q++) {
-        const int64_t o = (q / PS) * p.c_s[3] + (q % PS) * p.c_s[4];
-        xs[q] = cb[o] / sc;
-        ys[q] = cb[p.c_s[2] + o] / sc;
-        fy[q] = floor_to_int_sat(ys[q]);
-        fx[q] = floor_to_int_sat(xs[q]);
-        ymin = min(ymin, fy[q]); ymax = max(ymax, fy[q]);
-        xmin = min(xmin, fx[q]); xmax = max(xmax, fx[q]);
+    __syncthreads();
+    if (tid == 0) {
+        int acc = 0;
+        for (int l = 0; l < NLEV; l++) { meta[l].first_slot = acc; acc += meta[l].nslots; }
+        meta[0].pad = acc;  // total slots
     }
-    const bool fast = ((int64_t)ymax - ymin) <= 2 && ((int64_t)xmax - xmin) <= 2;
+    __syncthreads();
+    const int total = meta[0].pad;
 
-    const half_t* fm = p.fmap[lev] + b * p.f_s0[lev] + (int64_t)jx * p.f_s1[lev];
-    const int64_t fs3 = p.f_s3[lev], fs4 = p.f_s4[lev];
-    half_t* raw = raw_all + lev * NP * BOX * BOX;
-
-    __syncthreads();  // f1pk complete
-
-    // one pass computes every chain of box pixel u for all nine patch pixels
-    auto run_box = [&](int oy, int ox, int bw, int bh, int only_p) {
-        const int uy = t / bw, ux = t - uy * bw;
-        const bool act = t < bw * bh;
-        const int gy = wrap_add(oy, uy), gx = wrap_add(ox, ux);
-        const bool inb = act && idx_ok && gy >= 0 && gy < H2 && gx >= 0 && gx < W2;
-        half2_t acc[NPAIR];
-#pragma unroll
-        for (int q = 0; q < NPAIR; q++) acc[q] = (half2_t){(half_t)0, (half_t)0};
-        const uint4* wp = reinterpret_cast<const uint4*>(fm + (int64_t)(inb ? gy : 0) * fs3 + (int64_t)(inb ? gx : 0) * fs4);
-        const int C8 = C >> 3;
-        uint4 w = inb ? wp[0] : make_uint4(0, 0, 0, 0);
-        for (int c8 = 0; c8 < C8; c8++) {
-            const uint4 cur = w;
-            if (c8 + 1 < C8) w = inb ? wp[c8 + 1] : make_uint4(0, 0, 0, 0);
-            const uint32_t wd[4] = {cur.x, cur.y, cur.z, cur.w};
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const half2_t wv = as_h2(wd[k]);
-#pragma unroll
-                for (int hsel = 0; hsel < 2; hsel++) {
-                    const int c = c8 * 8 + 2 * k + hsel;
-                    const half_t ws = hsel ? wv.y : wv.x;
-                    const half2_t wb = {ws, ws};
-                    const uint4 f03 = *reinterpret_cast<const uint4*>(f1pk + c * 8);
-                    const uint32_t f4 = f1pk[c * 8 + 4];
-                    acc[0] = acc[0] + wb * as_h2(f03.x);
-                    acc[1] = acc[1] + wb * as_h2(f03.y);
-                    acc[2] = acc[2] + wb * as_h2(f03.z);
-                    acc[3] = acc[3] + wb * as_h2(f03.w);
-                    acc[4] = acc[4] + wb * as_h2(f4);
-                }
-            }
+    // slot -> (level, box pixel).  Every lane gets a valid row pointer (out-of-image
+    // lanes read the frame origin and their chains are zeroed afterwards), so the
+    // loads need no branches.
+    struct Slot { int lev, q_only, u; bool act, inb; const uint4* ptr; };
+    auto decode = [&](int slot) {
+        Slot s{0, -1, 0, false, false, nullptr};
+        s.act = slot < total;
+        const int sl = s.act ? slot : 0;
+        s.lev = (NLEV == 2 && sl >= meta[NLEV - 1].first_slot) ? NLEV - 1 : 0;
+        const LevelMeta& m = meta[s.lev];
+        const int loc = sl - m.first_slot;
+        int gy, gx;
+        if (m.fast) {
+            const int uy = loc / m.bw, ux = loc - uy * m.bw;
+            gy = wrap_add(m.oy, uy); gx = wrap_add(m.ox, ux);
+            s.u = loc;
+        } else {
+            const int q = loc / (D * D), u = loc - q * (D * D);
+            const int uy = u / D, ux = u - uy * D;
+            gy = wrap_add(m.fy[q], uy - R); gx = wrap_add(m.fx[q], ux - R);
+            s.q_only = q;
+            s.u = u;
         }
-        if (act) {
-            // out-of-image positions are exactly +0 in the reference (never accumulated)
-            const half_t z = (half_t)0;
-            const half_t s[NP] = {acc[0].x, acc[0].y, acc[1].x, acc[1].y, acc[2].x,
-                                  acc[2].y, acc[3].x, acc[3].y, acc[4].x};
-            if (only_p < 0) {
-#pragma unroll
-                for (int q = 0; q < NP; q++) raw[q * BOX * BOX + t] = inb ? s[q] : z;
-            } else {
-                half_t v = z;
-#pragma unroll
-                for (int q = 0; q < NP; q++) if (q == only_p) v = s[q];
-                raw[only_p * BOX * BOX + t] = inb ? v : z;
-            }
-        }
+        const int lv = s.lev;
+        s.inb = s.act && ix_ok && jx >= 0 && jx < p.N2[lv] && gy >= 0 && gy < p.H2[lv] && gx >= 0 && gx < p.W2[lv];
+        const half_t* base = p.fmap[lv] + b * p.f_s0[lv];
+        s.ptr = reinterpret_cast<const uint4*>(
+            s.inb ? base + (int64_t)jx * p.f_s1[lv] + (int64_t)gy * p.f_s3[lv] + (int64_t)gx * p.f_s4[lv] : base);
+        return s;
     };
 
-    if (fast) {
-        run_box(wrap_add(ymin, -R), wrap_add(xmin, -R), BOX, BOX, -1);
-    } else {
-        // rare: the nine windows do not share a 10x10 box
-        for (int q = 0; q < NP; q++) run_box(wrap_add(fy[q], -R), wrap_add(fx[q], -R), D, D, q);
+    // ---- the reference's chain, channel 0..C-1, for all nine patch pixels, two per op:
+    //      acc = acc + (W[c], W[c]) * (f1[p][c], f1[p'][c])   (no FMA: exact per-op rounding)
+    // The patch pairs are fetched per 8-channel chunk with inline-asm ds_reads: as
+    // plain loads, LLVM hoists all C x 5 of them to the top and the kernel drops to
+    // 2 waves/SIMD.
+    auto chunk = [&](half2_t (&acc)[NPAIR], const uint4 wq, int k) {
+        lds_u32* fb = (lds_u32*)(f1pk) + k * 64;  // 8 channels x 8 dwords (address-space cast)
+        u32x4 fa[8];
+        uint32_t fc[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[c]) : "v"(fb), "i"(c * 32));
+            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(fc[c]) : "v"(fb), "i"(c * 32 + 16));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t wd[4] = {wq.x, wq.y, wq.z, wq.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const half2_t wv = as_h2(wd[j]);
+#pragma unroll
+            for (int hsel = 0; hsel < 2; hsel++) {
+                const int c = 2 * j + hsel;
+                const half_t ws = hsel ? wv.y : wv.x;
+                const half2_t wb = {ws, ws};
+                acc[0] = acc[0] + wb * as_h2(fa[c].x);
+                acc[1] = acc[1] + wb * as_h2(fa[c].y);
+                acc[2] = acc[2] + wb * as_h2(fa[c].z);
+                acc[3] = acc[3] + wb * as_h2(fa[c].w);
+                acc[4] = acc[4] + wb * as_h2(fc[c]);
+            }
+        }
+        // pin this chunk's arithmetic before the next chunk's (volatile) reads
+#pragma unroll
+        for (int q = 0; q < NPAIR; q++) asm volatile("" : "+v"(acc[q]));
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // first pass: this lane's first four 16-byte chunks are in flight before the
+    // patch-feature repack and the barrier
+    Slot cur = decode(tid);
+    uint4 a0 = cur.ptr[0], a1 = cur.ptr[1], a2 = cur.ptr[2], a3 = cur.ptr[3];
+
+    // ---- patch features -> channel-major packed pairs, one global round trip
+    if (tid < C) {
+        const half_t* g = p.gmap + b * p.g_s[0] + (int64_t)(ix_ok ? ix : 0) * p.g_s[1] + tid * p.g_s[2];
+        half_t v[NP + 1];
+#pragma unroll
+        for (int q = 0; q < NP; q++) v[q] = g[(q / PS) * p.g_s[3] + (q % PS) * p.g_s[4]];
+        v[NP] = (half_t)0;
+        uint32_t d[NPAIR];
+#pragma unroll
+        for (int q = 0; q < NPAIR; q++) d[q] = __builtin_bit_cast(uint32_t, (half2_t){v[2 * q], v[2 * q + 1]});
+        *reinterpret_cast<uint4*>(f1pk + tid * 8) = make_uint4(d[0], d[1], d[2], d[3]);
+        f1pk[tid * 8 + 4] = d[4];
     }
     __syncthreads();
 
-    // ---- bilinear epilogue, exact rounding sequence of correlation_kernel.cu:221-232
-    half_t* ob = p.out + b * p.o_b + (int64_t)e * p.o_e + lev * p.o_l;
-    for (int o = t; o < NP * DO * DO; o += 128) {
-        const int q = o / (DO * DO), r = o - q * (DO * DO);
-        const int a = r / DO, bx = r - a * DO;  // a: y offset, bx: x offset
-        // raw tile of patch pixel q: inside the shared 10x10 box at its floor
-        // offset (fast), or its own 8x8 window (fallback)
-        const int bw = fast ? BOX : D;
-        int oy = 0, ox = 0;
-        if (fast) {
-#pragma unroll
-            for (int k = 0; k < NP; k++)
-                if (k == q) { oy = fy[k] - ymin; ox = fx[k] - xmin; }
+    for (int base = 0; base < total; base += NT) {
+        if (base > 0) {
+            cur = decode(base + tid);
+            a0 = cur.ptr[0]; a1 = cur.ptr[1]; a2 = cur.ptr[2]; a3 = cur.ptr[3];
         }
-        const int base = q * BOX * BOX + (oy + a) * bw + (ox + bx);
-        const half_t c00 = raw[base], c01 = raw[base + 1], c10 = raw[base + bw], c11 = raw[base + bw + 1];
-        float xq = 0.f, yq = 0.f;
+        half2_t acc[NPAIR];
 #pragma unroll
-        for (int k = 0; k < NP; k++)
-            if (k == q) { xq = xs[k]; yq = ys[k]; }
+        for (int q = 0; q < NPAIR; q++) acc[q] = (half2_t){(half_t)0, (half_t)0};
+        // software pipeline: 4 chunks (4 KB per wave) in flight while 4 are consumed
+#pragma unroll 1
+        for (int k = 0; k < C8; k += 8) {
+            const uint4 b0 = cur.ptr[k + 4], b1 = cur.ptr[k + 5], b2 = cur.ptr[k + 6], b3 = cur.ptr[k + 7];
+            chunk(acc, a0, k + 0);
+            chunk(acc, a1, k + 1);
+            chunk(acc, a2, k + 2);
+            chunk(acc, a3, k + 3);
+            if (k + 8 < C8) {
+                a0 = cur.ptr[k + 8]; a1 = cur.ptr[k + 9]; a2 = cur.ptr[k + 10]; a3 = cur.ptr[k + 11];
+            }
+            chunk(acc, b0, k + 4);
+            chunk(acc, b1, k + 5);
+            chunk(acc, b2, k + 6);
+            chunk(acc, b3, k + 7);
+        }
+        if (cur.act) {
+            // out-of-image taps are exactly +0 in the reference (never accumulated)
+            const half_t z = (half_t)0;
+            const half_t sv[NP] = {acc[0].x, acc[0].y, acc[1].x, acc[1].y, acc[2].x,
+                                   acc[2].y, acc[3].x, acc[3].y, acc[4].x};
+            if (cur.q_only < 0) {
+#pragma unroll
+                for (int q = 0; q < NP; q++) raw[cur.lev][q][cur.u] = cur.inb ? sv[q] : z;
+            } else {
+                half_t v = z;
+#pragma unroll
+                for (int q = 0; q < NP; q++) if (q == cur.q_only) v = sv[q];
+                raw[cur.lev][cur.q_only][cur.u] = cur.inb ? v : z;
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- bilinear epilogue, exact rounding sequence of correlation_kernel.cu:221-232,
+    // outputs enumerated in the stacked layout's memory order (x, y, pixel, level)
+    half_t* ob = p.out + b * p.o_b + (int64_t)e * p.o_e;
+    for (int o = tid; o < NLEV * NP * DO * DO; o += NT) {
+        const int lev = o % NLEV;
+        int r = o / NLEV;
+        const int q = r % NP; r /= NP;
+        const int a = r % DO;
+        const int bx = r / DO;
+        const LevelMeta& m = meta[lev];
+        const int bw = m.fast ? m.bw : D;
+        const int oy = m.fast ? m.fy[q] - (int)wrap_add(m.oy, R) : 0;
+        const int ox = m.fast ? m.fx[q] - (int)wrap_add(m.ox, R) : 0;
+        const half_t* t = &raw[lev][q][(oy + a) * bw + (ox + bx)];
+        const half_t c00 = t[0], c01 = t[1], c10 = t[bw], c11 = t[bw + 1];
+        const float xq = m.xs[q], yq = m.ys[q];
         const half_t dx = (half_t)(xq - floorf(xq));
         const half_t dy = (half_t)(yq - floorf(yq));
         const half_t one = (half_t)1.0f;
@@ -203,7 +282,7 @@ __global__ __launch_bounds__(128 * NLEV) void corr_fast_kernel(CorrFastParams p)
         v = hadd(v, hmul(hmul(dx, omdy), c01));
         v = hadd(v, hmul(hmul(omdx, dy), c10));
         v = hadd(v, hmul(hmul(dx, dy), c11));
-        ob[bx * p.o_x + a * p.o_y + q * p.o_p] = v;
+        ob[bx * p.o_x + a * p.o_y + q * p.o_p + lev * p.o_l] = v;
     }
 }
 
@@ -390,7 +469,7 @@ bool fast_path_ok(int dtype, const int64_t* gsz, const int64_t* fsz, const int64
 {
     if (dtype != DPVO_F16 || radius != corr::R) return false;
     if (gsz[3] != corr::PS || gsz[4] != corr::PS || csz[3] != corr::PS || csz[4] != corr::PS) return false;
-    if (gsz[2] % 8 != 0 || gsz[2] > 512 || fsz[2] != gsz[2]) return false;
+    if (gsz[2] != 128 || fsz[2] != gsz[2]) return false;
     if (fst[2] != 1) return false;  // channel-last storage
     if (fst[0] % 8 || fst[1] % 8 || fst[3] % 8 || fst[4] % 8) return false;  // 16-byte aligned pixels
     return true;
@@ -427,11 +506,10 @@ int launch_fast(int nlev, const void* gmap, const int64_t* gsz, const int64_t* g
     p.o_b = ostr[0]; p.o_e = ostr[1]; p.o_l = ostr[2]; p.o_x = ostr[3]; p.o_y = ostr[4]; p.o_p = ostr[5];
     const int64_t nblk = (int64_t)p.B * p.E;
     if (nblk == 0) return 0;
-    const size_t lds = (size_t)p.C * 8 * 4 + (size_t)nlev * corr::NP * corr::BOX * corr::BOX * sizeof(half_t);
     if (nlev == 2)
-        hipLaunchKernelGGL(corr_fast_kernel<2>, dim3((unsigned)nblk), dim3(256), lds, stream, p);
+        hipLaunchKernelGGL((corr_fast_kernel<2, 16>), dim3((unsigned)nblk), dim3(FastThreads<2>::value), 0, stream, p);
     else
-        hipLaunchKernelGGL(corr_fast_kernel<1>, dim3((unsigned)nblk), dim3(128), lds, stream, p);
+        hipLaunchKernelGGL((corr_fast_kernel<1, 16>), dim3((unsigned)nblk), dim3(FastThreads<1>::value), 0, stream, p);
     return 0;
 }
 
