@@ -155,6 +155,36 @@ int dpvo_transform(const float* poses, const float* patches, int P, const float*
 int dpvo_point_cloud(const float* poses, const float* patches, int P, const float* intrinsics, const int64_t* ix,
                      int64_t m, int centre_only, float* out, void* stream);
 
+/* ------------------------------------------------------------------------
+ * update-operator glue -- replaces torch_scatter 2.1.2 (scatter_softmax +
+ * scatter_sum in SoftAgg, reference dpvo/blocks.py:40-48) and the masked
+ * neighbour gather of Update.forward (dpvo/net.py:81-86).  Not part of the
+ * reference's FFI (torch_scatter is a pip dependency); the dpvo/blocks.py
+ * and dpvo/net.py mirrors call them through dpvo_hot.
+ * --------------------------------------------------------------------- */
+
+/* SoftAgg core: for every group g in [0,G) and channel d < D
+ *   y[g][d] = sum_{e: group[e]==g} f[e][d] * w[e][d],
+ *   w[e][d] = exp(s[e][d] - max_g s[.][d]) / (sum_g exp(s[.][d] - max) + eps)
+ * (torch_scatter.scatter_softmax then scatter_sum over dim 1), accumulated
+ * in fp32 over each group's edges in ascending edge order (deterministic for
+ * groups of up to DPVO_SOFTAGG_SORT_CAP edges; larger groups use arrival
+ * order).  f rows at f + e*ldf, s rows at s + e*lds (so one fused [E][2D]
+ * GEMM output can feed both); y contiguous [G][D] of `dtype`.  Group labels
+ * are torch.unique's inverse, in [0,G); edges with labels outside are
+ * ignored; an empty group yields 0. */
+#define DPVO_SOFTAGG_SORT_CAP 1024
+size_t dpvo_softagg_workspace_bytes(int64_t num_edges, int64_t groups);
+int dpvo_softagg_forward(int dtype, const void* f, int64_t ldf, const void* s, int64_t lds, const int64_t* group,
+                         int64_t num_edges, int D, int64_t groups, float eps, void* y, void* workspace,
+                         size_t workspace_bytes, void* stream);
+
+/* out[e][:] = idx[e] >= 0 ? x[idx[e]][:] : 0, converting in_dtype -> out_dtype
+ * (the mask_ix * net[:, ix] of net.py:82-85; x rows at x + r*ldx, out
+ * contiguous [n][D]). */
+int dpvo_gather_rows(int in_dtype, const void* x, int64_t ldx, int64_t rows, const int64_t* idx, int64_t n, int D,
+                     int out_dtype, void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

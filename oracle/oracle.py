@@ -209,3 +209,37 @@ def point_cloud_centre(poses, patches, intrinsics, ix):
     lib().oracle_point_cloud_centre(_p(poses), _p(patches), _p(intr), _p(ix), ctypes.c_int64(len(ix)),
                                     ctypes.c_int(P), _p(out))
     return out
+
+
+def softagg(f, s, group, groups, eps=1e-12):
+    """SoftAgg's grouped softmax-weighted sum (reference dpvo/blocks.py:40-48,
+    torch_scatter 2.1.2 ``scatter_softmax`` + ``scatter_sum`` over dim 1),
+    in float64: w = exp(s - max_g s) / (sum_g exp(s - max_g s) + eps);
+    y[g] = sum_{e in g} f[e] * w[e].  f, s: [E, D]; group: [E] in [0, groups).
+    torch_scatter is not under /root/reference: restated from its published
+    scatter_softmax (max-recentred, eps added to the group sum) -- parity
+    unpinned by reference fixtures."""
+    f = np.asarray(f, np.float64)
+    s = np.asarray(s, np.float64)
+    group = np.asarray(group, np.int64)
+    D = f.shape[1]
+    gmax = np.full((groups, D), -np.inf)
+    np.maximum.at(gmax, group, s)
+    ex = np.exp(s - gmax[group])
+    den = np.zeros((groups, D))
+    np.add.at(den, group, ex)
+    w = ex / (den + eps)[group]
+    y = np.zeros((groups, D))
+    np.add.at(y, group, f * w)
+    return y
+
+
+def gather_rows(x, idx):
+    """mask_ix * net[:, ix] of Update.forward (reference dpvo/net.py:82-85):
+    rows of x at idx, zero where idx < 0."""
+    x = np.asarray(x)
+    idx = np.asarray(idx, np.int64)
+    out = np.zeros((len(idx), x.shape[1]), x.dtype)
+    ok = idx >= 0
+    out[ok] = x[idx[ok]]
+    return out

@@ -169,3 +169,18 @@ def test_patchify_matches_direct_gather():
                     i, j = y + a - 1, x + c - 1
                     exp = net[b, :, i, j] if (0 <= i < 7 and 0 <= j < 9) else 0
                     np.testing.assert_array_equal(out[b, m, :, a, c], exp)
+
+
+def test_softagg_oracle_matches_torch_scatter_composition():
+    """oracle.softagg vs the scatter_softmax/scatter_sum composition of the
+    dpvo.blocks mirror run on CPU torch (both restate torch_scatter 2.1.2)."""
+    import torch
+    from dpvo.blocks import scatter_softmax, scatter_sum
+    g = torch.Generator().manual_seed(0)
+    E, G, D = 700, 23, 16
+    f = torch.randn(1, E, D, generator=g, dtype=torch.float64)
+    s = torch.randn(1, E, D, generator=g, dtype=torch.float64) * 4
+    lab = torch.randint(0, G, (E,), generator=g)
+    want = scatter_sum(f * scatter_softmax(s, lab, 1, G), lab, 1, G)[0].numpy()
+    got = oracle.softagg(f[0].numpy(), s[0].numpy(), lab.numpy(), G)
+    np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)

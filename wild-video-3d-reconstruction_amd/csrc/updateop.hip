@@ -1,0 +1,279 @@
+// updateop.hip -- native glue of the learned update operator (gfx950).
+//
+// SoftAgg (reference dpvo/blocks.py:40-48) aggregates edge features over
+// groups of edges sharing a key with torch_scatter 2.1.2's scatter_softmax +
+// scatter_sum.  torch_scatter is absent on ROCm and ATen's scatter_reduce
+// "amax" path is a same-address atomic storm (~2.4 ms per call at C3), so the
+// whole softmax-weighted sum is one streaming pass here:
+//
+//   1. CSR of the group labels: count (atomics on G counters), one-block
+//      exclusive scan, fill (atomic cursor per group);
+//   2. one wave64 per (group, 128-channel slice): the wave sorts its edge
+//      list in LDS (ascending edge index -> deterministic fp32 sums), then
+//      streams the f/s rows 8 edges at a time with a batched online softmax
+//      (one rescale per 8 edges), and writes y = acc / (l + eps).
+//
+// Bytes per edge: 2 rows x D x sizeof(T) read once (+12 B of CSR traffic);
+// the kernel is HBM-bound like the GEMMs around it.
+#include "common.hpp"
+
+namespace dpvo {
+namespace {
+
+constexpr int SA_WAVES = 4;          // waves per block in the reduce kernel
+constexpr int SA_UNROLL = 8;         // edges in flight per online-softmax step
+constexpr int SA_CAP = DPVO_SOFTAGG_SORT_CAP;
+
+struct SaLayout {
+    int64_t count, offs, cursor, perm, total;
+};
+
+inline int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
+
+SaLayout sa_layout(int64_t E, int64_t G)
+{
+    SaLayout L;
+    int64_t o = 0;
+    L.count = o;  o += align256(4 * G);
+    L.offs = o;   o += align256(4 * (G + 1));
+    L.cursor = o; o += align256(4 * G);
+    L.perm = o;   o += align256(4 * E);
+    L.total = o;
+    return L;
+}
+
+__global__ __launch_bounds__(256) void sa_count_kernel(const int64_t* __restrict__ group, int64_t E, int64_t G,
+                                                       int* __restrict__ count)
+{
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t g = group[e];
+        if (g >= 0 && g < G) atomicAdd(&count[g], 1);
+    }
+}
+
+// exclusive scan of count[0..G) -> offs[0..G], cursor = offs (single block)
+__global__ __launch_bounds__(1024) void sa_scan_kernel(const int* __restrict__ count, int64_t G,
+                                                       int* __restrict__ offs, int* __restrict__ cursor)
+{
+    __shared__ int part[1024];
+    const int tid = threadIdx.x;
+    const int64_t per = (G + 1023) / 1024;
+    const int64_t g0 = tid * per, g1 = min(G, g0 + per);
+    int sum = 0;
+    for (int64_t g = g0; g < g1; g++) sum += count[g];
+    part[tid] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const int add = tid >= off ? part[tid - off] : 0;
+        __syncthreads();
+        part[tid] += add;
+        __syncthreads();
+    }
+    int base = part[tid] - sum;
+    for (int64_t g = g0; g < g1; g++) {
+        offs[g] = base;
+        cursor[g] = base;
+        base += count[g];
+    }
+    if (tid == 1023) offs[G] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void sa_fill_kernel(const int64_t* __restrict__ group, int64_t E, int64_t G,
+                                                      int* __restrict__ cursor, int* __restrict__ perm)
+{
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t g = group[e];
+        if (g < 0 || g >= G) continue;
+        perm[atomicAdd(&cursor[g], 1)] = (int)e;
+    }
+}
+
+template <typename T> struct Pair;
+template <> struct Pair<half_t> {
+    typedef half2_t V;
+    static __device__ __forceinline__ float2_t load(const half_t* p) { V v = *(const V*)p; return {(float)v.x, (float)v.y}; }
+    static __device__ __forceinline__ void store(half_t* p, float2_t v) { *(V*)p = V{(half_t)v.x, (half_t)v.y}; }
+};
+template <> struct Pair<float> {
+    static __device__ __forceinline__ float2_t load(const float* p) { return *(const float2_t*)p; }
+    static __device__ __forceinline__ void store(float* p, float2_t v) { *(float2_t*)p = v; }
+};
+template <> struct Pair<double> {
+    static __device__ __forceinline__ float2_t load(const double* p) { return {(float)p[0], (float)p[1]}; }
+    static __device__ __forceinline__ void store(double* p, float2_t v) { p[0] = v.x; p[1] = v.y; }
+};
+
+// One wave per (group, 128-channel slice).  Lane owns channels c, c+1.
+template <typename T>
+__global__ __launch_bounds__(64 * SA_WAVES) void sa_reduce_kernel(const T* __restrict__ f, int64_t ldf,
+                                                                  const T* __restrict__ s, int64_t lds,
+                                                                  const int* __restrict__ offs,
+                                                                  const int* __restrict__ perm, int64_t G, int D,
+                                                                  int slices, float eps, T* __restrict__ y)
+{
+    __shared__ int lst[SA_WAVES][2][SA_CAP];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t task = (int64_t)blockIdx.x * SA_WAVES + w;
+    if (task >= G * slices) return;
+    const int64_t g = task / slices;
+    const int c = (int)(task % slices) * 128 + 2 * lane;
+    const int b = offs[g], S = offs[g + 1] - b;
+
+    // ascending edge order within the group (ranks of distinct edge ids)
+    const int* order = perm + b;
+    if (S <= SA_CAP) {
+        int* raw = lst[w][0];
+        int* srt = lst[w][1];
+        for (int i = lane; i < S; i += 64) raw[i] = perm[b + i];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        for (int i = lane; i < S; i += 64) {
+            const int v = raw[i];
+            int r = 0;
+            for (int j = 0; j < S; j++) r += raw[j] < v;
+            srt[r] = v;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        order = srt;
+    }
+    const bool act = c < D;
+    const int cc = act ? c : 0;
+
+    float2_t m = {-INFINITY, -INFINITY}, l = {0.f, 0.f}, acc = {0.f, 0.f};
+    for (int i0 = 0; i0 < S; i0 += SA_UNROLL) {
+        float2_t sv[SA_UNROLL], fv[SA_UNROLL];
+#pragma unroll
+        for (int u = 0; u < SA_UNROLL; u++) {
+            const int i = min(i0 + u, S - 1);
+            const int64_t e = order[i];
+            sv[u] = Pair<T>::load(s + e * lds + cc);
+            fv[u] = Pair<T>::load(f + e * ldf + cc);
+        }
+        float2_t mb = m;
+#pragma unroll
+        for (int u = 0; u < SA_UNROLL; u++) {
+            if (i0 + u < S) {
+                mb.x = fmaxf(mb.x, sv[u].x);
+                mb.y = fmaxf(mb.y, sv[u].y);
+            }
+        }
+        // rescale the running sums once per batch (exp(-inf) = 0 on the first)
+        const float ax = __expf(m.x - mb.x), ay = __expf(m.y - mb.y);
+        l.x *= ax; l.y *= ay; acc.x *= ax; acc.y *= ay;
+#pragma unroll
+        for (int u = 0; u < SA_UNROLL; u++) {
+            if (i0 + u < S) {
+                const float px = __expf(sv[u].x - mb.x), py = __expf(sv[u].y - mb.y);
+                l.x += px; l.y += py;
+                acc.x += px * fv[u].x; acc.y += py * fv[u].y;
+            }
+        }
+        m = mb;
+    }
+    if (act) Pair<T>::store(y + g * (int64_t)D + c, float2_t{acc.x / (l.x + eps), acc.y / (l.y + eps)});
+}
+
+template <typename TI, typename TO>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const TI* __restrict__ x, int64_t ldx, int64_t rows,
+                                                          const int64_t* __restrict__ idx, int64_t n, int D,
+                                                          TO* __restrict__ out)
+{
+    // one wave per output row, 2 channels per lane per step
+    const int lane = threadIdx.x & 63;
+    for (int64_t r = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; r < n;
+         r += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int64_t src = idx[r];
+        const bool ok = src >= 0 && src < rows;
+        for (int c = 2 * lane; c < D; c += 128) {
+            float2_t v = {0.f, 0.f};
+            if (ok) v = Pair<TI>::load(x + src * ldx + c);
+            Pair<TO>::store(out + r * (int64_t)D + c, v);
+        }
+    }
+}
+
+template <typename TI>
+int gather_dispatch_out(const TI* x, int64_t ldx, int64_t rows, const int64_t* idx, int64_t n, int D, int out_dtype,
+                        void* out, hipStream_t s)
+{
+    const unsigned grid = grid_for(n * 64, 256, 8192);
+    switch (out_dtype) {
+    case DPVO_F16: hipLaunchKernelGGL((gather_rows_kernel<TI, half_t>), dim3(grid), dim3(256), 0, s, x, ldx, rows, idx, n, D, (half_t*)out); break;
+    case DPVO_F32: hipLaunchKernelGGL((gather_rows_kernel<TI, float>), dim3(grid), dim3(256), 0, s, x, ldx, rows, idx, n, D, (float*)out); break;
+    case DPVO_F64: hipLaunchKernelGGL((gather_rows_kernel<TI, double>), dim3(grid), dim3(256), 0, s, x, ldx, rows, idx, n, D, (double*)out); break;
+    default: return -1;
+    }
+    return 0;
+}
+
+}  // namespace
+}  // namespace dpvo
+
+using namespace dpvo;
+
+extern "C" size_t dpvo_softagg_workspace_bytes(int64_t num_edges, int64_t groups)
+{
+    return (size_t)sa_layout(num_edges < 0 ? 0 : num_edges, groups < 0 ? 0 : groups).total + 256;
+}
+
+extern "C" int dpvo_softagg_forward(int dtype, const void* f, int64_t ldf, const void* s, int64_t lds,
+                                    const int64_t* group, int64_t num_edges, int D, int64_t groups, float eps,
+                                    void* y, void* workspace, size_t workspace_bytes, void* stream)
+{
+    DPVO_CHECK_ARG(D > 0 && D % 2 == 0, "feature dim must be even and positive");
+    DPVO_CHECK_ARG(num_edges >= 0 && groups >= 0 && num_edges < (int64_t(1) << 31), "bad sizes");
+    DPVO_CHECK_ARG(ldf >= D && lds >= D && ldf % 2 == 0 && lds % 2 == 0, "row strides must be even and >= D");
+    DPVO_CHECK_ARG(dtype == DPVO_F16 || dtype == DPVO_F32 || dtype == DPVO_F64, "unsupported dtype");
+    if (groups == 0) return 0;
+    DPVO_CHECK_ARG(num_edges > 0, "groups without edges");
+    const SaLayout L = sa_layout(num_edges, groups);
+    DPVO_CHECK_ARG(workspace != nullptr && workspace_bytes >= (size_t)L.total + 256, "workspace too small");
+    hipStream_t st = as_stream(stream);
+    char* ws = (char*)(((uintptr_t)workspace + 255) & ~uintptr_t(255));
+    int* count = (int*)(ws + L.count);
+    int* offs = (int*)(ws + L.offs);
+    int* cursor = (int*)(ws + L.cursor);
+    int* perm = (int*)(ws + L.perm);
+    DPVO_CHECK_HIP(hipMemsetAsync(count, 0, 4 * groups, st));
+    const unsigned gE = grid_for(num_edges, 256, 4096);
+    hipLaunchKernelGGL(sa_count_kernel, dim3(gE), dim3(256), 0, st, group, num_edges, groups, count);
+    hipLaunchKernelGGL(sa_scan_kernel, dim3(1), dim3(1024), 0, st, count, groups, offs, cursor);
+    hipLaunchKernelGGL(sa_fill_kernel, dim3(gE), dim3(256), 0, st, group, num_edges, groups, cursor, perm);
+    const int slices = (D + 127) / 128;
+    const unsigned gR = (unsigned)((groups * slices + SA_WAVES - 1) / SA_WAVES);
+    switch (dtype) {
+    case DPVO_F16:
+        hipLaunchKernelGGL(sa_reduce_kernel<half_t>, dim3(gR), dim3(64 * SA_WAVES), 0, st, (const half_t*)f, ldf,
+                           (const half_t*)s, lds, offs, perm, groups, D, slices, eps, (half_t*)y);
+        break;
+    case DPVO_F32:
+        hipLaunchKernelGGL(sa_reduce_kernel<float>, dim3(gR), dim3(64 * SA_WAVES), 0, st, (const float*)f, ldf,
+                           (const float*)s, lds, offs, perm, groups, D, slices, eps, (float*)y);
+        break;
+    default:
+        hipLaunchKernelGGL(sa_reduce_kernel<double>, dim3(gR), dim3(64 * SA_WAVES), 0, st, (const double*)f, ldf,
+                           (const double*)s, lds, offs, perm, groups, D, slices, eps, (double*)y);
+    }
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_gather_rows(int in_dtype, const void* x, int64_t ldx, int64_t rows, const int64_t* idx, int64_t n,
+                                int D, int out_dtype, void* out, void* stream)
+{
+    DPVO_CHECK_ARG(D > 0 && D % 2 == 0 && ldx >= D && ldx % 2 == 0, "feature dim / row stride must be even");
+    DPVO_CHECK_ARG(n >= 0 && rows >= 0, "bad sizes");
+    if (n == 0) return 0;
+    hipStream_t s = as_stream(stream);
+    int rc;
+    switch (in_dtype) {
+    case DPVO_F16: rc = gather_dispatch_out((const half_t*)x, ldx, rows, idx, n, D, out_dtype, out, s); break;
+    case DPVO_F32: rc = gather_dispatch_out((const float*)x, ldx, rows, idx, n, D, out_dtype, out, s); break;
+    case DPVO_F64: rc = gather_dispatch_out((const double*)x, ldx, rows, idx, n, D, out_dtype, out, s); break;
+    default: rc = -1;
+    }
+    DPVO_CHECK_ARG(rc == 0, "unsupported dtype");
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}

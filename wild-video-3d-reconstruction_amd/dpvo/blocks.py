@@ -1,11 +1,17 @@
 """Update-operator building blocks (reference dpvo/blocks.py:15-118).
 
 SoftAgg's grouped softmax/sum used torch-scatter 2.1.2 in the reference
-(absent on ROCm wheels); here it is restated with native scatter_reduce /
-index_add (same eps and max-recentering as torch_scatter.scatter_softmax).
+(absent on ROCm wheels).  Inference runs it as one HIP pass
+(update_ops.softagg, csrc/updateop.hip) over a single fused f|g GEMM; with
+autograd on (training) it falls back to the torch composition below (native
+scatter_reduce / index_add, same eps and max-recentring as
+torch_scatter.scatter_softmax).
 """
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
+
+import update_ops
 
 
 def scatter_sum(src, index, dim, dim_size):
@@ -44,12 +50,28 @@ class SoftAgg(nn.Module):
         self.f = nn.Linear(dim, dim)
         self.g = nn.Linear(dim, dim)
         self.h = nn.Linear(dim, dim)
+        self._fg = None
+
+    def _fused_fg(self):
+        """[f; g] weights for one [E, 2D] GEMM, rebuilt when either changes."""
+        key = tuple((p.data_ptr(), p._version) for p in (self.f.weight, self.f.bias, self.g.weight, self.g.bias))
+        if self._fg is None or self._fg[0] != key:
+            w = torch.cat([self.f.weight, self.g.weight], 0)
+            b = torch.cat([self.f.bias, self.g.bias], 0)
+            self._fg = (key, w, b)
+        return self._fg[1], self._fg[2]
 
     def forward(self, x, ix):
-        _, jx = torch.unique(ix, return_inverse=True)
-        groups = int(jx.max()) + 1 if jx.numel() else 0
-        w = scatter_softmax(self.g(x), jx, 1, groups)
-        y = scatter_sum(self.f(x) * w, jx, 1, groups)
+        uniq, jx = torch.unique(ix, return_inverse=True)
+        groups = uniq.numel()
+        if torch.is_grad_enabled() and x.requires_grad:
+            w = scatter_softmax(self.g(x), jx, 1, groups)
+            y = scatter_sum(self.f(x) * w, jx, 1, groups)
+        else:
+            w, b = self._fused_fg()
+            fg = F.linear(x[0], w, b)
+            D = self.dim
+            y = update_ops.softagg(fg[:, :D], fg[:, D:], jx, groups)[None]
         return self.h(y)[:, jx] if self.expand else self.h(y)
 
 

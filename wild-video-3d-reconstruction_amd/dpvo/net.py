@@ -9,6 +9,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+import update_ops
+
 from . import altcorr, fastba
 from .blocks import GatedResidual, GradientClip, SoftAgg
 from .extractor import BasicEncoder4
@@ -36,14 +38,23 @@ class Update(nn.Module):
         """edge hidden state -> (new state, (delta, weight, None)) (net.py:75-93)."""
         net = self.norm(net + inp + self.corr(corr))
         ix, jx = fastba.neighbors(kk, jj)  # temporal neighbours of the same patch, on the device
-        m_ix = (ix >= 0).to(net.dtype).view(1, -1, 1)
-        m_jx = (jx >= 0).to(net.dtype).view(1, -1, 1)
-        net = net + self.c1(m_ix * net[:, ix])
-        net = net + self.c2(m_jx * net[:, jx])
+        net = net + self.c1(self._neighbour(net, ix))
+        net = net + self.c2(self._neighbour(net, jx))
         net = net + self.agg_kk(net, kk)
         net = net + self.agg_ij(net, ii * 12345 + jj)
         net = self.gru(net)
         return net, (self.d(net), self.w(net), None)
+
+
+    @staticmethod
+    def _neighbour(net, ix):
+        """mask_ix * net[:, ix] (net.py:82-85).  Inference: one native gather
+        that writes zeros for ix < 0 and casts straight to the autocast dtype
+        the following Linear would cast to anyway."""
+        if torch.is_grad_enabled() and net.requires_grad:
+            return (ix >= 0).to(net.dtype).view(1, -1, 1) * net[:, ix]
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else net.dtype
+        return update_ops.gather_rows(net[0], ix, dtype=dt)[None]
 
 
 class Patchifier(nn.Module):
