@@ -173,3 +173,21 @@ def test_corr_backward_matches_autograd_reference():
     s = (grad * out).sum().double()
     assert torch.allclose((g1 * g32.detach()).sum().double(), s, rtol=1e-3)
     assert torch.allclose((g2 * f32.detach()).sum().double(), s, rtol=1e-3)
+
+
+def test_nan_coordinates_follow_reference_conversion():
+    """NaN coords: (int)floor(NaN) is 0 on the reference's GPU (cvt.rzi.s32), the
+    bilinear weights are NaN; compare with NaN == NaN (payload bits may differ)."""
+    import cuda_corr
+    d = dev()
+    gmap, f1, f2, ii, jj, coords = dpvo_sized_inputs(6, E=128, edge_cases=False)
+    coords[0, :4] = float("nan")                 # whole edges
+    coords[0, 4:8, 0, 1, 1] = float("nan")       # one patch pixel's x
+    coords[0, 8:12, 1, 0, 2] = float("inf")      # +inf y
+    out = cuda_corr.forward_pyramid(gmap.to(d), [channel_last(f1.to(d)), channel_last(f2.to(d))], coords.to(d),
+                                    ii.to(d), jj.to(d), 3, [1, 4]).cpu().float().numpy()
+    ref = oracle.corr_pyramid(gmap.numpy(), [f1.numpy(), f2.numpy()], coords.numpy(), ii.numpy(),
+                              jj.numpy()).astype(np.float32)
+    assert np.array_equal(np.isnan(out), np.isnan(ref))
+    ok = ~np.isnan(ref)
+    assert np.array_equal(out[ok], ref[ok])
