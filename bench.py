@@ -66,6 +66,27 @@ def barrier(world):
         dist.barrier()
 
 
+def max_over_ranks(value, device):
+    """The timed region's wall time: MAX over ranks (the slowest sequence)."""
+    import torch.distributed as dist
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_to_rank0(tensors, rank, world):
+    """gather every rank's result tensors (same shapes on all ranks: one
+    sequence per rank) to rank 0; returns [tensor][rank] there."""
+    import torch.distributed as dist
+    out = []
+    for t in tensors:
+        t = t.contiguous()
+        bufs = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+        dist.gather(t, bufs, dst=0)
+        out.append(bufs)
+    return out if rank == 0 else None
+
+
 class CorrProbe:
     """HIP events around every fused-altcorr launch, on the stream it runs on."""
 
@@ -195,19 +216,11 @@ def main():
 
     gather_ms = None
     if world > 1:
-        import torch.distributed as dist
-        t = torch.tensor([elapsed], device=slam.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = max_over_ranks(elapsed, slam.device)
         # result gather (C5): poses and point cloud of every sequence to rank 0, over RCCL
         torch.cuda.synchronize()
         tg = time.perf_counter()
-        pts = slam.pg.points_[:slam.pg.m].contiguous()
-        poses = slam.pg.poses_[:slam.n].contiguous()
-        out_p = [torch.empty_like(pts) for _ in range(world)] if rank == 0 else None
-        out_q = [torch.empty_like(poses) for _ in range(world)] if rank == 0 else None
-        dist.gather(pts, out_p, dst=0)
-        dist.gather(poses, out_q, dst=0)
+        gather_to_rank0([slam.pg.points_[:slam.pg.m], slam.pg.poses_[:slam.n]], rank, world)
         torch.cuda.synchronize()
         gather_ms = round((time.perf_counter() - tg) * 1e3, 3)
 
