@@ -66,6 +66,15 @@ int dpvo_corr_forward_pyramid(int dtype, const void* gmap, const int64_t* gmap_s
                               const float* coords, const int64_t* coords_size, const int64_t* coords_stride,
                               const int64_t* ii, const int64_t* jj, int radius, void* corr, void* stream);
 
+/* Same, with consecutive edges `edge_stride` elements apart (0 = packed), so
+ * the update operator's first Linear can read 16-byte aligned rows
+ * (882 features padded to 896; pad columns are left untouched). */
+int dpvo_corr_forward_pyramid_ld(int dtype, const void* gmap, const int64_t* gmap_size, const int64_t* gmap_stride,
+                                 int nlev, const void* const* fmaps, const int64_t* fmap_sizes,
+                                 const int64_t* fmap_strides, const float* level_scale, const float* coords,
+                                 const int64_t* coords_size, const int64_t* coords_stride, const int64_t* ii,
+                                 const int64_t* jj, int radius, void* corr, int64_t edge_stride, void* stream);
+
 /* cuda_corr.backward (correlation_kernel.cu:236-286): grad is the returned
  * (permuted) view's gradient given as contiguous [B][E][2r+1 (x)][2r+1 (y)][P][P]
  * float; gmap_grad / fmap_grad (contiguous, dtype, zero-filled by caller)
@@ -178,6 +187,52 @@ size_t dpvo_softagg_workspace_bytes(int64_t num_edges, int64_t groups);
 int dpvo_softagg_forward(int dtype, const void* f, int64_t ldf, const void* s, int64_t lds, const int64_t* group,
                          int64_t num_edges, int D, int64_t groups, float eps, void* y, void* workspace,
                          size_t workspace_bytes, void* stream);
+
+/* Full-row fused GEMM of the update operator (dpvo/net.py:75-93 and
+ * blocks.py GatedResidual under autocast), N = 384 output columns per row:
+ *   y16  = fp16(A W^T + bias)            A fp16 [M][K] rows at A + r*lda, or
+ *                                        gathered rows A + a_idx[m]*lda
+ *                                        (a_idx[m] < 0 -> zero_row);
+ *                                        W fp16 [384][K]; bias fp16 [384]
+ *   RELU / SIGMOID on y16 (fp16 result, as ATen's half kernels)
+ *   RES : v = res32[m] (+ res16[res16_idx[m]]) + y   (fp32; res16 rows of 384)
+ *   GATE: v = res32[m] + fp16(gate16[m] * y)         (GatedResidual, blocks.py:31)
+ *   LN  : v = LayerNorm(v; ln_g, ln_b, ln_eps) in fp32 [LN_RELU: relu(v)]
+ *   HEADS: head_out[m] = fp16 {W_d relu(v) + b_d (2), sigmoid(W_w relu(v) + b_w) (2)}
+ *          with head_w fp16 [4][384], head_b fp16 [4]   (net.py:63-72)
+ *   out32[m] = v (fp32, row stride ldo32) and/or out16[m] = fp16(v) (ldo16).
+ * K must be a multiple of 64 (pad W with zero columns; A's pad columns must
+ * be finite); A, W, zero_row 16-byte aligned; zero_row holds >= K zeros.
+ * Supported flag sets: 0, RELU, SIGMOID, LN|LN_RELU, RES, RES|LN, GATE,
+ * GATE|LN, GATE|HEADS. */
+enum {
+    DPVO_RG_RELU = 1, DPVO_RG_SIGMOID = 2, DPVO_RG_RES = 4, DPVO_RG_GATE = 8, DPVO_RG_LN = 16, DPVO_RG_LN_RELU = 32,
+    DPVO_RG_HEADS = 64
+};
+typedef struct dpvo_rowgemm_args {
+    const void* A; int64_t lda; const int64_t* a_idx; int64_t a_rows;
+    const void* W; int K; int N; const void* bias; const void* zero_row;
+    int64_t M;
+    const void* res32; int64_t ldr; const void* res16; const int64_t* res16_idx;
+    const void* gate16;
+    const float* ln_g; const float* ln_b; float ln_eps;
+    const void* head_w; const void* head_b; void* head_out;
+    void* out32; int64_t ldo32; void* out16; int64_t ldo16;
+    int flags;
+} dpvo_rowgemm_args;
+int dpvo_rowgemm(const dpvo_rowgemm_args* args, void* stream);
+
+/* Row add + LayerNorm over 384-wide rows (one pass):
+ *   v = a[m] (+ b16[b_idx[m]])  [-> LayerNorm]  -> out32 [M][384] / out16 [M][384]
+ * a is fp16 (a_f16=1) or fp32 with row stride lda; b_idx[m] < 0 adds nothing.
+ * Used for `net + h(y)[:, jx]` after SoftAgg and the GRU's first LayerNorm. */
+typedef struct dpvo_rowadd_args {
+    const void* a; int a_f16; int64_t lda; int64_t M;
+    const void* b16; const int64_t* b_idx; int64_t b_rows;
+    const float* ln_g; const float* ln_b; float ln_eps;
+    void* out32; void* out16;
+} dpvo_rowadd_args;
+int dpvo_rowadd_ln(const dpvo_rowadd_args* args, void* stream);
 
 /* out[e][:] = idx[e] >= 0 ? x[idx[e]][:] : 0, converting in_dtype -> out_dtype
  * (the mask_ix * net[:, ix] of net.py:82-85; x rows at x + r*ldx, out

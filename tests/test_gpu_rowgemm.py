@@ -1,0 +1,183 @@
+"""Full-row fused GEMM (csrc/rowgemm.hip) against a torch fp32 restatement of
+the reference's autocast dataflow (dpvo/net.py:75-93, blocks.py:15-30):
+Linear -> fp16 output, glue ops in fp32, LayerNorm in fp32.  Accumulation
+order differs from hipBLASLt, so fp16 outputs may differ by an ulp."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+D = 384
+
+
+def lin(K, seed):
+    g = torch.Generator().manual_seed(seed)
+    w = (torch.rand(D, K, generator=g) * 2 - 1) / K ** 0.5
+    b = (torch.rand(D, generator=g) * 2 - 1) / K ** 0.5
+    return w.cuda(), b.cuda()
+
+
+def y16(A16, w, b):
+    """autocast Linear: fp16 operands, fp32 accumulate, fp16 result."""
+    return (A16.float() @ w.half().float().t() + b.half().float()).half()
+
+
+def close16(got, want, tol=2e-2):
+    torch.testing.assert_close(got.float(), want.float(), rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("M", [1, 127, 128, 1000, 20000])
+@pytest.mark.parametrize("flags", [0, 1, 2])
+def test_linear_activations(M, flags):
+    import update_ops as U
+    A = torch.randn(M, D, device="cuda").half()
+    w, b = lin(D, 1)
+    W16, b16 = U.pack_linear(w, b)
+    _, out, _ = U.rowgemm(A, W16, b16, flags=flags)
+    want = y16(A, w, b)
+    if flags == U.RELU:
+        want = want.clamp_min(0)
+    if flags == U.SIGMOID:
+        want = torch.sigmoid(want.float()).half()
+    close16(out, want)
+
+
+def test_padded_k_and_row_gather():
+    """K = 882 (the corr features) padded to 896; A rows gathered, idx < 0 -> zeros."""
+    import update_ops as U
+    M, K = 3000, 882
+    buf = torch.zeros(M, 896, device="cuda", dtype=torch.float16)
+    buf[:, :K] = torch.randn(M, K, device="cuda").half()
+    w, b = lin(K, 2)
+    W16, b16 = U.pack_linear(w, b)
+    assert W16.shape == (D, 896)
+    idx = torch.randint(-1, M, (5000,), device="cuda")
+    _, out, _ = U.rowgemm(buf, W16, b16, flags=U.RELU, a_idx=idx)
+    rows = torch.where(idx[:, None] >= 0, buf[idx.clamp_min(0), :K], torch.zeros_like(buf[:1, :K]))
+    close16(out, y16(rows, w, b).clamp_min(0))
+
+
+def test_residual_layernorm_and_gather():
+    """corr L3: net = LN(net + imap[kk] + Linear(h))  (net.py:78-79)."""
+    import update_ops as U
+    M = 5000
+    A = torch.randn(M, D, device="cuda").half()
+    w, b = lin(D, 3)
+    W16, b16 = U.pack_linear(w, b)
+    net = torch.randn(M, D, device="cuda")
+    imap = torch.randn(700, D, device="cuda").half()
+    kk = torch.randint(0, 700, (M,), device="cuda")
+    g = torch.rand(D, device="cuda") + 0.5
+    be = torch.randn(D, device="cuda") * 0.1
+    o32, o16, _ = U.rowgemm(A, W16, b16, flags=U.RES | U.LN, res32=net, res16=imap, res16_idx=kk,
+                            ln=(g, be, 1e-3), want32=True)
+    v = net + imap[kk].float() + y16(A, w, b).float()
+    want = torch.nn.functional.layer_norm(v, (D,), g, be, 1e-3)
+    torch.testing.assert_close(o32, want, rtol=1e-3, atol=2e-3)
+    close16(o16, want.half())
+
+
+def test_layernorm_relu_fp16_out():
+    """corr L2: relu(LN(Linear(h))) -> fp16 (the next Linear's autocast input)."""
+    import update_ops as U
+    M = 4000
+    A = torch.randn(M, D, device="cuda").half()
+    w, b = lin(D, 4)
+    W16, b16 = U.pack_linear(w, b)
+    g = torch.rand(D, device="cuda") + 0.5
+    be = torch.randn(D, device="cuda") * 0.1
+    _, o16, _ = U.rowgemm(A, W16, b16, flags=U.LN | U.LN_RELU, ln=(g, be, 1e-3))
+    want = torch.nn.functional.layer_norm(y16(A, w, b).float(), (D,), g, be, 1e-3).clamp_min(0)
+    close16(o16, want.half())
+
+
+@pytest.mark.parametrize("with_ln", [False, True])
+def test_gated_residual_and_heads(with_ln):
+    """GatedResidual x + gate(x) * res(x) (blocks.py:26-30), then LN or the d/w heads (net.py:63-72)."""
+    import update_ops as U
+    M = 3000
+    h = torch.randn(M, D, device="cuda").half()
+    x = torch.randn(M, D, device="cuda")
+    gate = torch.sigmoid(torch.randn(M, D, device="cuda")).half()
+    w, b = lin(D, 5)
+    W16, b16 = U.pack_linear(w, b)
+    r = y16(h, w, b)
+    v = x + (gate * r).float()
+    if with_ln:
+        g = torch.rand(D, device="cuda") + 0.5
+        be = torch.randn(D, device="cuda") * 0.1
+        o32, o16, _ = U.rowgemm(h, W16, b16, flags=U.GATE | U.LN, res32=x, gate16=gate, ln=(g, be, 1e-3),
+                                want32=True)
+        want = torch.nn.functional.layer_norm(v, (D,), g, be, 1e-3)
+        torch.testing.assert_close(o32, want, rtol=1e-3, atol=2e-3)
+    else:
+        hw = (torch.randn(4, D, device="cuda") * 0.05).half()
+        hb = (torch.randn(4, device="cuda") * 0.1).half()
+        o32, _, heads = U.rowgemm(h, W16, b16, flags=U.GATE | U.HEADS, res32=x, gate16=gate, heads=(hw, hb),
+                                  want32=True, want16=False)
+        torch.testing.assert_close(o32, v, rtol=1e-3, atol=2e-3)
+        z = (v.clamp_min(0).half().float() @ hw.float().t() + hb.float()).half()
+        want = torch.cat([z[:, :2], torch.sigmoid(z[:, 2:].float()).half()], 1)
+        close16(heads, want)
+
+
+def test_rowadd_ln():
+    import update_ops as U
+    M = 3000
+    a = torch.randn(M, D, device="cuda")
+    hk = torch.randn(500, D, device="cuda").half()
+    jx = torch.randint(0, 500, (M,), device="cuda")
+    g = torch.rand(D, device="cuda") + 0.5
+    be = torch.randn(D, device="cuda") * 0.1
+    o32, o16 = U.rowadd_ln(a, hk, jx)
+    torch.testing.assert_close(o32, a + hk[jx].float())
+    o32, o16 = U.rowadd_ln(a, hk, jx, ln=(g, be, 1e-3))
+    want = torch.nn.functional.layer_norm(a + hk[jx].float(), (D,), g, be, 1e-3)
+    torch.testing.assert_close(o32, want, rtol=1e-4, atol=1e-4)
+    close16(o16, want.half())
+
+
+def test_errors():
+    import update_ops as U
+    A = torch.randn(10, D, device="cuda").half()
+    w, b = lin(D, 6)
+    W16, b16 = U.pack_linear(w, b)
+    with pytest.raises(RuntimeError):
+        U.rowgemm(A, W16, b16, flags=U.RES)           # residual missing
+    with pytest.raises(RuntimeError):
+        U.rowgemm(A, W16, b16, flags=U.RELU | U.LN)   # unsupported combination
+    with pytest.raises(RuntimeError):
+        U.rowgemm(A.float(), W16, b16)
+
+
+def test_fused_update_operator_matches_torch_path():
+    """Update.forward (net.py:75-93) fused path vs the module's own torch
+    composition, same weights and inputs, both under fp16 autocast."""
+    from dpvo.net import Update
+    from dpvo.synthetic import steady_state_edges
+    torch.manual_seed(0)
+    upd = Update(3).cuda()
+    with torch.no_grad():
+        for m in upd.modules():        # livelier than default init so LN/gates see O(1) values
+            if isinstance(m, torch.nn.Linear):
+                m.weight.mul_(3.0)
+    ii, jj, kk = steady_state_edges(40, 16, 13, 22, "cuda")
+    E = ii.numel()
+    net = torch.randn(1, E, 384, device="cuda")
+    inp = torch.randn(1, E, 384, device="cuda").half()
+    corr = torch.zeros(E, 896, device="cuda", dtype=torch.float16)
+    corr[:, :882] = torch.randn(E, 882, device="cuda").half()
+    corr = corr[:, :882][None]
+    outs = {}
+    for fused in (True, False):
+        Update.FUSED = fused
+        with torch.no_grad(), torch.autocast("cuda", enabled=True):
+            outs[fused] = upd(net, inp, corr, None, ii, jj, kk)
+    Update.FUSED = True
+    (nf, (df, wf, _)), (nt, (dt, wt, _)) = outs[True], outs[False]
+    assert nf.dtype == nt.dtype == torch.float32 and nf.shape == nt.shape == (1, E, 384)
+    assert df.dtype == torch.float16 and df.shape == dt.shape == (1, E, 2) and wf.shape == (1, E, 2)
+    err = (nf - nt).abs().max().item() / nt.abs().max().item()
+    assert err < 2e-2, err
+    torch.testing.assert_close(df.float(), dt.float(), rtol=5e-2, atol=5e-2)
+    torch.testing.assert_close(wf.float(), wt.float(), rtol=2e-2, atol=2e-2)

@@ -30,6 +30,8 @@ _SIGNATURES = {
     "dpvo_corr_forward": (_ip, [_ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip, _vp, _vp]),
     "dpvo_corr_forward_pyramid": (_ip, [_ip, _vp, _vp, _vp, _ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip,
                                         _vp, _vp]),
+    "dpvo_corr_forward_pyramid_ld": (_ip, [_ip, _vp, _vp, _vp, _ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                           _ip, _vp, _i64, _vp]),
     "dpvo_corr_backward": (_ip, [_ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip, _vp, _vp, _vp]),
     "dpvo_patchify_forward": (_ip, [_ip, _vp, _vp, _vp, _vp, _i64, _ip, _vp, _vp]),
     "dpvo_patchify_backward": (_ip, [_ip, _vp, _vp, _i64, _ip, _vp, _vp, _vp]),
@@ -46,6 +48,8 @@ _SIGNATURES = {
     "dpvo_softagg_workspace_bytes": (_sz, [_i64, _i64]),
     "dpvo_softagg_forward": (_ip, [_ip, _vp, _i64, _vp, _i64, _vp, _i64, _ip, _i64, _fp, _vp, _vp, _sz, _vp]),
     "dpvo_gather_rows": (_ip, [_ip, _vp, _i64, _i64, _vp, _i64, _ip, _ip, _vp, _vp]),
+    "dpvo_rowgemm": (_ip, [_vp, _vp]),
+    "dpvo_rowadd_ln": (_ip, [_vp, _vp]),
 }
 EXPORTED = tuple(_SIGNATURES)
 

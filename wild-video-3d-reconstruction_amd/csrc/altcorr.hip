@@ -588,14 +588,29 @@ extern "C" int dpvo_corr_forward_pyramid(int dtype, const void* gmap, const int6
                                          const int64_t* coords_stride, const int64_t* ii, const int64_t* jj,
                                          int radius, void* corr, void* stream)
 {
+    return dpvo_corr_forward_pyramid_ld(dtype, gmap, gmap_size, gmap_stride, nlev, fmaps, fmap_sizes, fmap_strides,
+                                        level_scale, coords, coords_size, coords_stride, ii, jj, radius, corr, 0,
+                                        stream);
+}
+
+extern "C" int dpvo_corr_forward_pyramid_ld(int dtype, const void* gmap, const int64_t* gmap_size,
+                                            const int64_t* gmap_stride, int nlev, const void* const* fmaps,
+                                            const int64_t* fmap_sizes, const int64_t* fmap_strides,
+                                            const float* level_scale, const float* coords,
+                                            const int64_t* coords_size, const int64_t* coords_stride,
+                                            const int64_t* ii, const int64_t* jj, int radius, void* corr,
+                                            int64_t edge_stride, void* stream)
+{
     DPVO_CHECK_ARG(check_common(dtype, gmap, gmap_size, coords_size, ii, jj, radius, corr),
                    "invalid arguments (dtype/radius/shapes)");
     DPVO_CHECK_ARG(nlev >= 1 && nlev <= 8 && fmaps && level_scale, "nlev must be 1..8");
     const int Do = 2 * radius + 1;
     const int64_t P2 = coords_size[3] * coords_size[4];
     const int64_t E = coords_size[1];
-    // output: [B][E][x][y][P][P][L]
-    const int64_t o_e = (int64_t)Do * Do * P2 * nlev;
+    // output: [B][E][x][y][P][P][L], edges edge_stride elements apart (0: packed)
+    const int64_t o_row = (int64_t)Do * Do * P2 * nlev;
+    DPVO_CHECK_ARG(edge_stride == 0 || edge_stride >= o_row, "edge_stride smaller than one edge's features");
+    const int64_t o_e = edge_stride ? edge_stride : o_row;
     bool all_fast = nlev <= 2;
     for (int l = 0; l < nlev && all_fast; l++)
         all_fast = fast_path_ok(dtype, gmap_size, fmap_sizes + 5 * l, fmap_strides + 5 * l, coords_size, radius) &&

@@ -1,0 +1,452 @@
+// rowgemm.hip -- full-row MFMA GEMM with fused update-operator epilogues (gfx950).
+//
+// The learned update operator (reference dpvo/net.py:75-93, blocks.py) is a
+// chain of Linear(384 -> 384) layers over E ~ 95k edge rows, glued by
+// LayerNorm, ReLU/sigmoid, residual adds, gating and row gathers.  Under the
+// reference's autocast every Linear is an fp16 GEMM (fp32 accumulate, fp16
+// output) and every glue op is its own elementwise pass over E x 384 fp32.
+//
+// Here one kernel computes   Y = A W^T + b   for a tile of 128 rows and ALL
+// 384 output columns, so any row-wise op can run in the epilogue:
+//   y16 = fp16(acc + b)  [-> relu | sigmoid]          (autocast Linear output)
+//   v   = y  | res32 + res16[idx] + y | res32 + fp16(gate16 * y)
+//   v   = LayerNorm(v) [-> relu]                       (fp32, as autocast)
+//   heads: d = W_d relu(v) + b_d, w = sigmoid(W_w relu(v) + b_w)  (fp16 out)
+//   out32 = v, out16 = fp16(v)
+// A rows may be gathered through an index (idx < 0 -> a zero row), which
+// fuses `mask_ix * net[:, ix]` (net.py:82-85) into the GEMM's operand load.
+//
+// Tiling: 512 threads = 8 waves as 2 (M) x 4 (N); wave tile 64 x 96 =
+// 4 x 6 mfma_f32_16x16x32_f16 accumulators.  BK = 64; A (16 KB) and W (48 KB)
+// stages are staged global -> LDS by global_load_lds (16 B per lane, source
+// pre-swizzled, conflict-free ds_read_b128 fragment reads), two stages in
+// flight.  Persistent blocks walk a flat (tile, k-stage) sequence, so the next
+// tile's first stage loads during the current tile's epilogue.
+#include "common.hpp"
+
+#include <algorithm>
+
+namespace dpvo {
+namespace {
+
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+constexpr int RG_BM = 128, RG_BN = 384, RG_BK = 64, RG_THREADS = 512;
+constexpr int RG_A_STAGE = RG_BM * RG_BK * 2;   // 16 KB
+constexpr int RG_W_STAGE = RG_BN * RG_BK * 2;   // 48 KB
+constexpr int RG_STAGE = RG_A_STAGE + RG_W_STAGE;
+constexpr int RG_LDS = 2 * RG_STAGE;            // 128 KB
+
+enum {
+    RG_RELU = DPVO_RG_RELU, RG_SIGMOID = DPVO_RG_SIGMOID, RG_RES = DPVO_RG_RES, RG_GATE = DPVO_RG_GATE,
+    RG_LN = DPVO_RG_LN, RG_LN_RELU = DPVO_RG_LN_RELU, RG_HEADS = DPVO_RG_HEADS
+};
+
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// all-reduce over a DPP row (16 lanes) by rotations: every lane gets the sum
+__device__ __forceinline__ float rowsum16(float s)
+{
+    s += dpp_f<0x128>(s);
+    s += dpp_f<0x124>(s);
+    s += dpp_f<0x122>(s);
+    s += dpp_f<0x121>(s);
+    return s;
+}
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_wave_base)
+{
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ float hround(float v) { return (float)(half_t)v; }
+
+// sum over the 64 lanes, broadcast (DPP row reduce + 4 readlanes)
+__device__ __forceinline__ float wave_sum(float s)
+{
+    s = rowsum16(s);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 0)) +
+           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 16)) +
+           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 32)) +
+           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 48));
+}
+
+constexpr int RG_YS = 784;  // y-tile row stride in bytes (768 + 16: conflict-free b16 writes)
+
+// One output row: lane owns columns 2*lane + 128*j (j < 3) as float2.
+template <int FLAGS>
+__device__ __forceinline__ void epilogue_row(const dpvo_rowgemm_args& p, const char* yrow, int64_t row, int lane)
+{
+    if (row >= p.M) return;
+    float2_t v[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const half2_t y = *(const half2_t*)(yrow + (128 * j + 2 * lane) * 2);
+        v[j] = float2_t{(float)y.x, (float)y.y};
+    }
+    if (FLAGS & (RG_RES | RG_GATE)) {
+        const float* r32 = (const float*)p.res32 + row * p.ldr;
+        const half_t* r16 = nullptr;
+        if ((FLAGS & RG_RES) && p.res16) {
+            const int64_t s = p.res16_idx ? p.res16_idx[row] : row;
+            if (s >= 0) r16 = (const half_t*)p.res16 + s * RG_BN;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int c = 128 * j + 2 * lane;
+            float2_t base = *(const float2_t*)(r32 + c);
+            if (FLAGS & RG_GATE) {
+                const half2_t g = *(const half2_t*)((const half_t*)p.gate16 + row * RG_BN + c);
+                v[j] = base + float2_t{hround((float)g.x * v[j].x), hround((float)g.y * v[j].y)};
+            } else {
+                if (r16) {
+                    const half2_t b = *(const half2_t*)(r16 + c);
+                    base += float2_t{(float)b.x, (float)b.y};
+                }
+                v[j] = base + v[j];
+            }
+        }
+    }
+    if (FLAGS & RG_LN) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 3; j++) s += v[j].x + v[j].y;
+        const float mean = wave_sum(s) * (1.f / RG_BN);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const float2_t d = v[j] - mean;
+            q += d.x * d.x + d.y * d.y;
+        }
+        const float rstd = rsqrtf(wave_sum(q) * (1.f / RG_BN) + p.ln_eps);
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int c = 128 * j + 2 * lane;
+            const float2_t g = *(const float2_t*)(p.ln_g + c);
+            const float2_t b = *(const float2_t*)(p.ln_b + c);
+            v[j] = (v[j] - mean) * rstd * g + b;
+            if (FLAGS & RG_LN_RELU) v[j] = float2_t{fmaxf(v[j].x, 0.f), fmaxf(v[j].y, 0.f)};
+        }
+    }
+    if (FLAGS & RG_HEADS) {
+        // d = W_d relu(v) + b_d ; w = sigmoid(W_w relu(v) + b_w)   (fp16 operands, fp32 accumulate)
+        float d[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int c = 128 * j + 2 * lane;
+            const float x0 = hround(fmaxf(v[j].x, 0.f)), x1 = hround(fmaxf(v[j].y, 0.f));
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const half2_t w = *(const half2_t*)((const half_t*)p.head_w + q * RG_BN + c);
+                d[q] += x0 * (float)w.x + x1 * (float)w.y;
+            }
+        }
+        half_t o[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            float h = hround(wave_sum(d[q]) + (float)((const half_t*)p.head_b)[q]);
+            if (q >= 2) h = hround(1.f / (1.f + expf(-h)));
+            o[q] = (half_t)h;
+        }
+        if (lane == 0) {
+            typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+            *(h4_t*)((half_t*)p.head_out + row * 4) = h4_t{o[0], o[1], o[2], o[3]};
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const int c = 128 * j + 2 * lane;
+        if (p.out32) *(float2_t*)((float*)p.out32 + row * p.ldo32 + c) = v[j];
+        if (p.out16) *(half2_t*)((half_t*)p.out16 + row * p.ldo16 + c) = half2_t{(half_t)v[j].x, (half_t)v[j].y};
+    }
+}
+
+template <int FLAGS>
+__global__ __launch_bounds__(RG_THREADS, 1) void rowgemm_kernel(dpvo_rowgemm_args p)
+{
+    __shared__ __attribute__((aligned(16))) char smem[RG_LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int K = p.K;
+    const int ksteps = K / RG_BK;
+    const int64_t ntiles = (p.M + RG_BM - 1) / RG_BM;
+    if ((int64_t)blockIdx.x >= ntiles) return;
+    const int64_t my_tiles = (ntiles - 1 - blockIdx.x) / gridDim.x + 1;
+    const int64_t total = my_tiles * ksteps;
+
+    const half_t* __restrict__ Wt = (const half_t*)p.W;
+    const half_t* __restrict__ zero = (const half_t*)p.zero_row;
+
+    // staging sources: lane L of a wave-instruction fills LDS row base+L/8,
+    // physical 16-B chunk L%8, holding logical chunk (L%8) ^ ((row>>1)&7)
+    const int srow = lane >> 3, pch = lane & 7;
+    const half_t* wsrc[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        const int n = (wave * 6 + j) * 8 + srow;
+        wsrc[j] = Wt + (int64_t)n * K + 8 * (pch ^ ((n >> 1) & 7));
+    }
+    const half_t* asrc[2];
+    auto set_tile_a = [&](int64_t tile) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int r = (wave * 2 + j) * 8 + srow;
+            const int64_t m = tile * RG_BM + r;
+            const half_t* row = zero;
+            if (m < p.M) {
+                const int64_t s = p.a_idx ? p.a_idx[m] : m;
+                if (s >= 0 && s < p.a_rows) row = (const half_t*)p.A + s * p.lda;
+            }
+            asrc[j] = row + 8 * (pch ^ ((r >> 1) & 7));
+        }
+    };
+    // stage s (0..ksteps) of the block's j-th tile -> buffer parity of the flat index
+    auto issue = [&](int ks, int64_t tile, int buf) {
+        if (ks == 0) set_tile_a(tile);
+        char* sA = smem + buf * RG_STAGE;
+        char* sW = sA + RG_A_STAGE;
+        const int k0 = ks * RG_BK;
+        glds16(asrc[0] + k0, sA + (wave * 2 + 0) * 1024);
+        glds16(asrc[1] + k0, sA + (wave * 2 + 1) * 1024);
+#pragma unroll
+        for (int j = 0; j < 6; j++) glds16(wsrc[j] + k0, sW + (wave * 6 + j) * 1024);
+    };
+
+    f4_t acc[4][6];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+
+    // fragment read offsets (bytes within a stage), k-step independent part
+    const int fr = lane & 15, fq = lane >> 4;
+    int a_off[4], w_off[6], a_sw[4], w_sw[6];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++) {
+        const int row = wm * 64 + mt * 16 + fr;
+        a_off[mt] = row * 128;
+        a_sw[mt] = (row >> 1) & 7;
+    }
+#pragma unroll
+    for (int nt = 0; nt < 6; nt++) {
+        const int n = wn * 96 + nt * 16 + fr;
+        w_off[nt] = RG_A_STAGE + n * 128;
+        w_sw[nt] = (n >> 1) & 7;
+    }
+
+    int64_t tile = blockIdx.x;
+    int ks = 0, buf = 0;
+    issue(0, tile, 0);
+    for (int64_t i = 0; i < total; i++) {
+        // the flat sequence's next (tile, stage)
+        int nks = ks + 1;
+        int64_t ntile = tile;
+        if (nks == ksteps) {
+            nks = 0;
+            ntile += gridDim.x;
+        }
+        if (i + 1 < total) {
+            issue(nks, ntile, buf ^ 1);
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const char* st = smem + buf * RG_STAGE;
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+            const int c = kk * 4 + fq;
+            h8_t a[4], b[6];
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(st + a_off[mt] + 16 * (c ^ a_sw[mt]));
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt] + 16 * (c ^ w_sw[nt]));
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                for (int nt = 0; nt < 6; nt++)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_barrier();
+        const int cur_buf = buf;
+        const int64_t cur_tile = tile;
+        const bool last = ks == ksteps - 1;
+        ks = nks;
+        tile = ntile;
+        buf ^= 1;
+        if (!last) continue;
+
+        // ------------------------------ epilogue ------------------------------
+        // Per 64-row half h: the waves owning it (wm == h) write y16 = fp16(acc + b)
+        // [act] into the just-consumed stage buffer; then every wave finishes 8
+        // whole rows (lanes over columns: coalesced loads/stores, DPP+readlane
+        // row reductions).  The other stage buffer is loading the next tile.
+        char* yt = smem + cur_buf * RG_STAGE;
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            if (wm == h) {
+#pragma unroll
+                for (int nt = 0; nt < 6; nt++) {
+                    const int cl = wn * 96 + nt * 16 + fr;
+                    const float bias = (float)((const half_t*)p.bias)[cl];
+#pragma unroll
+                    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            half_t y = (half_t)(acc[mt][nt][r] + bias);
+                            if (FLAGS & RG_RELU) y = y > (half_t)0 ? y : (half_t)0;
+                            if (FLAGS & RG_SIGMOID) y = (half_t)(1.f / (1.f + expf(-(float)y)));
+                            *(half_t*)(yt + (mt * 16 + fq * 4 + r) * RG_YS + cl * 2) = y;
+                            acc[mt][nt][r] = 0.f;
+                        }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int qb = 0; qb < 8; qb += 4) {
+#pragma unroll
+                for (int q = qb; q < qb + 4; q++)
+                    epilogue_row<FLAGS>(p, yt + (wave * 8 + q) * RG_YS, cur_tile * RG_BM + h * 64 + wave * 8 + q, lane);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+    }
+}
+
+
+// v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16   (one wave per row)
+__global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
+{
+    const int lane = threadIdx.x & 63;
+    for (int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; row < p.M;
+         row += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        float v[6];
+        const half_t* b = nullptr;
+        if (p.b16) {
+            const int64_t s = p.b_idx ? p.b_idx[row] : row;
+            if (s >= 0 && s < p.b_rows) b = (const half_t*)p.b16 + s * RG_BN;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int c = 128 * j + 2 * lane;
+            float2_t a;
+            if (p.a_f16) {
+                half2_t h = *(const half2_t*)((const half_t*)p.a + row * p.lda + c);
+                a = float2_t{(float)h.x, (float)h.y};
+            } else {
+                a = *(const float2_t*)((const float*)p.a + row * p.lda + c);
+            }
+            if (b) {
+                half2_t h = *(const half2_t*)(b + c);
+                a.x += (float)h.x;
+                a.y += (float)h.y;
+            }
+            v[2 * j] = a.x;
+            v[2 * j + 1] = a.y;
+        }
+        if (p.ln_g) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 6; j++) s += v[j];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+            const float mean = s * (1.f / RG_BN);
+            float q = 0.f;
+#pragma unroll
+            for (int j = 0; j < 6; j++) q += (v[j] - mean) * (v[j] - mean);
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
+            const float rstd = rsqrtf(q * (1.f / RG_BN) + p.ln_eps);
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const int c = 128 * j + 2 * lane;
+                v[2 * j] = (v[2 * j] - mean) * rstd * ((const float*)p.ln_g)[c] + ((const float*)p.ln_b)[c];
+                v[2 * j + 1] = (v[2 * j + 1] - mean) * rstd * ((const float*)p.ln_g)[c + 1] + ((const float*)p.ln_b)[c + 1];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int c = 128 * j + 2 * lane;
+            if (p.out32) *(float2_t*)((float*)p.out32 + row * RG_BN + c) = float2_t{v[2 * j], v[2 * j + 1]};
+            if (p.out16) *(half2_t*)((half_t*)p.out16 + row * RG_BN + c) = half2_t{(half_t)v[2 * j], (half_t)v[2 * j + 1]};
+        }
+    }
+}
+
+int g_num_cus = 0;
+
+}  // namespace
+}  // namespace dpvo
+
+using namespace dpvo;
+
+#define RG_CASE(F)                                                                                   \
+    case (F):                                                                                        \
+        hipLaunchKernelGGL(rowgemm_kernel<(F)>, dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a); \
+        break;
+
+extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
+{
+    DPVO_CHECK_ARG(a != nullptr, "null args");
+    DPVO_CHECK_ARG(a->N == RG_BN, "rowgemm: output width must be 384");
+    DPVO_CHECK_ARG(a->K > 0 && a->K % RG_BK == 0, "rowgemm: K must be a positive multiple of 64 (pad W with zeros)");
+    DPVO_CHECK_ARG(a->A && a->W && a->bias && a->zero_row, "rowgemm: A, W, bias and zero_row are required");
+    DPVO_CHECK_ARG(a->lda >= a->K && a->lda % 8 == 0, "rowgemm: lda must be >= K and a multiple of 8");
+    DPVO_CHECK_ARG(((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->W & 15) == 0 && ((uintptr_t)a->zero_row & 15) == 0,
+                   "rowgemm: A, W and zero_row must be 16-byte aligned");
+    const int f = a->flags;
+    DPVO_CHECK_ARG(!((f & DPVO_RG_RES) || (f & DPVO_RG_GATE)) || a->res32, "rowgemm: residual input missing");
+    DPVO_CHECK_ARG(!(f & DPVO_RG_GATE) || a->gate16, "rowgemm: gate input missing");
+    DPVO_CHECK_ARG(!(f & DPVO_RG_LN) || (a->ln_g && a->ln_b), "rowgemm: LayerNorm weights missing");
+    DPVO_CHECK_ARG(!(f & DPVO_RG_HEADS) || (a->head_w && a->head_b && a->head_out), "rowgemm: head weights missing");
+    if (a->M <= 0) return 0;
+    if (g_num_cus == 0) {
+        int dev = 0;
+        DPVO_CHECK_HIP(hipGetDevice(&dev));
+        DPVO_CHECK_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+        if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
+    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+    switch (f) {
+        RG_CASE(0)
+        RG_CASE(DPVO_RG_RELU)
+        RG_CASE(DPVO_RG_SIGMOID)
+        RG_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
+        RG_CASE(DPVO_RG_RES)
+        RG_CASE(DPVO_RG_RES | DPVO_RG_LN)
+        RG_CASE(DPVO_RG_GATE | DPVO_RG_LN)
+        RG_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
+        RG_CASE(DPVO_RG_GATE)
+    default:
+        set_error("dpvo_rowgemm: unsupported epilogue flag combination " + std::to_string(f));
+        return -1;
+    }
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_rowadd_ln(const dpvo_rowadd_args* a, void* stream)
+{
+    DPVO_CHECK_ARG(a != nullptr && a->a != nullptr, "rowadd_ln: input missing");
+    DPVO_CHECK_ARG(a->lda >= RG_BN && a->lda % 2 == 0, "rowadd_ln: lda must be even and >= 384");
+    DPVO_CHECK_ARG(a->out32 || a->out16, "rowadd_ln: no output");
+    DPVO_CHECK_ARG(!a->ln_g == !a->ln_b, "rowadd_ln: LayerNorm needs both weight and bias");
+    if (a->M <= 0) return 0;
+    const unsigned grid = grid_for(a->M * 64, 256, 16384);
+    hipLaunchKernelGGL(rowadd_ln_kernel, dim3(grid), dim3(256), 0, as_stream(stream), *a);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}

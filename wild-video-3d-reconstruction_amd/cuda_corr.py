@@ -34,23 +34,30 @@ def forward(fmap1, fmap2, coords, ii, jj, radius):
     return [out.permute(0, 1, 3, 2, 4, 5)]
 
 
-def forward_pyramid(fmap1, pyramid, coords, ii, jj, radius, scales):
+def forward_pyramid(fmap1, pyramid, coords, ii, jj, radius, scales, out=None):
     """Fused form of DPVO.corr (dpvo/dpvo.py:326-333): all levels in one
-    launch, returned in the stacked layout torch.stack([...], -1).view(B, E, -1)."""
+    launch, returned in the stacked layout torch.stack([...], -1).view(B, E, -1).
+    ``out`` may be a [B, E, F] view of wider rows (e.g. F = 882 of 896)."""
     for f in pyramid:
         _check_corr_args(fmap1, f, coords, ii, jj)
     B, E, _, Hh, W = coords.shape
     L = len(pyramid)
     Do = 2 * radius + 1
-    out = torch.empty((B, E, Do * Do * Hh * W * L), dtype=fmap1.dtype, device=fmap1.device)
+    F = Do * Do * Hh * W * L
+    if out is None:
+        out = torch.empty((B, E, F), dtype=fmap1.dtype, device=fmap1.device)
+    elif (out.shape != (B, E, F) or out.dtype != fmap1.dtype or out.stride(2) != 1 or
+          (B > 1 and out.stride(0) != E * out.stride(1))):
+        raise RuntimeError("forward_pyramid: out must be [B, E, F] with unit feature stride")
     ii, jj = H.idx64(ii), H.idx64(jj)
     ptrs = (H._vp * L)(*[f.data_ptr() for f in pyramid])
     fs = H.i64arr([s for f in pyramid for s in f.shape])
     fst = H.i64arr([s for f in pyramid for s in f.stride()])
     sc = (H._fp * L)(*[float(s) for s in scales])
-    H.check(H.lib().dpvo_corr_forward_pyramid(
+    H.check(H.lib().dpvo_corr_forward_pyramid_ld(
         H.dtype_code(fmap1), H.ptr(fmap1), H.sizes(fmap1), H.strides(fmap1), L, ptrs, fs, fst, sc, H.ptr(coords),
-        H.sizes(coords), H.strides(coords), H.ptr(ii), H.ptr(jj), int(radius), H.ptr(out), H.stream_of(fmap1)))
+        H.sizes(coords), H.strides(coords), H.ptr(ii), H.ptr(jj), int(radius), H.ptr(out),
+        out.stride(1) if E > 0 else 0, H.stream_of(fmap1)))
     return out
 
 

@@ -24,6 +24,9 @@ from .patchgraph import PatchGraph
 from .utils import Timer, flatmeshgrid
 
 
+CORR_DIM, CORR_ROW = 882, 896  # 2 levels x 7 x 7 x 3 x 3 features; padded row
+
+
 def _ring(pmem, C, h, w, channel_last, **kw):
     if channel_last:
         return torch.zeros(1, pmem, h, w, C, **kw).permute(0, 1, 4, 2, 3)
@@ -165,7 +168,21 @@ class DPVO:
         ii, jj = indicies if indicies is not None else (self.pg.kk, self.pg.jj)
         ii1 = ii % (self.M * self.pmem)
         jj1 = jj % self.pmem
-        return altcorr.corr_pyramid(self.gmap, self.pyramid, coords, ii1, jj1, 3, (1, 4)).view(1, len(ii), -1)
+        E = len(ii)
+        out = None
+        if self.gmap_.dtype == torch.float16:
+            # rows padded to 896 (zeros past 882): the update operator's first
+            # Linear reads them as 16-byte aligned GEMM rows without a copy
+            buf = self._corr_rows(E)
+            out = buf[:E, :CORR_DIM].unsqueeze(0)
+        return altcorr.corr_pyramid(self.gmap, self.pyramid, coords, ii1, jj1, 3, (1, 4), out=out).view(1, E, -1)
+
+    def _corr_rows(self, E):
+        buf = getattr(self, "_corr_buf", None)
+        if buf is None or buf.shape[0] < E:
+            buf = torch.zeros(max(E, 1024) * 5 // 4, CORR_ROW, dtype=torch.float16, device=self.device)
+            self._corr_buf = buf
+        return buf
 
     def reproject(self, indicies=None):
         """patch kk from frame ii into frame jj -> [1, E, 2, P, P] (dpvo.py:335-339)."""

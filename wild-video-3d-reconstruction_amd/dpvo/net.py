@@ -33,9 +33,88 @@ class Update(nn.Module):
                                   nn.LayerNorm(DIM, eps=1e-3), nn.ReLU(inplace=True), nn.Linear(DIM, DIM))
         self.d = nn.Sequential(nn.ReLU(inplace=False), nn.Linear(DIM, 2), GradientClip())
         self.w = nn.Sequential(nn.ReLU(inplace=False), nn.Linear(DIM, 2), GradientClip(), nn.Sigmoid())
+        self._pk = None
+
+    FUSED = True  # inference under fp16 autocast runs the fused HIP path (class-level switch for A/B tests)
+
+    # ------------------------------------------------------------ fused path
+    def _packed(self):
+        """fp16 GEMM operands (what autocast casts the parameters to), rebuilt when any parameter changes."""
+        key = tuple((q.data_ptr(), q._version) for q in self.parameters())
+        if self._pk is not None and self._pk[0] == key:
+            return self._pk[1]
+        P = update_ops.pack_linear
+        ln = lambda m: (m.weight.detach().float().contiguous(), m.bias.detach().float().contiguous(), m.eps)
+        agg = lambda a: (P(a.f.weight, a.f.bias), P(a.g.weight, a.g.bias), P(a.h.weight, a.h.bias))
+        gr = lambda g: (P(g.gate[0].weight, g.gate[0].bias), P(g.res[0].weight, g.res[0].bias),
+                        P(g.res[2].weight, g.res[2].bias))
+        pk = {
+            "corr": (P(self.corr[0].weight, self.corr[0].bias), P(self.corr[2].weight, self.corr[2].bias),
+                     ln(self.corr[3]), P(self.corr[5].weight, self.corr[5].bias)),
+            "norm": ln(self.norm),
+            "c1": (P(self.c1[0].weight, self.c1[0].bias), P(self.c1[2].weight, self.c1[2].bias)),
+            "c2": (P(self.c2[0].weight, self.c2[0].bias), P(self.c2[2].weight, self.c2[2].bias)),
+            "agg_kk": agg(self.agg_kk), "agg_ij": agg(self.agg_ij),
+            "gru": (ln(self.gru[0]), gr(self.gru[1]), ln(self.gru[2]), gr(self.gru[3])),
+            "heads": (torch.cat([self.d[1].weight, self.w[1].weight]).detach().half().contiguous(),
+                      torch.cat([self.d[1].bias, self.w[1].bias]).detach().half().contiguous()),
+        }
+        self._pk = (key, pk)
+        return pk
+
+    def _fusable(self, net, inp, corr):
+        return (not torch.is_grad_enabled() and net.is_cuda and net.dtype == torch.float32 and
+                inp.dtype == torch.float16 and corr.dtype == torch.float16 and net.shape[0] == 1 and
+                torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16 and
+                self.FUSED)
+
+    def _forward_fused(self, net, inp, corr, ii, jj, kk):
+        """The same dataflow as the reference under autocast, in 19 full-row
+        fused GEMMs (csrc/rowgemm.hip) + 2 SoftAggs: every Linear is an fp16
+        GEMM with fp32 accumulate; residual adds, LayerNorms, gating and the
+        d/w heads run in fp32 in the GEMM epilogues."""
+        U = update_ops
+        pk = self._packed()
+        E = net.shape[1]
+        c = corr[0]
+        if c.stride(0) < 896 or c.data_ptr() % 16:
+            padded = torch.zeros(E, 896, dtype=torch.float16, device=c.device)
+            padded[:, :c.shape[1]] = c
+            c = padded
+        c0, c1, cln, c2 = pk["corr"]
+        _, h, _ = U.rowgemm(c, *c0, flags=U.RELU)
+        _, h, _ = U.rowgemm(h, *c1, flags=U.LN | U.LN_RELU, ln=cln)
+        n32, n16, _ = U.rowgemm(h, *c2, flags=U.RES | U.LN, res32=net[0], res16=inp[0].contiguous(),
+                                ln=pk["norm"], want32=True)
+        ix, jx = fastba.neighbors(kk, jj)
+        for (la, lb), nb in ((pk["c1"], ix), (pk["c2"], jx)):
+            _, h, _ = U.rowgemm(n16, *la, flags=U.RELU, a_idx=nb)
+            n32, n16, _ = U.rowgemm(h, *lb, flags=U.RES, res32=n32, want32=True)
+        ln0, gr1, ln1, gr2 = pk["gru"]
+        for (pf, pg_, ph), key, ln in ((pk["agg_kk"], kk, None), (pk["agg_ij"], ii * 12345 + jj, ln0)):
+            uniq, gid = torch.unique(key, return_inverse=True)
+            _, f16, _ = U.rowgemm(n16, *pf)
+            _, g16, _ = U.rowgemm(n16, *pg_)
+            y = U.softagg(f16, g16, gid, uniq.numel())
+            _, hy, _ = U.rowgemm(y, *ph)
+            n32, n16 = U.rowadd_ln(n32, hy, gid, ln=ln)
+        # gru = LN0 (fused above), GatedResidual, LN1, GatedResidual; then the d / w heads
+        for gr, last in ((gr1, False), (gr2, True)):
+            pgate, pr1, pr2 = gr
+            _, g16, _ = U.rowgemm(n16, *pgate, flags=U.SIGMOID)
+            _, h, _ = U.rowgemm(n16, *pr1, flags=U.RELU)
+            if last:
+                n32, _, heads = U.rowgemm(h, *pr2, flags=U.GATE | U.HEADS, res32=n32, gate16=g16,
+                                          heads=pk["heads"], want32=True, want16=False)
+            else:
+                n32, n16, _ = U.rowgemm(h, *pr2, flags=U.GATE | U.LN, res32=n32, gate16=g16, ln=ln1,
+                                        want32=True)
+        return n32[None], (heads[None, :, :2], heads[None, :, 2:], None)
 
     def forward(self, net, inp, corr, flow, ii, jj, kk):
         """edge hidden state -> (new state, (delta, weight, None)) (net.py:75-93)."""
+        if self._fusable(net, inp, corr):
+            return self._forward_fused(net, inp, corr, ii, jj, kk)
         net = self.norm(net + inp + self.corr(corr))
         ix, jx = fastba.neighbors(kk, jj)  # temporal neighbours of the same patch, on the device
         net = net + self.c1(self._neighbour(net, ix))

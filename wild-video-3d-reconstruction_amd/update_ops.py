@@ -47,3 +47,129 @@ def gather_rows(x, idx, dtype=None):
     H.check(H.lib().dpvo_gather_rows(H.dtype_code(x), H.ptr(x), x.stride(0), x.shape[0], H.ptr(idx), idx.numel(),
                                      x.shape[1], H.dtype_code(out), H.ptr(out), H.stream_of(x)))
     return out
+
+
+# ---------------------------------------------------------------------------
+# full-row fused GEMM (csrc/rowgemm.hip)
+# ---------------------------------------------------------------------------
+import ctypes as _ct  # noqa: E402
+
+RELU, SIGMOID, RES, GATE, LN, LN_RELU, HEADS = 1, 2, 4, 8, 16, 32, 64
+WIDTH = 384
+
+
+class RowGemmArgs(_ct.Structure):
+    _fields_ = [("A", _ct.c_void_p), ("lda", _ct.c_int64), ("a_idx", _ct.c_void_p), ("a_rows", _ct.c_int64),
+                ("W", _ct.c_void_p), ("K", _ct.c_int), ("N", _ct.c_int), ("bias", _ct.c_void_p),
+                ("zero_row", _ct.c_void_p), ("M", _ct.c_int64),
+                ("res32", _ct.c_void_p), ("ldr", _ct.c_int64), ("res16", _ct.c_void_p), ("res16_idx", _ct.c_void_p),
+                ("gate16", _ct.c_void_p),
+                ("ln_g", _ct.c_void_p), ("ln_b", _ct.c_void_p), ("ln_eps", _ct.c_float),
+                ("head_w", _ct.c_void_p), ("head_b", _ct.c_void_p), ("head_out", _ct.c_void_p),
+                ("out32", _ct.c_void_p), ("ldo32", _ct.c_int64), ("out16", _ct.c_void_p), ("ldo16", _ct.c_int64),
+                ("flags", _ct.c_int)]
+
+
+class RowAddArgs(_ct.Structure):
+    _fields_ = [("a", _ct.c_void_p), ("a_f16", _ct.c_int), ("lda", _ct.c_int64), ("M", _ct.c_int64),
+                ("b16", _ct.c_void_p), ("b_idx", _ct.c_void_p), ("b_rows", _ct.c_int64),
+                ("ln_g", _ct.c_void_p), ("ln_b", _ct.c_void_p), ("ln_eps", _ct.c_float),
+                ("out32", _ct.c_void_p), ("out16", _ct.c_void_p)]
+
+
+_ZEROS = {}
+
+
+def zero_row(device, K):
+    z = _ZEROS.get(device)
+    if z is None or z.numel() < K:
+        z = torch.zeros(max(K, 4096), dtype=torch.float16, device=device)
+        _ZEROS[device] = z
+    return z
+
+
+def pack_linear(weight, bias, kpad=64):
+    """nn.Linear(K -> 384) parameters as the kernel's operands: fp16 W [384][Kp]
+    (zero columns up to a multiple of 64) and fp16 bias -- what autocast casts them to."""
+    n, k = weight.shape
+    kp = (k + kpad - 1) // kpad * kpad
+    w = torch.zeros(n, kp, dtype=torch.float16, device=weight.device)
+    w[:, :k] = weight.detach()
+    return w.contiguous(), bias.detach().to(torch.float16).contiguous()
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+def rowgemm(A, W16, b16, flags=0, a_idx=None, M=None, res32=None, res16=None, res16_idx=None, gate16=None, ln=None,
+            heads=None, out32=None, out16=None, want32=False, want16=True):
+    """Y = epilogue(A W^T + b) over 384-wide rows (see include/dpvo_hot.h).
+    A: fp16 [R, >=Kp] (row-contiguous); a_idx: optional int64 [M] row gather.
+    ln = (gamma f32, beta f32, eps); heads = (W fp16 [4,384], b fp16 [4]).
+    Returns (out32, out16, head_out)."""
+    H.on_gpu(A, W16, b16)
+    if A.dtype != torch.float16 or W16.dtype != torch.float16 or b16.dtype != torch.float16:
+        raise RuntimeError("rowgemm: A, W and bias must be fp16")
+    if A.dim() != 2 or A.stride(1) != 1 or W16.shape[0] != WIDTH or not W16.is_contiguous():
+        raise RuntimeError("rowgemm: A must be [rows, K] row-contiguous and W [384, Kp] contiguous")
+    Kp = W16.shape[1]
+    if A.stride(0) < Kp:
+        raise RuntimeError(f"rowgemm: A's row stride {A.stride(0)} < padded K {Kp}")
+    dev = A.device
+    if a_idx is not None:
+        a_idx = H.idx64(a_idx)
+        M = a_idx.numel()
+    elif M is None:
+        M = A.shape[0]
+    if want32 and out32 is None:
+        out32 = torch.empty(M, WIDTH, dtype=torch.float32, device=dev)
+    if want16 and out16 is None:
+        out16 = torch.empty(M, WIDTH, dtype=torch.float16, device=dev)
+    head_out = torch.empty(M, 4, dtype=torch.float16, device=dev) if heads is not None else None
+    if res16_idx is not None:
+        res16_idx = H.idx64(res16_idx)
+    a = RowGemmArgs()
+    a.A, a.lda, a.a_idx, a.a_rows = _p(A), A.stride(0), _p(a_idx), A.shape[0]
+    a.W, a.K, a.N, a.bias, a.zero_row = _p(W16), Kp, WIDTH, _p(b16), _p(zero_row(dev, Kp))
+    a.M = M
+    a.res32, a.ldr = _p(res32), (res32.stride(0) if res32 is not None else 0)
+    a.res16, a.res16_idx, a.gate16 = _p(res16), _p(res16_idx), _p(gate16)
+    if ln is not None:
+        a.ln_g, a.ln_b, a.ln_eps = _p(ln[0]), _p(ln[1]), float(ln[2])
+    if heads is not None:
+        a.head_w, a.head_b, a.head_out = _p(heads[0]), _p(heads[1]), _p(head_out)
+    a.out32, a.ldo32 = _p(out32), (out32.stride(0) if out32 is not None else 0)
+    a.out16, a.ldo16 = _p(out16), (out16.stride(0) if out16 is not None else 0)
+    a.flags = int(flags)
+    for t, nm in ((res32, "res32"), (out32, "out32")):
+        if t is not None and (t.dtype != torch.float32 or t.stride(1) != 1):
+            raise RuntimeError(f"rowgemm: {nm} must be fp32 with contiguous rows")
+    for t, nm in ((res16, "res16"), (gate16, "gate16")):
+        if t is not None and (t.dtype != torch.float16 or not t.is_contiguous() or t.shape[-1] != WIDTH):
+            raise RuntimeError(f"rowgemm: {nm} must be contiguous fp16 [*, 384]")
+    H.check(H.lib().dpvo_rowgemm(_ct.byref(a), H.stream_of(A)))
+    return out32, out16, head_out
+
+
+def rowadd_ln(a, b16=None, b_idx=None, ln=None, want32=True, want16=True):
+    """v = a (+ b16[b_idx]) [-> LayerNorm] over 384-wide rows -> (out32, out16)."""
+    H.on_gpu(a)
+    if a.dim() != 2 or a.shape[1] != WIDTH or a.stride(1) != 1 or a.dtype not in (torch.float16, torch.float32):
+        raise RuntimeError("rowadd_ln: a must be [M, 384] fp16/fp32 with contiguous rows")
+    M, dev = a.shape[0], a.device
+    out32 = torch.empty(M, WIDTH, dtype=torch.float32, device=dev) if want32 else None
+    out16 = torch.empty(M, WIDTH, dtype=torch.float16, device=dev) if want16 else None
+    if b_idx is not None:
+        b_idx = H.idx64(b_idx)
+    args = RowAddArgs()
+    args.a, args.a_f16, args.lda, args.M = _p(a), int(a.dtype == torch.float16), a.stride(0), M
+    if b16 is not None:
+        if b16.dtype != torch.float16 or not b16.is_contiguous():
+            raise RuntimeError("rowadd_ln: b16 must be contiguous fp16 [*, 384]")
+        args.b16, args.b_idx, args.b_rows = _p(b16), _p(b_idx), b16.shape[0]
+    if ln is not None:
+        args.ln_g, args.ln_b, args.ln_eps = _p(ln[0]), _p(ln[1]), float(ln[2])
+    args.out32, args.out16 = _p(out32), _p(out16)
+    H.check(H.lib().dpvo_rowadd_ln(_ct.byref(args), H.stream_of(a)))
+    return out32, out16
