@@ -212,13 +212,35 @@ __device__ __forceinline__ bool failed(const BaParams& p) { return *(volatile in
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void ba_mark_kernel(BaParams p)
 {
-    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < p.E; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t k = p.kk[e];
-        if (k < 0 || k >= p.num_patches) {
-            atomicExch(p.status, -1);  // patch index out of range
-            continue;
+    // Consecutive edges mostly reference consecutive patches, so a wave's
+    // lanes hit 1-3 bitmap words: OR-reduce per word across the wave and issue
+    // one atomic per distinct word (same-address atomics serialise in L2).
+    const int lane = threadIdx.x & 63;
+    for (int64_t e0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~int64_t(63); e0 < p.E;
+         e0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = e0 + lane;
+        int64_t word = -1;
+        uint32_t bit = 0;
+        if (e < p.E) {
+            const int64_t k = p.kk[e];
+            if (k < 0 || k >= p.num_patches) {
+                atomicExch(p.status, -1);  // patch index out of range
+            } else {
+                word = k >> 5;
+                bit = 1u << (k & 31);
+            }
         }
-        atomicOr(&p.bits[k >> 5], 1u << (k & 31));
+        uint64_t pending = __ballot(word >= 0);
+        while (pending) {
+            const int leader = __ffsll((unsigned long long)pending) - 1;
+            const int64_t lw = __shfl(word, leader);
+            const bool mine = word == lw;
+            uint32_t b = mine ? bit : 0u;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) b |= __shfl_xor(b, o);
+            if (lane == leader) atomicOr(&p.bits[lw], b);
+            pending &= ~__ballot(mine);
+        }
     }
 }
 
@@ -466,6 +488,92 @@ __global__ __launch_bounds__(256) void ba_schur_kernel(BaParams p)
 // ---------------------------------------------------------------------------
 // dense solve (fp64 Cholesky) + pose retraction; one workgroup
 // ---------------------------------------------------------------------------
+// retraction of the N optimised poses by dX (ba_cuda.cu:160-188) and reset of
+// the pose accumulators; shared by both solve kernels
+__device__ void ba_retract_and_reset(BaParams& p, const double* yv, int tid, int nthreads)
+{
+    const int n = p.n6;
+    for (int i = tid; i < n; i += nthreads) p.dX[i] = (float)yv[i];
+    for (int i = tid; i < p.N; i += nthreads) {
+        float* P = p.poses + (int64_t)(p.t0 + i) * 7;
+        const float t0v[3] = {P[0], P[1], P[2]}, q0v[4] = {P[3], P[4], P[5], P[6]};
+        float xi[6], t1v[3], q1v[4];
+        for (int k = 0; k < 6; k++) xi[k] = (float)yv[6 * i + k];
+        retrSE3(xi, t0v, q0v, t1v, q1v);
+        P[0] = t1v[0]; P[1] = t1v[1]; P[2] = t1v[2];
+        P[3] = q1v[0]; P[4] = q1v[1]; P[5] = q1v[2]; P[6] = q1v[3];
+    }
+    for (int i = tid; i < n * n; i += nthreads) { p.B[i] = 0.f; p.S[i] = 0.f; }
+    for (int i = tid; i < n; i += nthreads) { p.v[i] = 0.f; p.y[i] = 0.f; }
+}
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// n6 <= 64: one wave, lane r owns row r; no block barriers.  Same arithmetic
+// as ba_solve_kernel (fp64 right-looking Cholesky, forward/backward solve).
+__global__ __launch_bounds__(64) void ba_solve_wave_kernel(BaParams p)
+{
+    __shared__ double A[64 * 65];
+    __shared__ double yv[64];
+    if (failed(p)) return;
+    const int n = p.n6, ld = n + 1, r = threadIdx.x;
+    for (int i = r; i < n * n; i += 64) {
+        const int a = i / n, b = i - a * n;
+        const int r0 = a < b ? a : b, c0 = a < b ? b : a;
+        double s = (double)(p.B[r0 * n + c0] - p.S[r0 * n + c0]);
+        if (a == b) s += 1e-4 * s + 1.0;
+        A[a * ld + b] = s;
+    }
+    if (r < n) yv[r] = (double)(p.v[r] - p.y[r]);
+    wave_sync_lds();
+    int fail = 0;
+    for (int j = 0; j < n; j++) {
+        const double djj = A[j * ld + j];
+        if (!(djj > 0.0)) {
+            fail = j + 1;
+            break;
+        }
+        const double ljj = sqrt(djj);
+        double lrj = 0.0;
+        if (r > j && r < n) {
+            lrj = A[r * ld + j] / ljj;
+            A[r * ld + j] = lrj;
+        }
+        wave_sync_lds();
+        if (r == j) A[j * ld + j] = ljj;
+        if (r > j && r < n) {
+            double* row = A + r * ld;
+            for (int c = j + 1; c <= r; c++) row[c] -= lrj * A[c * ld + j];
+        }
+        wave_sync_lds();
+    }
+    if (fail) {
+        if (r == 0) atomicExch(p.status, fail);
+        return;
+    }
+    // L z = y (row j of L is complete; lanes i > j update)
+    for (int j = 0; j < n; j++) {
+        const double yj = yv[j] / A[j * ld + j];
+        if (r > j && r < n) yv[r] -= A[r * ld + j] * yj;
+        wave_sync_lds();
+        if (r == j) yv[j] = yj;
+        wave_sync_lds();
+    }
+    // L^T x = z
+    for (int j = n - 1; j >= 0; j--) {
+        const double yj = yv[j] / A[j * ld + j];
+        if (r < j) yv[r] -= A[j * ld + r] * yj;
+        wave_sync_lds();
+        if (r == j) yv[j] = yj;
+        wave_sync_lds();
+    }
+    ba_retract_and_reset(p, yv, r, 64);
+}
+
 __global__ __launch_bounds__(256) void ba_solve_kernel(BaParams p)
 {
     extern __shared__ __attribute__((aligned(16))) double sA[];  // [n6][n6+1] + [n6]
@@ -526,21 +634,8 @@ __global__ __launch_bounds__(256) void ba_solve_kernel(BaParams p)
         for (int i = tid; i < j; i += blockDim.x) yv[i] -= A[j * ld + i] * yj;
         __syncthreads();
     }
-    for (int i = tid; i < n; i += blockDim.x) p.dX[i] = (float)yv[i];
     __syncthreads();
-    // pose retraction (ba_cuda.cu:160-188)
-    for (int i = tid; i < p.N; i += blockDim.x) {
-        float* P = p.poses + (int64_t)(p.t0 + i) * 7;
-        const float t0v[3] = {P[0], P[1], P[2]}, q0v[4] = {P[3], P[4], P[5], P[6]};
-        float xi[6], t1v[3], q1v[4];
-        for (int k = 0; k < 6; k++) xi[k] = (float)yv[6 * i + k];
-        retrSE3(xi, t0v, q0v, t1v, q1v);
-        P[0] = t1v[0]; P[1] = t1v[1]; P[2] = t1v[2];
-        P[3] = q1v[0]; P[4] = q1v[1]; P[5] = q1v[2]; P[6] = q1v[3];
-    }
-    // reset the pose accumulators for the next iteration
-    for (int i = tid; i < n * n; i += blockDim.x) { p.B[i] = 0.f; p.S[i] = 0.f; }
-    for (int i = tid; i < n; i += blockDim.x) { p.v[i] = 0.f; p.y[i] = 0.f; }
+    ba_retract_and_reset(p, yv, tid, blockDim.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -701,7 +796,10 @@ extern "C" int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches
             hipLaunchKernelGGL(ba_hessian_kernel<false>, dim3(gH), dim3(256), 0, s, p);
         if (N > 0) {
             hipLaunchKernelGGL(ba_schur_kernel, dim3(gS), dim3(256), lds_s, s, p);
-            hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), lds_v, s, p);
+            if (p.n6 <= 64)
+                hipLaunchKernelGGL(ba_solve_wave_kernel, dim3(1), dim3(64), 0, s, p);
+            else
+                hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), lds_v, s, p);
         }
         hipLaunchKernelGGL(ba_patch_kernel, dim3(gP), dim3(256), 0, s, p, N == 0 ? 1 : 0, it + 1 < iterations ? 1 : 0);
         DPVO_CHECK_LAUNCH();

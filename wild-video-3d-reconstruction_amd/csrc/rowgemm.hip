@@ -38,7 +38,8 @@ constexpr int RG_BM = 128, RG_BN = 384, RG_BK = 64, RG_THREADS = 512;
 constexpr int RG_A_STAGE = RG_BM * RG_BK * 2;   // 16 KB
 constexpr int RG_W_STAGE = RG_BN * RG_BK * 2;   // 48 KB
 constexpr int RG_STAGE = RG_A_STAGE + RG_W_STAGE;
-constexpr int RG_LDS = 2 * RG_STAGE;            // 128 KB
+constexpr int RG_EXTRA = 32 * 1024;             // + the consumed stage = the 96 KB y tile
+constexpr int RG_LDS = 2 * RG_STAGE + RG_EXTRA;  // 160 KB: the whole CU
 
 enum {
     RG_RELU = DPVO_RG_RELU, RG_SIGMOID = DPVO_RG_SIGMOID, RG_RES = DPVO_RG_RES, RG_GATE = DPVO_RG_GATE,
@@ -77,93 +78,156 @@ __device__ __forceinline__ float wave_sum(float s)
            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 48));
 }
 
-constexpr int RG_YS = 784;  // y-tile row stride in bytes (768 + 16: conflict-free b16 writes)
-
-// One output row: lane owns columns 2*lane + 128*j (j < 3) as float2.
-template <int FLAGS>
-__device__ __forceinline__ void epilogue_row(const dpvo_rowgemm_args& p, const char* yrow, int64_t row, int lane)
+// y tile: 128 rows x 768 B (fp16 row-major) spread over the consumed stage
+// buffer (64 KB) and the extra region (32 KB); 32-B granules XOR-swizzled by
+// (row/4)&3 so the C-layout b16 writes of 4 row groups hit distinct banks.
+__device__ __forceinline__ int ytile_off(int cur_buf, int r, int byte)
 {
-    if (row >= p.M) return;
-    float2_t v[3];
+    const int o = r * 768 + (byte ^ (((r >> 2) & 3) << 5));
+    return o < 65536 ? cur_buf * 65536 + o : 2 * RG_STAGE + (o - 65536);
+}
+
+__device__ __forceinline__ float fast_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+
+struct EpiConsts {
+    float2_t g[3], b[3];     // LayerNorm weight / bias at this lane's columns
+    float2_t hw[4][3];       // head weights (fp16 values)
+    float hb[4];
+};
+
+template <int FLAGS>
+__device__ __forceinline__ void load_consts(const dpvo_rowgemm_args& p, int lane, EpiConsts& k)
+{
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-        const half2_t y = *(const half2_t*)(yrow + (128 * j + 2 * lane) * 2);
-        v[j] = float2_t{(float)y.x, (float)y.y};
-    }
-    if (FLAGS & (RG_RES | RG_GATE)) {
-        const float* r32 = (const float*)p.res32 + row * p.ldr;
-        const half_t* r16 = nullptr;
-        if ((FLAGS & RG_RES) && p.res16) {
-            const int64_t s = p.res16_idx ? p.res16_idx[row] : row;
-            if (s >= 0) r16 = (const half_t*)p.res16 + s * RG_BN;
+        const int c = 128 * j + 2 * lane;
+        if (FLAGS & RG_LN) {
+            k.g[j] = *(const float2_t*)(p.ln_g + c);
+            k.b[j] = *(const float2_t*)(p.ln_b + c);
         }
+        if (FLAGS & RG_HEADS) {
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const int c = 128 * j + 2 * lane;
-            float2_t base = *(const float2_t*)(r32 + c);
-            if (FLAGS & RG_GATE) {
-                const half2_t g = *(const half2_t*)((const half_t*)p.gate16 + row * RG_BN + c);
-                v[j] = base + float2_t{hround((float)g.x * v[j].x), hround((float)g.y * v[j].y)};
-            } else {
-                if (r16) {
-                    const half2_t b = *(const half2_t*)(r16 + c);
-                    base += float2_t{(float)b.x, (float)b.y};
-                }
-                v[j] = base + v[j];
+            for (int q = 0; q < 4; q++) {
+                const half2_t w = *(const half2_t*)((const half_t*)p.head_w + q * RG_BN + c);
+                k.hw[q][j] = float2_t{(float)w.x, (float)w.y};
             }
         }
     }
-    if (FLAGS & RG_LN) {
-        float s = 0.f;
+    if (FLAGS & RG_HEADS) {
 #pragma unroll
-        for (int j = 0; j < 3; j++) s += v[j].x + v[j].y;
-        const float mean = wave_sum(s) * (1.f / RG_BN);
-        float q = 0.f;
+        for (int q = 0; q < 4; q++) k.hb[q] = (float)((const half_t*)p.head_b)[q];
+    }
+}
+
+// R whole output rows per wave (lane owns columns 2*lane + 128*j, j < 3):
+// all of the batch's loads are issued before any row's reductions.
+template <int FLAGS, int R>
+__device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, const char* smem, int cur_buf, int lrow0,
+                                              int64_t row0, int lane, const EpiConsts& k)
+{
+    float2_t v[R][3];
+    int64_t rows[R];
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+        rows[q] = row0 + q < p.M ? row0 + q : p.M - 1;   // clamped for loads; stores skip rows >= M
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-            const float2_t d = v[j] - mean;
-            q += d.x * d.x + d.y * d.y;
+            const half2_t y = *(const half2_t*)(smem + ytile_off(cur_buf, lrow0 + q, (128 * j + 2 * lane) * 2));
+            v[q][j] = float2_t{(float)y.x, (float)y.y};
         }
-        const float rstd = rsqrtf(wave_sum(q) * (1.f / RG_BN) + p.ln_eps);
+    }
+    if (FLAGS & (RG_RES | RG_GATE)) {
+        float2_t base[R][3];
+        float2_t add[R][3];
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const int c = 128 * j + 2 * lane;
-            const float2_t g = *(const float2_t*)(p.ln_g + c);
-            const float2_t b = *(const float2_t*)(p.ln_b + c);
-            v[j] = (v[j] - mean) * rstd * g + b;
-            if (FLAGS & RG_LN_RELU) v[j] = float2_t{fmaxf(v[j].x, 0.f), fmaxf(v[j].y, 0.f)};
+        for (int q = 0; q < R; q++) {
+            const float* r32 = (const float*)p.res32 + rows[q] * p.ldr;
+            const half_t* r16 = nullptr;
+            if (FLAGS & RG_GATE) {
+                r16 = (const half_t*)p.gate16 + rows[q] * RG_BN;
+            } else if (p.res16) {
+                const int64_t s = p.res16_idx ? p.res16_idx[rows[q]] : rows[q];
+                r16 = (const half_t*)p.res16 + (s >= 0 ? s : 0) * RG_BN;
+                if (s < 0) r16 = nullptr;
+            }
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const int c = 128 * j + 2 * lane;
+                base[q][j] = *(const float2_t*)(r32 + c);
+                half2_t h = half2_t{(half_t)0, (half_t)0};
+                if (r16) h = *(const half2_t*)(r16 + c);
+                add[q][j] = float2_t{(float)h.x, (float)h.y};
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < R; q++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                if (FLAGS & RG_GATE)   // x + fp16(gate * res)   (blocks.py:30, fp16 product)
+                    v[q][j] = base[q][j] + float2_t{hround(add[q][j].x * v[q][j].x), hround(add[q][j].y * v[q][j].y)};
+                else                   // (res32 + res16) + y
+                    v[q][j] = (base[q][j] + add[q][j]) + v[q][j];
+            }
+    }
+    if (FLAGS & RG_LN) {
+        float mean[R];
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; j++) s += v[q][j].x + v[q][j].y;
+            mean[q] = wave_sum(s) * (1.f / RG_BN);
+        }
+#pragma unroll
+        for (int q = 0; q < R; q++) {
+            float s = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const float2_t d = v[q][j] - mean[q];
+                s += d.x * d.x + d.y * d.y;
+            }
+            const float rstd = rsqrtf(wave_sum(s) * (1.f / RG_BN) + p.ln_eps);
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                v[q][j] = (v[q][j] - mean[q]) * rstd * k.g[j] + k.b[j];
+                if (FLAGS & RG_LN_RELU) v[q][j] = float2_t{fmaxf(v[q][j].x, 0.f), fmaxf(v[q][j].y, 0.f)};
+            }
         }
     }
     if (FLAGS & RG_HEADS) {
         // d = W_d relu(v) + b_d ; w = sigmoid(W_w relu(v) + b_w)   (fp16 operands, fp32 accumulate)
-        float d[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const int c = 128 * j + 2 * lane;
-            const float x0 = hround(fmaxf(v[j].x, 0.f)), x1 = hround(fmaxf(v[j].y, 0.f));
+        for (int q = 0; q < R; q++) {
+            float d[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const half2_t w = *(const half2_t*)((const half_t*)p.head_w + q * RG_BN + c);
-                d[q] += x0 * (float)w.x + x1 * (float)w.y;
+            for (int j = 0; j < 3; j++) {
+                const float x0 = hround(fmaxf(v[q][j].x, 0.f)), x1 = hround(fmaxf(v[q][j].y, 0.f));
+#pragma unroll
+                for (int h = 0; h < 4; h++) d[h] += x0 * k.hw[h][j].x + x1 * k.hw[h][j].y;
             }
-        }
-        half_t o[4];
+            half_t o[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            float h = hround(wave_sum(d[q]) + (float)((const half_t*)p.head_b)[q]);
-            if (q >= 2) h = hround(1.f / (1.f + expf(-h)));
-            o[q] = (half_t)h;
-        }
-        if (lane == 0) {
-            typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
-            *(h4_t*)((half_t*)p.head_out + row * 4) = h4_t{o[0], o[1], o[2], o[3]};
+            for (int h = 0; h < 4; h++) {
+                float z = hround(wave_sum(d[h]) + k.hb[h]);
+                if (h >= 2) z = hround(fast_sigmoid(z));
+                o[h] = (half_t)z;
+            }
+            if (lane == 0 && row0 + q < p.M) {
+                typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+                *(h4_t*)((half_t*)p.head_out + (row0 + q) * 4) = h4_t{o[0], o[1], o[2], o[3]};
+            }
         }
     }
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int c = 128 * j + 2 * lane;
-        if (p.out32) *(float2_t*)((float*)p.out32 + row * p.ldo32 + c) = v[j];
-        if (p.out16) *(half2_t*)((half_t*)p.out16 + row * p.ldo16 + c) = half2_t{(half_t)v[j].x, (half_t)v[j].y};
+    for (int q = 0; q < R; q++) {
+        if (row0 + q >= p.M) continue;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int c = 128 * j + 2 * lane;
+            if (p.out32) *(float2_t*)((float*)p.out32 + (row0 + q) * p.ldo32 + c) = v[q][j];
+            if (p.out16)
+                *(half2_t*)((half_t*)p.out16 + (row0 + q) * p.ldo16 + c) = half2_t{(half_t)v[q][j].x, (half_t)v[q][j].y};
+        }
     }
 }
 
@@ -240,6 +304,8 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm_kernel(dpvo_rowgemm_arg
         w_sw[nt] = (n >> 1) & 7;
     }
 
+    EpiConsts kc;
+    load_consts<FLAGS>(p, lane, kc);
     int64_t tile = blockIdx.x;
     int ks = 0, buf = 0;
     issue(0, tile, 0);
@@ -284,44 +350,34 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm_kernel(dpvo_rowgemm_arg
         if (!last) continue;
 
         // ------------------------------ epilogue ------------------------------
-        // Per 64-row half h: the waves owning it (wm == h) write y16 = fp16(acc + b)
-        // [act] into the just-consumed stage buffer; then every wave finishes 8
-        // whole rows (lanes over columns: coalesced loads/stores, DPP+readlane
-        // row reductions).  The other stage buffer is loading the next tile.
-        char* yt = smem + cur_buf * RG_STAGE;
+        // Every wave writes y16 = fp16(acc + b) [act] of its 64x96 block into
+        // the y tile (consumed stage buffer + extra region), then finishes 16
+        // whole rows: lanes over columns, coalesced loads/stores, DPP+readlane
+        // row reductions.  The other stage buffer is loading the next tile.
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            if (wm == h) {
+        for (int nt = 0; nt < 6; nt++) {
+            const int cl = wn * 96 + nt * 16 + fr;
+            const float bias = (float)((const half_t*)p.bias)[cl];
 #pragma unroll
-                for (int nt = 0; nt < 6; nt++) {
-                    const int cl = wn * 96 + nt * 16 + fr;
-                    const float bias = (float)((const half_t*)p.bias)[cl];
+            for (int mt = 0; mt < 4; mt++)
 #pragma unroll
-                    for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            half_t y = (half_t)(acc[mt][nt][r] + bias);
-                            if (FLAGS & RG_RELU) y = y > (half_t)0 ? y : (half_t)0;
-                            if (FLAGS & RG_SIGMOID) y = (half_t)(1.f / (1.f + expf(-(float)y)));
-                            *(half_t*)(yt + (mt * 16 + fq * 4 + r) * RG_YS + cl * 2) = y;
-                            acc[mt][nt][r] = 0.f;
-                        }
+                for (int r = 0; r < 4; r++) {
+                    half_t y = (half_t)(acc[mt][nt][r] + bias);
+                    if (FLAGS & RG_RELU) y = y > (half_t)0 ? y : (half_t)0;
+                    if (FLAGS & RG_SIGMOID) y = (half_t)fast_sigmoid((float)y);
+                    *(half_t*)(smem + ytile_off(cur_buf, wm * 64 + mt * 16 + fq * 4 + r, cl * 2)) = y;
+                    acc[mt][nt][r] = 0.f;
                 }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-#pragma unroll
-            for (int qb = 0; qb < 8; qb += 4) {
-#pragma unroll
-                for (int q = qb; q < qb + 4; q++)
-                    epilogue_row<FLAGS>(p, yt + (wave * 8 + q) * RG_YS, cur_tile * RG_BM + h * 64 + wave * 8 + q, lane);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        epilogue_rows<FLAGS, 8>(p, smem, cur_buf, wave * 16, cur_tile * RG_BM + wave * 16, lane, kc);
+        __builtin_amdgcn_sched_barrier(0);
+        epilogue_rows<FLAGS, 8>(p, smem, cur_buf, wave * 16 + 8, cur_tile * RG_BM + wave * 16 + 8, lane, kc);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
     }
 }
 
