@@ -188,6 +188,23 @@ int dpvo_softagg_forward(int dtype, const void* f, int64_t ldf, const void* s, i
                          int64_t num_edges, int D, int64_t groups, float eps, void* y, void* workspace,
                          size_t workspace_bytes, void* stream);
 
+/* Sync-free group-by: torch.unique(key, return_inverse=True) plus the CSR of
+ * the groups, without a host round trip.  gid[e] = rank of key[e] among the
+ * distinct keys (ascending, = torch.unique's inverse); group g's edges are
+ * perm[offs[g] .. offs[g+1]) in ascending edge order; *groups (device int64)
+ * = number of distinct keys.  Keys must lie in [0, 2^key_bits), key_bits <= 32.
+ * offs has n+1 entries, perm n. */
+size_t dpvo_group_by_workspace_bytes(int64_t n);
+int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_t* gid, int* offs, int* perm, int64_t* groups,
+                  void* workspace, size_t workspace_bytes, void* stream);
+
+/* dpvo_softagg_forward over a CSR from dpvo_group_by; the group count is read
+ * from device memory (*groups <= max_groups); y rows >= *groups are untouched.
+ * Sums run in ascending edge order: deterministic for every group size. */
+int dpvo_softagg_csr(int dtype, const void* f, int64_t ldf, const void* s, int64_t lds, const int* offs,
+                     const int* perm, const int64_t* groups, int64_t max_groups, int D, float eps, void* y,
+                     void* stream);
+
 /* Full-row fused GEMM of the update operator (dpvo/net.py:75-93 and
  * blocks.py GatedResidual under autocast), N = 384 output columns per row:
  *   y16  = fp16(A W^T + bias)            A fp16 [M][K] rows at A + r*lda, or
@@ -219,6 +236,7 @@ typedef struct dpvo_rowgemm_args {
     const void* head_w; const void* head_b; void* head_out;
     void* out32; int64_t ldo32; void* out16; int64_t ldo16;
     int flags;
+    const int64_t* M_dev;   /* optional: row count read on the device (M is then the upper bound) */
 } dpvo_rowgemm_args;
 int dpvo_rowgemm(const dpvo_rowgemm_args* args, void* stream);
 

@@ -91,3 +91,54 @@ def test_errors():
         update_ops.gather_rows(x, torch.zeros(4, dtype=torch.int64, device="cuda"))  # odd D
     with pytest.raises(RuntimeError):
         update_ops.softagg(x.cpu(), x.cpu(), torch.zeros(10, dtype=torch.int64), 1)
+
+
+@pytest.mark.parametrize("n,hi", [(1, 5), (1000, 40), (95424, 4416 * 5), (5000, 2 ** 31 - 1)])
+def test_group_by_matches_torch_unique(n, hi):
+    """Device group-by == torch.unique(return_inverse=True); CSR lists each group's edges ascending."""
+    import update_ops
+    key = torch.randint(0, hi, (n,), device="cuda")
+    gid, offs, perm, G = update_ops.group_by(key)
+    uniq, inv = torch.unique(key, return_inverse=True)
+    assert int(G.item()) == uniq.numel()
+    assert torch.equal(gid, inv)
+    g = int(G.item())
+    offs, perm = offs[: g + 1].long().cpu(), perm.long().cpu()
+    assert offs[0] == 0 and offs[-1] == n
+    inv_c = inv.cpu()
+    for k in range(0, g, max(1, g // 50)):
+        members = perm[offs[k]: offs[k + 1]]
+        assert (members[1:] > members[:-1]).all()
+        assert (inv_c[members] == k).all()
+
+
+def test_group_by_empty():
+    import update_ops
+    gid, offs, perm, G = update_ops.group_by(torch.zeros(0, dtype=torch.int64, device="cuda"))
+    assert int(G.item()) == 0 and gid.numel() == 0
+
+
+def test_softagg_csr_matches_oracle_and_dense_path():
+    import update_ops
+    E, D = 20000, 384
+    fs = torch.randn(E, 2 * D, device="cuda").half()
+    key = torch.randint(0, 3000, (E,), device="cuda") * 12345 + 11
+    gid, offs, perm, G = update_ops.group_by(key)
+    g = int(G.item())
+    y = update_ops.softagg_csr(fs[:, :D], fs[:, D:], offs, perm, G, E)[:g]
+    want = oracle.softagg(fs[:, :D].double().cpu().numpy(), fs[:, D:].double().cpu().numpy(), gid.cpu().numpy(), g)
+    np.testing.assert_allclose(y.double().cpu().numpy(), want, rtol=2e-3, atol=2e-3)
+    dense = update_ops.softagg(fs[:, :D], fs[:, D:], gid, g)
+    assert torch.equal(y, dense)   # same ascending order, same arithmetic
+
+
+def test_rowgemm_device_row_count():
+    """rowgemm with M read on the device: rows past *M_dev are left untouched."""
+    import update_ops as U
+    A = torch.randn(1000, 384, device="cuda").half()
+    W16, b16 = U.pack_linear(torch.randn(384, 384, device="cuda") * 0.05, torch.randn(384, device="cuda") * 0.1)
+    out = torch.full((1000, 384), 7.0, device="cuda").half()
+    U.rowgemm(A, W16, b16, out16=out, M_dev=torch.tensor([300], device="cuda"))
+    _, ref, _ = U.rowgemm(A, W16, b16)
+    assert torch.equal(out[:300], ref[:300])
+    assert (out[300:] == 7.0).all()

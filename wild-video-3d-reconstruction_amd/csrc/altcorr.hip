@@ -23,6 +23,8 @@
 //   reference's exact rounding sequence and written in the caller's layout.
 //   Boxes wider than 10x10 fall back, inside the same kernel, to one 8x8
 //   window per patch pixel.
+#include <stdlib.h>
+
 #include "common.hpp"
 
 namespace dpvo {
@@ -46,6 +48,7 @@ struct CorrFastParams {
     float scale[2];
     half_t* out;
     int64_t o_b, o_e, o_l, o_x, o_y, o_p;
+    const uint32_t* f1tab;   // [B*N1][C][5] packed patch-feature pairs (corr_pack_kernel)
 };
 
 __device__ __forceinline__ half2_t as_h2(uint32_t v) { return __builtin_bit_cast(half2_t, v); }
@@ -260,6 +263,216 @@ __global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_fast_kernel(Cor
 
     // ---- bilinear epilogue, exact rounding sequence of correlation_kernel.cu:221-232,
     // outputs enumerated in the stacked layout's memory order (x, y, pixel, level)
+    half_t* ob = p.out + b * p.o_b + (int64_t)e * p.o_e;
+    for (int o = tid; o < NLEV * NP * DO * DO; o += NT) {
+        const int lev = o % NLEV;
+        int r = o / NLEV;
+        const int q = r % NP; r /= NP;
+        const int a = r % DO;
+        const int bx = r / DO;
+        const LevelMeta& m = meta[lev];
+        const int bw = m.fast ? m.bw : D;
+        const int oy = m.fast ? m.fy[q] - (int)wrap_add(m.oy, R) : 0;
+        const int ox = m.fast ? m.fx[q] - (int)wrap_add(m.ox, R) : 0;
+        const half_t* t = &raw[lev][q][(oy + a) * bw + (ox + bx)];
+        const half_t c00 = t[0], c01 = t[1], c10 = t[bw], c11 = t[bw + 1];
+        const float xq = m.xs[q], yq = m.ys[q];
+        const half_t dx = (half_t)(xq - floorf(xq));
+        const half_t dy = (half_t)(yq - floorf(yq));
+        const half_t one = (half_t)1.0f;
+        const half_t omdx = one - dx, omdy = one - dy;
+        half_t v = hmul(hmul(omdx, omdy), c00);
+        v = hadd(v, hmul(hmul(dx, omdy), c01));
+        v = hadd(v, hmul(hmul(omdx, dy), c10));
+        v = hadd(v, hmul(hmul(dx, dy), c11));
+        ob[bx * p.o_x + a * p.o_y + q * p.o_p + lev * p.o_l] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// v3 fast path: the patch features are uniform over the workgroup, so they are
+// read as SCALAR operands (s_load from a per-call packed table) instead of LDS
+// broadcasts -- no ds_read latency in the chain, 40 fewer VGPRs (occupancy).
+// ---------------------------------------------------------------------------
+typedef unsigned int u32x16 __attribute__((ext_vector_type(16)));
+
+// gmap [B][N1][C][3][3] -> table [B*N1][C][5] dwords: (p0,p1)(p2,p3)(p4,p5)(p6,p7)(p8,0)
+__global__ __launch_bounds__(256) void corr_pack_kernel(const half_t* __restrict__ gmap, int64_t gs0, int64_t gs1,
+                                                        int64_t gs2, int64_t gs3, int64_t gs4, int B, int N1, int C,
+                                                        uint32_t* __restrict__ tab)
+{
+    const int64_t total = (int64_t)B * N1 * C;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(t % C);
+        const int64_t bn = t / C;
+        const int n = (int)(bn % N1), b = (int)(bn / N1);
+        const half_t* g = gmap + b * gs0 + n * gs1 + c * gs2;
+        half_t v[10];
+#pragma unroll
+        for (int q = 0; q < 9; q++) v[q] = g[(q / 3) * gs3 + (q % 3) * gs4];
+        v[9] = (half_t)0;
+        uint32_t* o = tab + t * 5;
+#pragma unroll
+        for (int q = 0; q < 5; q++) o[q] = __builtin_bit_cast(uint32_t, (half2_t){v[2 * q], v[2 * q + 1]});
+    }
+}
+
+template <int NLEV, int C8>
+__global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_sfast_kernel(CorrFastParams p)
+{
+    using namespace corr;
+    constexpr int NT = FastThreads<NLEV>::value;
+    constexpr int C = C8 * 8;
+    __shared__ half_t raw[NLEV][NP][BOX * BOX];
+    __shared__ LevelMeta meta[NLEV];
+
+    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
+    const int b = bid / p.E, e = bid - b * p.E;
+    const int tid = threadIdx.x;
+    const int ix = (int)p.ii[e];
+    const int jx = (int)p.jj[e];
+    const bool ix_ok = ix >= 0 && ix < p.N1;
+
+    // ---- per-(level, patch pixel) coordinates and floors: 9*NLEV threads
+    if (tid < NLEV * NP) {
+        const int lev = tid / NP, q = tid - lev * NP;
+        const float sc = p.scale[lev];
+        const float* cb = p.coords + b * p.c_s[0] + (int64_t)e * p.c_s[1];
+        const int64_t o = (q / PS) * p.c_s[3] + (q % PS) * p.c_s[4];
+        const float x = cb[o] / sc, y = cb[p.c_s[2] + o] / sc;
+        LevelMeta& m = meta[lev];
+        m.xs[q] = x; m.ys[q] = y;
+        m.fy[q] = floor_to_int_sat(y);
+        m.fx[q] = floor_to_int_sat(x);
+    }
+    __syncthreads();
+    if (tid < NLEV) {
+        LevelMeta& m = meta[tid];
+        int ymin = 0x7fffffff, ymax = (int)0x80000000u, xmin = 0x7fffffff, xmax = (int)0x80000000u;
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            ymin = min(ymin, m.fy[q]); ymax = max(ymax, m.fy[q]);
+            xmin = min(xmin, m.fx[q]); xmax = max(xmax, m.fx[q]);
+        }
+        m.fast = ((int64_t)ymax - ymin) <= 2 && ((int64_t)xmax - xmin) <= 2;
+        m.oy = wrap_add(ymin, -R);
+        m.ox = wrap_add(xmin, -R);
+        m.bh = m.fast ? (ymax - ymin) + D : D;
+        m.bw = m.fast ? (xmax - xmin) + D : D;
+        m.nslots = m.fast ? m.bh * m.bw : NP * D * D;
+    }
+    __syncthreads();
+    const int n0 = meta[0].nslots;
+    const int total = NLEV == 2 ? n0 + meta[NLEV - 1].nslots : n0;
+
+    struct Slot { int lev, q_only, u; bool act, inb; const uint4* ptr; };
+    auto decode = [&](int slot) {
+        Slot s{0, -1, 0, false, false, nullptr};
+        s.act = slot < total;
+        const int sl = s.act ? slot : 0;
+        s.lev = (NLEV == 2 && sl >= n0) ? NLEV - 1 : 0;
+        const LevelMeta& m = meta[s.lev];
+        const int loc = s.lev ? sl - n0 : sl;
+        int gy, gx;
+        if (m.fast) {
+            const int uy = loc / m.bw, ux = loc - uy * m.bw;
+            gy = wrap_add(m.oy, uy); gx = wrap_add(m.ox, ux);
+            s.u = loc;
+        } else {
+            const int q = loc / (D * D), u = loc - q * (D * D);
+            const int uy = u / D, ux = u - uy * D;
+            gy = wrap_add(m.fy[q], uy - R); gx = wrap_add(m.fx[q], ux - R);
+            s.q_only = q;
+            s.u = u;
+        }
+        const int lv = s.lev;
+        s.inb = s.act && ix_ok && jx >= 0 && jx < p.N2[lv] && gy >= 0 && gy < p.H2[lv] && gx >= 0 && gx < p.W2[lv];
+        const half_t* base = p.fmap[lv] + b * p.f_s0[lv];
+        s.ptr = reinterpret_cast<const uint4*>(
+            s.inb ? base + (int64_t)jx * p.f_s1[lv] + (int64_t)gy * p.f_s3[lv] + (int64_t)gx * p.f_s4[lv] : base);
+        return s;
+    };
+
+    // this patch's packed features: 4 channels = 20 dwords (s_load x16 + x4)
+    const uint32_t* T = p.f1tab + ((int64_t)b * p.N1 + (ix_ok ? ix : 0)) * C * 5;
+
+    for (int base = 0; base < total; base += NT) {
+        const Slot cur = decode(base + tid);
+        half2_t acc[NPAIR];
+#pragma unroll
+        for (int q = 0; q < NPAIR; q++) acc[q] = (half2_t){(half_t)0, (half_t)0};
+        // Hand-scheduled: pixel-row chunks by asm global loads (4 in flight,
+        // counted vmcnt), patch features by asm scalar loads one 4-channel step
+        // ahead (SMEM returns out of order: lgkmcnt(0) per step).
+        u32x4 w[C8];
+        u32x16 fa16, fb16;
+        u32x4 fa4, fb4;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(w[k]) : "v"(cur.ptr), "i"(k * 16));
+        asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x40"
+                     : "=s"(fa16), "=s"(fa4) : "s"(T));
+#pragma unroll
+        for (int k = 0; k < C8; k++) {
+            // chunk k holds channels 8k..8k+7 = steps 2k, 2k+1
+            switch (C8 - 1 - k < 3 ? C8 - 1 - k : 3) {   // outstanding younger chunks
+            case 3: asm volatile("s_waitcnt vmcnt(3)" : "+v"(w[k])); break;
+            case 2: asm volatile("s_waitcnt vmcnt(2)" : "+v"(w[k])); break;
+            case 1: asm volatile("s_waitcnt vmcnt(1)" : "+v"(w[k])); break;
+            default: asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[k])); break;
+            }
+            if (k + 4 < C8)
+                asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(w[k + 4]) : "v"(cur.ptr), "i"((k + 4) * 16));
+#pragma unroll
+            for (int hs = 0; hs < 2; hs++) {
+                const int step = 2 * k + hs;
+                u32x16& c16 = (step & 1) ? fb16 : fa16;
+                u32x4& c4 = (step & 1) ? fb4 : fa4;
+                u32x16& n16 = (step & 1) ? fa16 : fb16;
+                u32x4& n4 = (step & 1) ? fa4 : fb4;
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(c16), "+s"(c4));
+                if (step + 1 < 2 * C8)
+                    asm volatile("s_load_dwordx16 %0, %2, %3\n\ts_load_dwordx4 %1, %2, %4"
+                                 : "=s"(n16), "=s"(n4) : "s"(T), "i"((step + 1) * 80), "i"((step + 1) * 80 + 64));
+                const uint32_t fs[20] = {c16[0], c16[1], c16[2], c16[3], c16[4], c16[5], c16[6], c16[7],
+                                         c16[8], c16[9], c16[10], c16[11], c16[12], c16[13], c16[14], c16[15],
+                                         c4[0], c4[1], c4[2], c4[3]};
+                const uint32_t wd[2] = {hs ? w[k][2] : w[k][0], hs ? w[k][3] : w[k][1]};
+#pragma unroll
+                for (int j = 0; j < 2; j++) {
+                    const half2_t wv = as_h2(wd[j]);
+#pragma unroll
+                    for (int hsel = 0; hsel < 2; hsel++) {
+                        const int c = 2 * j + hsel;
+                        const half_t ws = hsel ? wv.y : wv.x;
+                        const half2_t wb = {ws, ws};
+#pragma unroll
+                        for (int q = 0; q < NPAIR; q++) acc[q] = acc[q] + wb * as_h2(fs[c * 5 + q]);
+                    }
+                }
+                // keep this step's arithmetic ahead of the next step's (volatile) loads:
+                // LLVM otherwise sinks the pure VALU chain and spills the SGPR operands
+                asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if (cur.act) {
+            const half_t z = (half_t)0;
+            const half_t sv[NP] = {acc[0].x, acc[0].y, acc[1].x, acc[1].y, acc[2].x,
+                                   acc[2].y, acc[3].x, acc[3].y, acc[4].x};
+            if (cur.q_only < 0) {
+#pragma unroll
+                for (int q = 0; q < NP; q++) raw[cur.lev][q][cur.u] = cur.inb ? sv[q] : z;
+            } else {
+                half_t v = z;
+#pragma unroll
+                for (int q = 0; q < NP; q++) if (q == cur.q_only) v = sv[q];
+                raw[cur.lev][cur.q_only][cur.u] = cur.inb ? v : z;
+            }
+        }
+    }
+    __syncthreads();
+
     half_t* ob = p.out + b * p.o_b + (int64_t)e * p.o_e;
     for (int o = tid; o < NLEV * NP * DO * DO; o += NT) {
         const int lev = o % NLEV;
@@ -506,6 +719,28 @@ int launch_fast(int nlev, const void* gmap, const int64_t* gsz, const int64_t* g
     p.o_b = ostr[0]; p.o_e = ostr[1]; p.o_l = ostr[2]; p.o_x = ostr[3]; p.o_y = ostr[4]; p.o_p = ostr[5];
     const int64_t nblk = (int64_t)p.B * p.E;
     if (nblk == 0) return 0;
+    static const int version = [] {
+        const char* v = getenv("DPVO_CORR_KERNEL");
+        return v ? atoi(v) : 3;
+    }();
+    if (version == 3) {
+        // patch features -> scalar-load table (stream-ordered scratch)
+        const size_t tab_bytes = (size_t)p.B * p.N1 * p.C * 5 * 4;
+        void* tab = nullptr;
+        if (hipMallocAsync(&tab, tab_bytes, stream) != hipSuccess) return 2;
+        const int64_t np = (int64_t)p.B * p.N1 * p.C;
+        hipLaunchKernelGGL(corr_pack_kernel, dim3(grid_for(np, 256, 8192)), dim3(256), 0, stream, p.gmap, p.g_s[0],
+                           p.g_s[1], p.g_s[2], p.g_s[3], p.g_s[4], p.B, p.N1, p.C, (uint32_t*)tab);
+        p.f1tab = (const uint32_t*)tab;
+        if (nlev == 2)
+            hipLaunchKernelGGL((corr_sfast_kernel<2, 16>), dim3((unsigned)nblk), dim3(FastThreads<2>::value), 0,
+                               stream, p);
+        else
+            hipLaunchKernelGGL((corr_sfast_kernel<1, 16>), dim3((unsigned)nblk), dim3(FastThreads<1>::value), 0,
+                               stream, p);
+        (void)hipFreeAsync(tab, stream);
+        return 0;
+    }
     if (nlev == 2)
         hipLaunchKernelGGL((corr_fast_kernel<2, 16>), dim3((unsigned)nblk), dim3(FastThreads<2>::value), 0, stream, p);
     else

@@ -122,14 +122,14 @@ __device__ __forceinline__ void load_consts(const dpvo_rowgemm_args& p, int lane
 // R whole output rows per wave (lane owns columns 2*lane + 128*j, j < 3):
 // all of the batch's loads are issued before any row's reductions.
 template <int FLAGS, int R>
-__device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, const char* smem, int cur_buf, int lrow0,
-                                              int64_t row0, int lane, const EpiConsts& k)
+__device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, int64_t M, const char* smem, int cur_buf,
+                                              int lrow0, int64_t row0, int lane, const EpiConsts& k)
 {
     float2_t v[R][3];
     int64_t rows[R];
 #pragma unroll
     for (int q = 0; q < R; q++) {
-        rows[q] = row0 + q < p.M ? row0 + q : p.M - 1;   // clamped for loads; stores skip rows >= M
+        rows[q] = row0 + q < M ? row0 + q : M - 1;   // clamped for loads; stores skip rows >= M
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             const half2_t y = *(const half2_t*)(smem + ytile_off(cur_buf, lrow0 + q, (128 * j + 2 * lane) * 2));
@@ -212,7 +212,7 @@ __device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, const 
                 if (h >= 2) z = hround(fast_sigmoid(z));
                 o[h] = (half_t)z;
             }
-            if (lane == 0 && row0 + q < p.M) {
+            if (lane == 0 && row0 + q < M) {
                 typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
                 *(h4_t*)((half_t*)p.head_out + (row0 + q) * 4) = h4_t{o[0], o[1], o[2], o[3]};
             }
@@ -220,7 +220,7 @@ __device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, const 
     }
 #pragma unroll
     for (int q = 0; q < R; q++) {
-        if (row0 + q >= p.M) continue;
+        if (row0 + q >= M) continue;
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             const int c = 128 * j + 2 * lane;
@@ -239,7 +239,8 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm_kernel(dpvo_rowgemm_arg
     const int wm = wave & 1, wn = wave >> 1;
     const int K = p.K;
     const int ksteps = K / RG_BK;
-    const int64_t ntiles = (p.M + RG_BM - 1) / RG_BM;
+    const int64_t Mrows = p.M_dev ? min(*p.M_dev, p.M) : p.M;
+    const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
     if ((int64_t)blockIdx.x >= ntiles) return;
     const int64_t my_tiles = (ntiles - 1 - blockIdx.x) / gridDim.x + 1;
     const int64_t total = my_tiles * ksteps;
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm_kernel(dpvo_rowgemm_arg
             const int r = (wave * 2 + j) * 8 + srow;
             const int64_t m = tile * RG_BM + r;
             const half_t* row = zero;
-            if (m < p.M) {
+            if (m < Mrows) {
                 const int64_t s = p.a_idx ? p.a_idx[m] : m;
                 if (s >= 0 && s < p.a_rows) row = (const half_t*)p.A + s * p.lda;
             }
@@ -372,9 +373,9 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm_kernel(dpvo_rowgemm_arg
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        epilogue_rows<FLAGS, 8>(p, smem, cur_buf, wave * 16, cur_tile * RG_BM + wave * 16, lane, kc);
+        epilogue_rows<FLAGS, 8>(p, Mrows, smem, cur_buf, wave * 16, cur_tile * RG_BM + wave * 16, lane, kc);
         __builtin_amdgcn_sched_barrier(0);
-        epilogue_rows<FLAGS, 8>(p, smem, cur_buf, wave * 16 + 8, cur_tile * RG_BM + wave * 16 + 8, lane, kc);
+        epilogue_rows<FLAGS, 8>(p, Mrows, smem, cur_buf, wave * 16 + 8, cur_tile * RG_BM + wave * 16 + 8, lane, kc);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");

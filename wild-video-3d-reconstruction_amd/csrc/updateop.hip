@@ -15,6 +15,8 @@
 //
 // Bytes per edge: 2 rows x D x sizeof(T) read once (+12 B of CSR traffic);
 // the kernel is HBM-bound like the GEMMs around it.
+#include <hipcub/hipcub.hpp>
+
 #include "common.hpp"
 
 namespace dpvo {
@@ -207,6 +209,120 @@ int gather_dispatch_out(const TI* x, int64_t ldx, int64_t rows, const int64_t* i
     return 0;
 }
 
+// ---------------------------------------------------------------------------
+// sync-free group-by (torch.unique(key, return_inverse=True) + CSR)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gb_keys_kernel(const int64_t* __restrict__ key, int64_t n,
+                                                      uint32_t* __restrict__ k32, int* __restrict__ idx)
+{
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        k32[e] = (uint32_t)key[e];
+        idx[e] = (int)e;
+    }
+}
+
+__global__ __launch_bounds__(256) void gb_flags_kernel(const uint32_t* __restrict__ sk, int64_t n, int* __restrict__ flag)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        flag[i] = (i == 0 || sk[i] != sk[i - 1]) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void gb_finish_kernel(const int* __restrict__ flag, const int* __restrict__ incl,
+                                                        const int* __restrict__ perm, int64_t n,
+                                                        int64_t* __restrict__ gid, int* __restrict__ offs,
+                                                        int64_t* __restrict__ groups)
+{
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int r = incl[i] - 1;
+        gid[perm[i]] = r;
+        if (flag[i]) offs[r] = (int)i;
+        if (i == n - 1) {
+            offs[r + 1] = (int)n;
+            *groups = r + 1;
+        }
+    }
+}
+
+struct GbLayout {
+    int64_t k_in, k_out, v_in, flag, incl, tmp, tmp_bytes, total;
+};
+
+size_t gb_tmp_bytes(int64_t n)
+{
+    size_t a = 0, b = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, (int*)nullptr,
+                                             (int*)nullptr, (int)n);
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, b, (int*)nullptr, (int*)nullptr, (int)n);
+    return a > b ? a : b;
+}
+
+GbLayout gb_layout(int64_t n)
+{
+    GbLayout L;
+    int64_t o = 0;
+    L.k_in = o;  o += align256(4 * n);
+    L.k_out = o; o += align256(4 * n);
+    L.v_in = o;  o += align256(4 * n);
+    L.flag = o;  o += align256(4 * n);
+    L.incl = o;  o += align256(4 * n);
+    L.tmp = o;
+    L.tmp_bytes = (int64_t)gb_tmp_bytes(n);
+    o += align256(L.tmp_bytes);
+    L.total = o;
+    return L;
+}
+
+// SoftAgg over a prebuilt CSR whose group count lives on the device.  Group
+// members are already in ascending edge order (stable sort): no LDS sort.
+template <typename T>
+__global__ __launch_bounds__(256) void sa_reduce_csr_kernel(const T* __restrict__ f, int64_t ldf,
+                                                            const T* __restrict__ s, int64_t lds,
+                                                            const int* __restrict__ offs,
+                                                            const int* __restrict__ perm,
+                                                            const int64_t* __restrict__ groups, int D, int slices,
+                                                            float eps, T* __restrict__ y)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t ntask = *groups * slices;
+    for (int64_t task = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; task < ntask;
+         task += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int64_t g = task / slices;
+        const int c = (int)(task % slices) * 128 + 2 * lane;
+        const int b = offs[g], S = offs[g + 1] - b;
+        const int* order = perm + b;
+        const bool act = c < D;
+        const int cc = act ? c : 0;
+        float2_t m = {-INFINITY, -INFINITY}, l = {0.f, 0.f}, acc = {0.f, 0.f};
+        for (int i0 = 0; i0 < S; i0 += SA_UNROLL) {
+            float2_t sv[SA_UNROLL], fv[SA_UNROLL];
+#pragma unroll
+            for (int u = 0; u < SA_UNROLL; u++) {
+                const int64_t e = order[min(i0 + u, S - 1)];
+                sv[u] = Pair<T>::load(s + e * lds + cc);
+                fv[u] = Pair<T>::load(f + e * ldf + cc);
+            }
+            float2_t mb = m;
+#pragma unroll
+            for (int u = 0; u < SA_UNROLL; u++)
+                if (i0 + u < S) {
+                    mb.x = fmaxf(mb.x, sv[u].x);
+                    mb.y = fmaxf(mb.y, sv[u].y);
+                }
+            const float ax = __expf(m.x - mb.x), ay = __expf(m.y - mb.y);
+            l.x *= ax; l.y *= ay; acc.x *= ax; acc.y *= ay;
+#pragma unroll
+            for (int u = 0; u < SA_UNROLL; u++)
+                if (i0 + u < S) {
+                    const float px = __expf(sv[u].x - mb.x), py = __expf(sv[u].y - mb.y);
+                    l.x += px; l.y += py;
+                    acc.x += px * fv[u].x; acc.y += py * fv[u].y;
+                }
+            m = mb;
+        }
+        if (act) Pair<T>::store(y + g * (int64_t)D + c, float2_t{acc.x / (l.x + eps), acc.y / (l.y + eps)});
+    }
+}
+
 }  // namespace
 }  // namespace dpvo
 
@@ -274,6 +390,77 @@ extern "C" int dpvo_gather_rows(int in_dtype, const void* x, int64_t ldx, int64_
     default: rc = -1;
     }
     DPVO_CHECK_ARG(rc == 0, "unsupported dtype");
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" size_t dpvo_group_by_workspace_bytes(int64_t n)
+{
+    return (size_t)gb_layout(n > 0 ? n : 1).total + 256;
+}
+
+extern "C" int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_t* gid, int* offs, int* perm,
+                             int64_t* groups, void* workspace, size_t workspace_bytes, void* stream)
+{
+    DPVO_CHECK_ARG(n >= 0 && n < (int64_t(1) << 31), "bad size");
+    DPVO_CHECK_ARG(key_bits >= 1 && key_bits <= 32, "key_bits must be 1..32");
+    DPVO_CHECK_ARG(groups != nullptr, "groups output missing");
+    hipStream_t st = as_stream(stream);
+    if (n == 0) {
+        DPVO_CHECK_HIP(hipMemsetAsync(groups, 0, sizeof(int64_t), st));
+        DPVO_CHECK_HIP(hipMemsetAsync(offs, 0, sizeof(int), st));
+        return 0;
+    }
+    const GbLayout L = gb_layout(n);
+    DPVO_CHECK_ARG(workspace != nullptr && workspace_bytes >= (size_t)L.total + 256, "workspace too small");
+    char* ws = (char*)(((uintptr_t)workspace + 255) & ~uintptr_t(255));
+    uint32_t* k_in = (uint32_t*)(ws + L.k_in);
+    uint32_t* k_out = (uint32_t*)(ws + L.k_out);
+    int* v_in = (int*)(ws + L.v_in);
+    int* flag = (int*)(ws + L.flag);
+    int* incl = (int*)(ws + L.incl);
+    size_t tmp_bytes = (size_t)L.tmp_bytes;
+    const unsigned g = grid_for(n, 256, 2048);
+    hipLaunchKernelGGL(gb_keys_kernel, dim3(g), dim3(256), 0, st, key, n, k_in, v_in);
+    DPVO_CHECK_LAUNCH();
+    DPVO_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(ws + L.tmp, tmp_bytes, k_in, k_out, v_in, perm, (int)n, 0,
+                                                      key_bits, st));
+    hipLaunchKernelGGL(gb_flags_kernel, dim3(g), dim3(256), 0, st, k_out, n, flag);
+    tmp_bytes = (size_t)L.tmp_bytes;
+    DPVO_CHECK_HIP(hipcub::DeviceScan::InclusiveSum(ws + L.tmp, tmp_bytes, flag, incl, (int)n, st));
+    hipLaunchKernelGGL(gb_finish_kernel, dim3(g), dim3(256), 0, st, flag, incl, perm, n, gid, offs, groups);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_softagg_csr(int dtype, const void* f, int64_t ldf, const void* s, int64_t lds, const int* offs,
+                                const int* perm, const int64_t* groups, int64_t max_groups, int D, float eps, void* y,
+                                void* stream)
+{
+    DPVO_CHECK_ARG(D > 0 && D % 2 == 0, "feature dim must be even and positive");
+    DPVO_CHECK_ARG(ldf >= D && lds >= D && ldf % 2 == 0 && lds % 2 == 0, "row strides must be even and >= D");
+    DPVO_CHECK_ARG(groups != nullptr && offs != nullptr && perm != nullptr, "CSR missing");
+    if (max_groups <= 0) return 0;
+    hipStream_t st = as_stream(stream);
+    const int slices = (D + 127) / 128;
+    const unsigned grid = grid_for(max_groups * slices * 64, 256, 4096);
+    switch (dtype) {
+    case DPVO_F16:
+        hipLaunchKernelGGL(sa_reduce_csr_kernel<half_t>, dim3(grid), dim3(256), 0, st, (const half_t*)f, ldf,
+                           (const half_t*)s, lds, offs, perm, groups, D, slices, eps, (half_t*)y);
+        break;
+    case DPVO_F32:
+        hipLaunchKernelGGL(sa_reduce_csr_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)f, ldf,
+                           (const float*)s, lds, offs, perm, groups, D, slices, eps, (float*)y);
+        break;
+    case DPVO_F64:
+        hipLaunchKernelGGL(sa_reduce_csr_kernel<double>, dim3(grid), dim3(256), 0, st, (const double*)f, ldf,
+                           (const double*)s, lds, offs, perm, groups, D, slices, eps, (double*)y);
+        break;
+    default:
+        set_error("dpvo_softagg_csr: unsupported dtype");
+        return -1;
+    }
     DPVO_CHECK_LAUNCH();
     return 0;
 }

@@ -92,11 +92,12 @@ class Update(nn.Module):
             n32, n16, _ = U.rowgemm(h, *lb, flags=U.RES, res32=n32, want32=True)
         ln0, gr1, ln1, gr2 = pk["gru"]
         for (pf, pg_, ph), key, ln in ((pk["agg_kk"], kk, None), (pk["agg_ij"], ii * 12345 + jj, ln0)):
-            uniq, gid = torch.unique(key, return_inverse=True)
+            # unique(key) + CSR on the device (no host sync); G stays on the device
+            gid, offs, perm, G = U.group_by(key, key_bits=32)
             _, f16, _ = U.rowgemm(n16, *pf)
             _, g16, _ = U.rowgemm(n16, *pg_)
-            y = U.softagg(f16, g16, gid, uniq.numel())
-            _, hy, _ = U.rowgemm(y, *ph)
+            y = U.softagg_csr(f16, g16, offs, perm, G, E)
+            _, hy, _ = U.rowgemm(y, *ph, M_dev=G)
             n32, n16 = U.rowadd_ln(n32, hy, gid, ln=ln)
         # gru = LN0 (fused above), GatedResidual, LN1, GatedResidual; then the d / w heads
         for gr, last in ((gr1, False), (gr2, True)):

@@ -35,6 +35,38 @@ def softagg(f, s, group, groups, eps=1e-12):
     return y
 
 
+def group_by(key, key_bits=32):
+    """torch.unique(key, return_inverse=True) without a host sync, plus the
+    groups' CSR: -> (gid int64 [E], offs int32 [E+1], perm int32 [E],
+    groups int64 [1] on the device).  Keys must lie in [0, 2**key_bits)."""
+    H.on_gpu(key)
+    key = H.idx64(key)
+    n = key.numel()
+    dev = key.device
+    gid = torch.empty(n, dtype=torch.int64, device=dev)
+    offs = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    perm = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    groups = torch.empty(1, dtype=torch.int64, device=dev)
+    nbytes = H.lib().dpvo_group_by_workspace_bytes(n)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    H.check(H.lib().dpvo_group_by(H.ptr(key), n, int(key_bits), H.ptr(gid), H.ptr(offs), H.ptr(perm), H.ptr(groups),
+                                  H.ptr(ws), nbytes, H.stream_of(key)))
+    return gid, offs, perm, groups
+
+
+def softagg_csr(f, s, offs, perm, groups, max_groups, eps=1e-12):
+    """softagg over group_by's CSR; y [max_groups, D], rows >= groups untouched."""
+    H.on_gpu(f, s, offs, perm, groups)
+    if f.dim() != 2 or s.shape != f.shape or f.dtype != s.dtype or f.stride(1) != 1 or s.stride(1) != 1:
+        raise RuntimeError("softagg_csr: f and s must be [E, D] with channel-contiguous rows, same dtype")
+    D = f.shape[1]
+    y = torch.empty(max_groups, D, dtype=f.dtype, device=f.device)
+    H.check(H.lib().dpvo_softagg_csr(H.dtype_code(f), H.ptr(f), f.stride(0), H.ptr(s), s.stride(0), H.ptr(offs),
+                                     H.ptr(perm), H.ptr(groups), int(max_groups), D, float(eps), H.ptr(y),
+                                     H.stream_of(f)))
+    return y
+
+
 def gather_rows(x, idx, dtype=None):
     """out[e] = x[idx[e]] if idx[e] >= 0 else 0, cast to ``dtype`` (default x's).
     x: [R, D] with unit channel stride; idx: [n] int64."""
@@ -67,7 +99,7 @@ class RowGemmArgs(_ct.Structure):
                 ("ln_g", _ct.c_void_p), ("ln_b", _ct.c_void_p), ("ln_eps", _ct.c_float),
                 ("head_w", _ct.c_void_p), ("head_b", _ct.c_void_p), ("head_out", _ct.c_void_p),
                 ("out32", _ct.c_void_p), ("ldo32", _ct.c_int64), ("out16", _ct.c_void_p), ("ldo16", _ct.c_int64),
-                ("flags", _ct.c_int)]
+                ("flags", _ct.c_int), ("M_dev", _ct.c_void_p)]
 
 
 class RowAddArgs(_ct.Structure):
@@ -103,7 +135,7 @@ def _p(t):
 
 
 def rowgemm(A, W16, b16, flags=0, a_idx=None, M=None, res32=None, res16=None, res16_idx=None, gate16=None, ln=None,
-            heads=None, out32=None, out16=None, want32=False, want16=True):
+            heads=None, out32=None, out16=None, want32=False, want16=True, M_dev=None):
     """Y = epilogue(A W^T + b) over 384-wide rows (see include/dpvo_hot.h).
     A: fp16 [R, >=Kp] (row-contiguous); a_idx: optional int64 [M] row gather.
     ln = (gamma f32, beta f32, eps); heads = (W fp16 [4,384], b fp16 [4]).
@@ -142,6 +174,10 @@ def rowgemm(A, W16, b16, flags=0, a_idx=None, M=None, res32=None, res16=None, re
     a.out32, a.ldo32 = _p(out32), (out32.stride(0) if out32 is not None else 0)
     a.out16, a.ldo16 = _p(out16), (out16.stride(0) if out16 is not None else 0)
     a.flags = int(flags)
+    if M_dev is not None:
+        if M_dev.dtype != torch.int64 or not M_dev.is_cuda:
+            raise RuntimeError("rowgemm: M_dev must be a device int64 scalar")
+        a.M_dev = M_dev.data_ptr()
     for t, nm in ((res32, "res32"), (out32, "out32")):
         if t is not None and (t.dtype != torch.float32 or t.stride(1) != 1):
             raise RuntimeError(f"rowgemm: {nm} must be fp32 with contiguous rows")
