@@ -16,8 +16,9 @@ rc=$?; echo "trace rc=$rc"; tail -3 "$OUT/trace.log"
 [ $rc -eq 0 ] || exit $rc
 [ "${PMC:-1}" = "1" ] || exit 0
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex corr_fast -f csv -d "$OUT/pmc_$C" -o run -- python "$REPO/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$C.log" 2>&1
+  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex 'corr_s?fast' -f csv -d "$OUT/pmc_$C" -o run -- python "$REPO/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$C.log" 2>&1
   rc=$?; echo "pmc $C rc=$rc"; tail -2 "$OUT/pmc_$C.log"
   [ $rc -eq 0 ] || exit $rc
 done
-find "$OUT" -name "*.csv" | head -20
+cd "$REPO"
+python scripts/traffic_json.py "$OUT/pmc_FETCH_SIZE" "$OUT/pmc_WRITE_SIZE" 95424 "$OUT/altcorr_traffic.json"

@@ -70,4 +70,31 @@ __device__ __forceinline__ int floor_to_int_sat(float v)
 }
 __device__ __forceinline__ int wrap_add(int a, int b) { return (int)((unsigned)a + (unsigned)b); }
 
+// ---------------------------------------------------------------------------
+// wave64 reductions (DPP row rotations + readlanes)
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp_rot(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// all-reduce over a DPP row (16 lanes): every lane of the row gets the row's sum
+__device__ __forceinline__ float row16_sum(float s)
+{
+    s += dpp_rot<0x128>(s);
+    s += dpp_rot<0x124>(s);
+    s += dpp_rot<0x122>(s);
+    s += dpp_rot<0x121>(s);
+    return s;
+}
+// sum over all 64 lanes (wave-uniform result)
+__device__ __forceinline__ float wave64_sum(float s)
+{
+    s = row16_sum(s);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 0)) +
+           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 16)) +
+           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 32)) +
+           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(s), 48));
+}
+
 }  // namespace dpvo

@@ -22,6 +22,7 @@
 // The unique-id inverse (the reference's torch::_unique, ba_cuda.cu:435) is
 // recomputed per edge from the bitmap instead of being stored.
 #include <algorithm>
+#include <stdlib.h>
 
 #include <hipcub/hipcub.hpp>
 
@@ -203,6 +204,7 @@ struct BaParams {
     float *B, *v, *C, *u, *Em, *S, *y, *dX;
     double* Sd;
     double* yd;
+    int red_iters;   // wave reductions of the pose-block terms per wave (0 = per-lane atomics only)
 };
 
 __device__ __forceinline__ bool failed(const BaParams& p) { return *(volatile int*)p.status != 0; }
@@ -241,6 +243,7 @@ __global__ __launch_bounds__(256) void ba_mark_kernel(BaParams p)
             if (lane == leader) atomicOr(&p.bits[lw], b);
             pending &= ~__ballot(mine);
         }
+
     }
 }
 
@@ -315,16 +318,22 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
     const float fx = p.intrinsics[0], fy = p.intrinsics[1], cx = p.intrinsics[2], cy = p.intrinsics[3];
     const int64_t PP = (int64_t)p.P * p.P, centre = (p.P / 2) * p.P + p.P / 2;
 
-    for (int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; n < p.E; n += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t kxn = p.kk[n];
-        if (kxn < 0 || kxn >= p.num_patches) continue;
-        const int k = unique_rank(p, kxn);
-        const int64_t i_abs = p.ii[n], j_abs = p.jj[n];
+    const int lane = threadIdx.x & 63;
+    // whole waves walk the edges together (the pose-block reduction below is per wave)
+    for (int64_t n0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~int64_t(63); n0 < p.E;
+         n0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t n = n0 + lane;
+        const int64_t kxn = n < p.E ? p.kk[n] : -1;
+        const bool valid = kxn >= 0 && kxn < p.num_patches;
+        const int64_t ne = valid ? n : n0;                // a valid edge index for the (discarded) loads
+        const int64_t kc = valid ? kxn : 0;
+        const int k = unique_rank(p, kc);
+        const int64_t i_abs = p.ii[ne], j_abs = p.jj[ne];
         const float* Pi = p.poses + i_abs * 7;
         const float* Pj = p.poses + j_abs * 7;
         const float ti[3] = {Pi[0], Pi[1], Pi[2]}, tj[3] = {Pj[0], Pj[1], Pj[2]};
         const float qi[4] = {Pi[3], Pi[4], Pi[5], Pi[6]}, qj[4] = {Pj[3], Pj[4], Pj[5], Pj[6]};
-        const float* pa = p.patches + kxn * 3 * PP + centre;
+        const float* pa = p.patches + kc * 3 * PP + centre;
         float Xi[4], Xj[4], tij[3], qij[4];
         Xi[0] = (pa[0] - cx) / fx;
         Xi[1] = (pa[PP] - cy) / fy;
@@ -336,17 +345,17 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
         const float d = (Z >= 0.2f) ? 1.0f / Z : 0.0f;
         const float d2 = d * d;
         const float x1 = fx * (X / Z) + cx, y1 = fy * (Y / Z) + cy;
-        const float rx = p.target[n * 2 + 0] - x1, ry = p.target[n * 2 + 1] - y1;
+        const float rx = p.target[ne * 2 + 0] - x1, ry = p.target[ne * 2 + 1] - y1;
         const bool in_bounds = (sqrtf(rx * rx + ry * ry) < 128.f) && (Z > 0.2f) && (x1 > -64.f) && (y1 > -64.f) &&
                                (x1 < 2.f * cx + 64.f) && (y1 < 2.f * cy + 64.f);
-        const float mask = in_bounds ? 1.0f : 0.0f;
+        const float mask = (in_bounds && valid) ? 1.0f : 0.0f;
         const int ix = (int)(i_abs - p.t0), jx = (int)(j_abs - p.t0);
-        const bool iv = ix >= 0 && ix < p.N, jv = jx >= 0 && jx < p.N;
+        const bool iv = valid && ix >= 0 && ix < p.N, jv = valid && jx >= 0 && jx < p.N;
 
         // both residual rows, summed per destination
         float Ji[2][6], Jj[2][6], Jz[2], w[2], r[2];
-        w[0] = mask * p.weight[n * 2 + 0];
-        w[1] = mask * p.weight[n * 2 + 1];
+        w[0] = mask * p.weight[ne * 2 + 0];
+        w[1] = mask * p.weight[ne * 2 + 1];
         r[0] = rx;
         r[1] = ry;
         Jz[0] = fx * (tij[0] * d - tij[2] * (X * d2));
@@ -360,83 +369,162 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
         adjSE3(tij, qij, Jj[0], Ji[0]);
         adjSE3(tij, qij, Jj[1], Ji[1]);
 
-        // patch terms: E rows (device atomics), C, u
-        float Ei[6], Ej[6], Ck = 0.f, uk = 0.f;
+        // patch terms: E rows (device atomics; a wave's lanes mostly hold different patches), C, u
+        if (valid) {
+            float Ei[6], Ej[6], Ck = 0.f, uk = 0.f;
 #pragma unroll
-        for (int t = 0; t < 6; t++) { Ei[t] = 0.f; Ej[t] = 0.f; }
+            for (int t = 0; t < 6; t++) { Ei[t] = 0.f; Ej[t] = 0.f; }
 #pragma unroll
-        for (int row = 0; row < 2; row++) {
+            for (int row = 0; row < 2; row++) {
 #pragma unroll
-            for (int t = 0; t < 6; t++) {
-                Ei[t] += -w[row] * Jz[row] * Ji[row][t];
-                Ej[t] += w[row] * Jz[row] * Jj[row][t];
+                for (int t = 0; t < 6; t++) {
+                    Ei[t] += -w[row] * Jz[row] * Ji[row][t];
+                    Ej[t] += w[row] * Jz[row] * Jj[row][t];
+                }
+                Ck += w[row] * Jz[row] * Jz[row];
+                uk += w[row] * r[row] * Jz[row];
             }
-            Ck += w[row] * Jz[row] * Jz[row];
-            uk += w[row] * r[row] * Jz[row];
-        }
-        atomicAdd(&p.C[k], Ck);
-        atomicAdd(&p.u[k], uk);
-        float* Erow = p.Em + (int64_t)k * n6;
-        if (iv) {
+            atomicAdd(&p.C[k], Ck);
+            atomicAdd(&p.u[k], uk);
+            float* Erow = p.Em + (int64_t)k * n6;
+            if (iv) {
 #pragma unroll
-            for (int t = 0; t < 6; t++) atomicAdd(&Erow[6 * ix + t], Ei[t]);
-        }
-        if (jv) {
+                for (int t = 0; t < 6; t++) atomicAdd(&Erow[6 * ix + t], Ei[t]);
+            }
+            if (jv) {
 #pragma unroll
-            for (int t = 0; t < 6; t++) atomicAdd(&Erow[6 * jx + t], Ej[t]);
+                for (int t = 0; t < 6; t++) atomicAdd(&Erow[6 * jx + t], Ej[t]);
+            }
         }
-        // pose terms: v, and the upper triangle of B
-        if (iv) {
+
+        // pose terms: v_i, v_j and the B blocks (ii, jj upper triangles; ij off-diagonal,
+        // stored once in the upper triangle; a self edge folds into ii).  Lanes with the
+        // same (ix, jx) -- runs of consecutive edges share a frame pair -- are summed
+        // across the wave first: one LDS / device atomic per value instead of 64.
+        const bool self = iv && jv && ix == jx;
+        const bool up = ix < jx;
+        float vi[6], vj[6], bii[21], bjj[21], bij[36];
 #pragma unroll
-            for (int t = 0; t < 6; t++) atomicAdd(&vacc[6 * ix + t], -w[0] * r[0] * Ji[0][t] - w[1] * r[1] * Ji[1][t]);
+        for (int t = 0; t < 6; t++) {
+            vi[t] = iv ? -w[0] * r[0] * Ji[0][t] - w[1] * r[1] * Ji[1][t] : 0.f;
+            vj[t] = jv ? w[0] * r[0] * Jj[0][t] + w[1] * r[1] * Jj[1][t] : 0.f;
         }
-        if (jv) {
-#pragma unroll
-            for (int t = 0; t < 6; t++) atomicAdd(&vacc[6 * jx + t], w[0] * r[0] * Jj[0][t] + w[1] * r[1] * Jj[1][t]);
-        }
-        if (iv && jv && ix == jx) {
-            // self edge: Bii + Bjj - Bij - Bji land in one diagonal block
+        {
+            int u = 0;
 #pragma unroll
             for (int a = 0; a < 6; a++)
 #pragma unroll
-                for (int b = a; b < 6; b++) {
-                    float s = 0.f;
+                for (int b = a; b < 6; b++, u++) {
+                    float sii = 0.f, sjj = 0.f;
+                    if (self) {
 #pragma unroll
-                    for (int row = 0; row < 2; row++)
-                        s += w[row] * (Ji[row][a] * Ji[row][b] + Jj[row][a] * Jj[row][b] - Ji[row][a] * Jj[row][b] -
-                                       Jj[row][a] * Ji[row][b]);
-                    atomicAdd(&Bacc[(6 * ix + a) * n6 + 6 * ix + b], s);
+                        for (int row = 0; row < 2; row++)
+                            sii += w[row] * (Ji[row][a] * Ji[row][b] + Jj[row][a] * Jj[row][b] - Ji[row][a] * Jj[row][b] -
+                                             Jj[row][a] * Ji[row][b]);
+                    } else {
+                        if (iv) sii = w[0] * Ji[0][a] * Ji[0][b] + w[1] * Ji[1][a] * Ji[1][b];
+                        if (jv) sjj = w[0] * Jj[0][a] * Jj[0][b] + w[1] * Jj[1][a] * Jj[1][b];
+                    }
+                    bii[u] = sii;
+                    bjj[u] = sjj;
                 }
-            continue;
         }
-        if (iv) {
 #pragma unroll
-            for (int a = 0; a < 6; a++)
+        for (int a = 0; a < 6; a++)
 #pragma unroll
-                for (int b = a; b < 6; b++)
-                    atomicAdd(&Bacc[(6 * ix + a) * n6 + 6 * ix + b],
-                              w[0] * Ji[0][a] * Ji[0][b] + w[1] * Ji[1][a] * Ji[1][b]);
-        }
-        if (jv) {
+            for (int b = 0; b < 6; b++) {
+                float s = 0.f;
+                if (iv && jv && !self)
+                    s = up ? -(w[0] * Ji[0][a] * Jj[0][b] + w[1] * Ji[1][a] * Jj[1][b])
+                           : -(w[0] * Jj[0][a] * Ji[0][b] + w[1] * Jj[1][a] * Ji[1][b]);
+                bij[a * 6 + b] = s;
+            }
+        const bool has = iv || jv;
+        const int key = has ? ((ix & 0x3ff) << 12 | (jx & 0x3ff) << 2 | (iv ? 2 : 0) | (jv ? 1 : 0)) : -1;
+        uint64_t pending = __ballot(has);
+        for (int iter = 0; pending && iter < p.red_iters; iter++) {
+            const int leader = __ffsll((unsigned long long)pending) - 1;
+            const int lkey = __shfl(key, leader);
+            const bool mine = key == lkey;
+            const int lix = __shfl(ix, leader), ljx = __shfl(jx, leader);
+            const bool liv = (lkey & 2) != 0, ljv = (lkey & 1) != 0;
+            const bool lself = liv && ljv && lix == ljx;
+            const bool lup = lix < ljx;
+            auto red = [&](float v) { return wave64_sum(mine ? v : 0.f); };
+            if (liv) {
 #pragma unroll
-            for (int a = 0; a < 6; a++)
-#pragma unroll
-                for (int b = a; b < 6; b++)
-                    atomicAdd(&Bacc[(6 * jx + a) * n6 + 6 * jx + b],
-                              w[0] * Jj[0][a] * Jj[0][b] + w[1] * Jj[1][a] * Jj[1][b]);
-        }
-        if (iv && jv) {
-            // off-diagonal block stored once, in the upper triangle
-            const bool up = ix < jx;
-            const int r0 = up ? ix : jx, c0 = up ? jx : ix;
-#pragma unroll
-            for (int a = 0; a < 6; a++)
-#pragma unroll
-                for (int b = 0; b < 6; b++) {
-                    const float s = up ? -(w[0] * Ji[0][a] * Jj[0][b] + w[1] * Ji[1][a] * Jj[1][b])
-                                       : -(w[0] * Jj[0][a] * Ji[0][b] + w[1] * Jj[1][a] * Ji[1][b]);
-                    atomicAdd(&Bacc[(6 * r0 + a) * n6 + 6 * c0 + b], s);
+                for (int t = 0; t < 6; t++) {
+                    const float s = red(vi[t]);
+                    if (lane == leader) atomicAdd(&vacc[6 * lix + t], s);
                 }
+                int u = 0;
+#pragma unroll
+                for (int a = 0; a < 6; a++)
+#pragma unroll
+                    for (int b = a; b < 6; b++, u++) {
+                        const float s = red(bii[u]);
+                        if (lane == leader) atomicAdd(&Bacc[(6 * lix + a) * n6 + 6 * lix + b], s);
+                    }
+            }
+            if (ljv) {
+#pragma unroll
+                for (int t = 0; t < 6; t++) {
+                    const float s = red(vj[t]);
+                    if (lane == leader) atomicAdd(&vacc[6 * ljx + t], s);
+                }
+            }
+            if (ljv && !lself) {
+                int u = 0;
+#pragma unroll
+                for (int a = 0; a < 6; a++)
+#pragma unroll
+                    for (int b = a; b < 6; b++, u++) {
+                        const float s = red(bjj[u]);
+                        if (lane == leader) atomicAdd(&Bacc[(6 * ljx + a) * n6 + 6 * ljx + b], s);
+                    }
+            }
+            if (liv && ljv && !lself) {
+                const int r0 = lup ? lix : ljx, c0 = lup ? ljx : lix;
+#pragma unroll
+                for (int a = 0; a < 6; a++)
+#pragma unroll
+                    for (int b = 0; b < 6; b++) {
+                        const float s = red(bij[a * 6 + b]);
+                        if (lane == leader) atomicAdd(&Bacc[(6 * r0 + a) * n6 + 6 * c0 + b], s);
+                    }
+            }
+            pending &= ~__ballot(mine);
+        }
+        // many distinct frame pairs in this wave (kk-major backward edges): plain
+        // per-lane atomics for the lanes not reduced above
+        if ((pending >> lane) & 1) {
+            if (iv) {
+#pragma unroll
+                for (int t = 0; t < 6; t++) atomicAdd(&vacc[6 * ix + t], vi[t]);
+                int u = 0;
+#pragma unroll
+                for (int a = 0; a < 6; a++)
+#pragma unroll
+                    for (int b = a; b < 6; b++, u++) atomicAdd(&Bacc[(6 * ix + a) * n6 + 6 * ix + b], bii[u]);
+            }
+            if (jv) {
+#pragma unroll
+                for (int t = 0; t < 6; t++) atomicAdd(&vacc[6 * jx + t], vj[t]);
+            }
+            if (jv && !self) {
+                int u = 0;
+#pragma unroll
+                for (int a = 0; a < 6; a++)
+#pragma unroll
+                    for (int b = a; b < 6; b++, u++) atomicAdd(&Bacc[(6 * jx + a) * n6 + 6 * jx + b], bjj[u]);
+            }
+            if (iv && jv && !self) {
+                const int r0 = up ? ix : jx, c0 = up ? jx : ix;
+#pragma unroll
+                for (int a = 0; a < 6; a++)
+#pragma unroll
+                    for (int b = 0; b < 6; b++) atomicAdd(&Bacc[(6 * r0 + a) * n6 + 6 * c0 + b], bij[a * 6 + b]);
+            }
         }
     }
     if (LDS_B) {
@@ -452,6 +540,7 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
 // Schur complement terms: S_acc += Q_k e_k e_k^T (upper), y_acc += Q_k u_k e_k
 // ---------------------------------------------------------------------------
 constexpr int SCHUR_CHUNK = 64;
+
 
 __global__ __launch_bounds__(256) void ba_schur_kernel(BaParams p)
 {
@@ -513,64 +602,101 @@ __device__ __forceinline__ void wave_sync_lds()
     __builtin_amdgcn_wave_barrier();
 }
 
-// n6 <= 64: one wave, lane r owns row r; no block barriers.  Same arithmetic
-// as ba_solve_kernel (fp64 right-looking Cholesky, forward/backward solve).
+__device__ __forceinline__ double a_diag_lds(const double* L, int j) { return L[j * 65 + j]; }
+
+__device__ __forceinline__ double readlane_d(double v, int lane)
+{
+    const int64_t u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(u & 0xffffffff), lane);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), lane);
+    return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+
+// n6 <= 64: one wave, lane r holds row r of the system in registers (fully
+// unrolled, compile-time column indices).  Column j of L is broadcast through
+// LDS (one ds_write per lane, broadcast ds_read2 of the column): no readlane
+// round trips and no per-element branches.  fp64 right-looking Cholesky and
+// forward / backward substitution -- the arithmetic of ba_solve_kernel.
+__device__ __forceinline__ void wave_lds_fence()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __global__ __launch_bounds__(64) void ba_solve_wave_kernel(BaParams p)
 {
-    __shared__ double A[64 * 65];
+    __shared__ double col[64];
+    __shared__ double Lsh[64 * 65];
     __shared__ double yv[64];
     if (failed(p)) return;
-    const int n = p.n6, ld = n + 1, r = threadIdx.x;
-    for (int i = r; i < n * n; i += 64) {
-        const int a = i / n, b = i - a * n;
-        const int r0 = a < b ? a : b, c0 = a < b ? b : a;
-        double s = (double)(p.B[r0 * n + c0] - p.S[r0 * n + c0]);
-        if (a == b) s += 1e-4 * s + 1.0;
-        A[a * ld + b] = s;
+    const int n = p.n6, r = threadIdx.x;
+    double a[64];
+    // unconditional loads from clamped (valid) indices, then select: a load
+    // under a per-element condition makes hipcc wait vmcnt(0) per element
+    const int rc = r < n ? r : n - 1;
+    float bv[64], sv[64];
+#pragma unroll
+    for (int c = 0; c < 64; c++) {
+        const int cc = c < n ? c : n - 1;
+        const int r0 = rc < cc ? rc : cc, c0 = rc < cc ? cc : rc;
+        bv[c] = p.B[r0 * n + c0];
+        sv[c] = p.S[r0 * n + c0];
     }
-    if (r < n) yv[r] = (double)(p.v[r] - p.y[r]);
-    wave_sync_lds();
+#pragma unroll
+    for (int c = 0; c < 64; c++) {
+        double s = (double)(bv[c] - sv[c]);
+        if (r == c) s += 1e-4 * s + 1.0;
+        a[c] = (r < n && c < n) ? s : 0.0;
+    }
+    const float v_r = p.v[rc], y_r = p.y[rc];
+    double y = r < n ? (double)(v_r - y_r) : 0.0;
     int fail = 0;
-    for (int j = 0; j < n; j++) {
-        const double djj = A[j * ld + j];
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        if (j >= n || fail) break;
+        col[r] = a[j];
+        wave_lds_fence();
+        const double djj = col[j];
         if (!(djj > 0.0)) {
             fail = j + 1;
             break;
         }
         const double ljj = sqrt(djj);
-        double lrj = 0.0;
-        if (r > j && r < n) {
-            lrj = A[r * ld + j] / ljj;
-            A[r * ld + j] = lrj;
-        }
-        wave_sync_lds();
-        if (r == j) A[j * ld + j] = ljj;
-        if (r > j && r < n) {
-            double* row = A + r * ld;
-            for (int c = j + 1; c <= r; c++) row[c] -= lrj * A[c * ld + j];
-        }
-        wave_sync_lds();
+        const double l = r > j ? a[j] / ljj : (r == j ? ljj : 0.0);
+        a[j] = l;
+        wave_lds_fence();
+        col[r] = l;
+        wave_lds_fence();
+#pragma unroll
+        for (int c = j + 1; c < 64; c++) a[c] -= l * col[c];   // rows r >= c kept (lower triangle)
+        wave_lds_fence();
     }
     if (fail) {
         if (r == 0) atomicExch(p.status, fail);
         return;
     }
-    // L z = y (row j of L is complete; lanes i > j update)
+    // L to LDS (row r), then L z = y and L^T x = z with one broadcast per step
+#pragma unroll
+    for (int c = 0; c < 64; c++) Lsh[r * 65 + c] = a[c];
+    wave_lds_fence();
     for (int j = 0; j < n; j++) {
-        const double yj = yv[j] / A[j * ld + j];
-        if (r > j && r < n) yv[r] -= A[r * ld + j] * yj;
-        wave_sync_lds();
-        if (r == j) yv[j] = yj;
-        wave_sync_lds();
+        if (r == j) col[0] = y / a_diag_lds(Lsh, j);
+        wave_lds_fence();
+        const double zj = col[0];
+        if (r == j) y = zj;
+        else if (r > j) y -= Lsh[r * 65 + j] * zj;
+        wave_lds_fence();
     }
-    // L^T x = z
     for (int j = n - 1; j >= 0; j--) {
-        const double yj = yv[j] / A[j * ld + j];
-        if (r < j) yv[r] -= A[j * ld + r] * yj;
-        wave_sync_lds();
-        if (r == j) yv[j] = yj;
-        wave_sync_lds();
+        if (r == j) col[0] = y / a_diag_lds(Lsh, j);
+        wave_lds_fence();
+        const double xj = col[0];
+        if (r == j) y = xj;
+        else if (r < j) y -= Lsh[j * 65 + r] * xj;
+        wave_lds_fence();
     }
+    if (r < n) yv[r] = y;
+    wave_lds_fence();
     ba_retract_and_reset(p, yv, r, 64);
 }
 
@@ -764,6 +890,13 @@ extern "C" int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches
     p.P = P; p.t0 = t0; p.N = N; p.n6 = 6 * N;
     p.hdr = (int*)(ws + L.hdr);
     p.status = status ? status : p.hdr + HDR_STATUS;
+    {
+        static const int red = [] {
+            const char* v = getenv("DPVO_BA_WAVE_RED");
+            return v ? atoi(v) : 2;
+        }();
+        p.red_iters = red;
+    }
     p.bits = (uint32_t*)(ws + L.bits);
     p.wordbase = (int*)(ws + L.wordbase);
     p.kx = (int*)(ws + L.kx);
@@ -796,7 +929,8 @@ extern "C" int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches
             hipLaunchKernelGGL(ba_hessian_kernel<false>, dim3(gH), dim3(256), 0, s, p);
         if (N > 0) {
             hipLaunchKernelGGL(ba_schur_kernel, dim3(gS), dim3(256), lds_s, s, p);
-            if (p.n6 <= 64)
+            static const bool block_solve = getenv("DPVO_BA_BLOCK_SOLVE") != nullptr;  // A/B switch
+            if (p.n6 <= 64 && !block_solve)
                 hipLaunchKernelGGL(ba_solve_wave_kernel, dim3(1), dim3(64), 0, s, p);
             else
                 hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), lds_v, s, p);

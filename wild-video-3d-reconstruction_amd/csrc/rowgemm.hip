@@ -25,6 +25,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <stdlib.h>
 
 namespace dpvo {
 namespace {
@@ -121,8 +122,13 @@ __device__ __forceinline__ void load_consts(const dpvo_rowgemm_args& p, int lane
 
 // R whole output rows per wave (lane owns columns 2*lane + 128*j, j < 3):
 // all of the batch's loads are issued before any row's reductions.
-template <int FLAGS, int R>
-__device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, int64_t M, const char* smem, int cur_buf,
+struct YMapFull {   // v1: 128-row tile over the consumed stage + extra region
+    int cur_buf;
+    __device__ int off(int r, int byte) const { return ytile_off(cur_buf, r, byte); }
+};
+
+template <int FLAGS, int R, typename YMap>
+__device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, int64_t M, const char* smem, YMap ym,
                                               int lrow0, int64_t row0, int lane, const EpiConsts& k)
 {
     float2_t v[R][3];
@@ -132,7 +138,7 @@ __device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, int64_
         rows[q] = row0 + q < M ? row0 + q : M - 1;   // clamped for loads; stores skip rows >= M
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-            const half2_t y = *(const half2_t*)(smem + ytile_off(cur_buf, lrow0 + q, (128 * j + 2 * lane) * 2));
+            const half2_t y = *(const half2_t*)(smem + ym.off(lrow0 + q, (128 * j + 2 * lane) * 2));
             v[q][j] = float2_t{(float)y.x, (float)y.y};
         }
     }
@@ -373,15 +379,172 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm_kernel(dpvo_rowgemm_arg
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        epilogue_rows<FLAGS, 8>(p, Mrows, smem, cur_buf, wave * 16, cur_tile * RG_BM + wave * 16, lane, kc);
+        epilogue_rows<FLAGS, 8>(p, Mrows, smem, YMapFull{cur_buf}, wave * 16, cur_tile * RG_BM + wave * 16, lane, kc);
         __builtin_amdgcn_sched_barrier(0);
-        epilogue_rows<FLAGS, 8>(p, Mrows, smem, cur_buf, wave * 16 + 8, cur_tile * RG_BM + wave * 16 + 8, lane, kc);
+        epilogue_rows<FLAGS, 8>(p, Mrows, smem, YMapFull{cur_buf}, wave * 16 + 8, cur_tile * RG_BM + wave * 16 + 8,
+                                lane, kc);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// v2: two workgroups per CU.  BM = 64 rows, 4 waves (each 64 rows x 96 columns,
+// the same 4 x 6 accumulators), BK = 32 stages (A 4 KB + W 24 KB), 56 KB of
+// LDS per workgroup.  The epilogue stages 32-row halves of y through the
+// consumed stage buffer.  With two resident workgroups one's HBM-bound
+// epilogue overlaps the other's MFMA loop.
+// ---------------------------------------------------------------------------
+constexpr int R2_BM = 64, R2_BK = 32, R2_THREADS = 256;
+constexpr int R2_A_STAGE = R2_BM * R2_BK * 2;    // 4 KB
+constexpr int R2_W_STAGE = RG_BN * R2_BK * 2;    // 24 KB
+constexpr int R2_STAGE = R2_A_STAGE + R2_W_STAGE;
+constexpr int R2_LDS = 2 * R2_STAGE;             // 56 KB
+
+struct YMapHalf {   // v2: 32 rows x 768 B in one stage buffer, 32-B granules XOR (row/4)&3
+    int base;
+    __device__ int off(int r, int byte) const { return base + r * 768 + (byte ^ (((r >> 2) & 3) << 5)); }
+};
+
+template <int FLAGS>
+__global__ __launch_bounds__(R2_THREADS, 2) void rowgemm2_kernel(dpvo_rowgemm_args p)
+{
+    __shared__ __attribute__((aligned(16))) char smem[R2_LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int K = p.K;
+    const int ksteps = K / R2_BK;
+    const int64_t Mrows = p.M_dev ? min(*p.M_dev, p.M) : p.M;
+    const int64_t ntiles = (Mrows + R2_BM - 1) / R2_BM;
+    if ((int64_t)blockIdx.x >= ntiles) return;
+    const int64_t my_tiles = (ntiles - 1 - blockIdx.x) / gridDim.x + 1;
+    const int64_t total = my_tiles * ksteps;
+
+    const half_t* __restrict__ Wt = (const half_t*)p.W;
+    const half_t* __restrict__ zero = (const half_t*)p.zero_row;
+    // staging: lane L of a wave-instruction fills LDS row base + L/4, physical 16-B
+    // chunk L%4, holding logical chunk (L%4) ^ ((row>>2)&3)
+    const int srow = lane >> 2, pch = lane & 3;
+    const half_t* wsrc[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        const int n = (wave * 6 + j) * 16 + srow;
+        wsrc[j] = Wt + (int64_t)n * K + 8 * (pch ^ ((n >> 2) & 3));
+    }
+    const half_t* asrc;
+    auto set_tile_a = [&](int64_t tile) {
+        const int r = wave * 16 + srow;
+        const int64_t m = tile * R2_BM + r;
+        const half_t* row = zero;
+        if (m < Mrows) {
+            const int64_t s = p.a_idx ? p.a_idx[m] : m;
+            if (s >= 0 && s < p.a_rows) row = (const half_t*)p.A + s * p.lda;
+        }
+        asrc = row + 8 * (pch ^ ((r >> 2) & 3));
+    };
+    auto issue = [&](int ks, int64_t tile, int buf) {
+        if (ks == 0) set_tile_a(tile);
+        char* sA = smem + buf * R2_STAGE;
+        char* sW = sA + R2_A_STAGE;
+        const int k0 = ks * R2_BK;
+        glds16(asrc + k0, sA + wave * 1024);
+#pragma unroll
+        for (int j = 0; j < 6; j++) glds16(wsrc[j] + k0, sW + (wave * 6 + j) * 1024);
+    };
+
+    f4_t acc[4][6];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, fq = lane >> 4;
+    int a_off[4], w_off[6];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++) {
+        const int row = mt * 16 + fr;
+        a_off[mt] = row * 64 + 16 * (fq ^ ((row >> 2) & 3));
+    }
+#pragma unroll
+    for (int nt = 0; nt < 6; nt++) {
+        const int n = wave * 96 + nt * 16 + fr;
+        w_off[nt] = R2_A_STAGE + n * 64 + 16 * (fq ^ ((n >> 2) & 3));
+    }
+    EpiConsts kc;
+    load_consts<FLAGS>(p, lane, kc);
+
+    int64_t tile = blockIdx.x;
+    int ks = 0, buf = 0;
+    issue(0, tile, 0);
+    for (int64_t i = 0; i < total; i++) {
+        int nks = ks + 1;
+        int64_t ntile = tile;
+        if (nks == ksteps) {
+            nks = 0;
+            ntile += gridDim.x;
+        }
+        if (i + 1 < total) {
+            issue(nks, ntile, buf ^ 1);
+            asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const char* st = smem + buf * R2_STAGE;
+        h8_t a[4], b[6];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(st + a_off[mt]);
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++)
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+        __builtin_amdgcn_s_barrier();
+        const int cur_buf = buf;
+        const int64_t cur_tile = tile;
+        const bool last = ks == ksteps - 1;
+        ks = nks;
+        tile = ntile;
+        buf ^= 1;
+        if (!last) continue;
+
+        // epilogue in two 32-row halves through the consumed stage buffer
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) {
+                const int cl = wave * 96 + nt * 16 + fr;
+                const float bias = (float)((const half_t*)p.bias)[cl];
+#pragma unroll
+                for (int mm = 0; mm < 2; mm++) {
+                    const int mt = 2 * h + mm;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        half_t y = (half_t)(acc[mt][nt][r] + bias);
+                        if (FLAGS & RG_RELU) y = y > (half_t)0 ? y : (half_t)0;
+                        if (FLAGS & RG_SIGMOID) y = (half_t)fast_sigmoid((float)y);
+                        *(half_t*)(smem + YMapHalf{cur_buf * R2_STAGE}.off(mm * 16 + fq * 4 + r, cl * 2)) = y;
+                        acc[mt][nt][r] = 0.f;
+                    }
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            constexpr int RB = (FLAGS & (RG_RES | RG_GATE)) ? 4 : 8;   // rows per batch (register budget)
+#pragma unroll
+            for (int q0 = 0; q0 < 8; q0 += RB)
+                epilogue_rows<FLAGS, RB>(p, Mrows, smem, YMapHalf{cur_buf * R2_STAGE}, wave * 8 + q0,
+                                         cur_tile * R2_BM + h * 32 + wave * 8 + q0, lane, kc);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+    }
+}
 
 // v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16   (one wave per row)
 __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
@@ -459,6 +622,7 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
     DPVO_CHECK_ARG(a != nullptr, "null args");
     DPVO_CHECK_ARG(a->N == RG_BN, "rowgemm: output width must be 384");
     DPVO_CHECK_ARG(a->K > 0 && a->K % RG_BK == 0, "rowgemm: K must be a positive multiple of 64 (pad W with zeros)");
+    // (v2 stages K in steps of 32; every multiple of 64 is one)
     DPVO_CHECK_ARG(a->A && a->W && a->bias && a->zero_row, "rowgemm: A, W, bias and zero_row are required");
     DPVO_CHECK_ARG(a->lda >= a->K && a->lda % 8 == 0, "rowgemm: lda must be >= K and a multiple of 8");
     DPVO_CHECK_ARG(((uintptr_t)a->A & 15) == 0 && ((uintptr_t)a->W & 15) == 0 && ((uintptr_t)a->zero_row & 15) == 0,
@@ -474,6 +638,35 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
         DPVO_CHECK_HIP(hipGetDevice(&dev));
         DPVO_CHECK_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
         if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    static const int version = [] {
+        const char* v = getenv("DPVO_ROWGEMM");   // 1 (default): one 128-row workgroup per CU; 2: two 64-row
+        return v ? atoi(v) : 1;
+    }();
+    if (version == 2) {
+        const int64_t nt2 = (a->M + R2_BM - 1) / R2_BM;
+        const unsigned grid = (unsigned)std::min<int64_t>(nt2, 2 * (int64_t)g_num_cus);
+        switch (f) {
+#define R2_CASE(F)                                                                                           \
+    case (F):                                                                                                \
+        hipLaunchKernelGGL(rowgemm2_kernel<(F)>, dim3(grid), dim3(R2_THREADS), 0, as_stream(stream), *a); \
+        break;
+            R2_CASE(0)
+            R2_CASE(DPVO_RG_RELU)
+            R2_CASE(DPVO_RG_SIGMOID)
+            R2_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
+            R2_CASE(DPVO_RG_RES)
+            R2_CASE(DPVO_RG_RES | DPVO_RG_LN)
+            R2_CASE(DPVO_RG_GATE | DPVO_RG_LN)
+            R2_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
+            R2_CASE(DPVO_RG_GATE)
+#undef R2_CASE
+        default:
+            set_error("dpvo_rowgemm: unsupported epilogue flag combination " + std::to_string(f));
+            return -1;
+        }
+        DPVO_CHECK_LAUNCH();
+        return 0;
     }
     const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
     const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
