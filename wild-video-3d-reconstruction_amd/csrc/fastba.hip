@@ -614,9 +614,12 @@ __device__ __forceinline__ double readlane_d(double v, int lane)
 
 // n6 <= 64: one wave, lane r holds row r of the system in registers (fully
 // unrolled, compile-time column indices).  Column j of L is broadcast through
-// LDS (one ds_write per lane, broadcast ds_read2 of the column): no readlane
-// round trips and no per-element branches.  fp64 right-looking Cholesky and
-// forward / backward substitution -- the arithmetic of ba_solve_kernel.
+// LDS (one ds_write per lane, broadcast reads of the column): no readlane
+// round trips and no per-element branches.  Right-looking Cholesky and
+// forward / backward substitution in fp32 -- the precision of the reference,
+// which factors the float32 S with torch::linalg::cholesky (ba_cuda.cu:518-521).
+// A single wave has no partner to hide latency behind, so the short fp32
+// sqrt / div chains (vs fp64) are what sets this kernel's time.
 __device__ __forceinline__ void wave_lds_fence()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -625,12 +628,13 @@ __device__ __forceinline__ void wave_lds_fence()
 
 __global__ __launch_bounds__(64) void ba_solve_wave_kernel(BaParams p)
 {
-    __shared__ double col[64];
-    __shared__ double Lsh[64 * 65];
+    typedef float RT;
+    __shared__ RT col[64];
+    __shared__ RT Lsh[64 * 65];
     __shared__ double yv[64];
     if (failed(p)) return;
     const int n = p.n6, r = threadIdx.x;
-    double a[64];
+    RT a[64];
     // unconditional loads from clamped (valid) indices, then select: a load
     // under a per-element condition makes hipcc wait vmcnt(0) per element
     const int rc = r < n ? r : n - 1;
@@ -644,25 +648,25 @@ __global__ __launch_bounds__(64) void ba_solve_wave_kernel(BaParams p)
     }
 #pragma unroll
     for (int c = 0; c < 64; c++) {
-        double s = (double)(bv[c] - sv[c]);
-        if (r == c) s += 1e-4 * s + 1.0;
-        a[c] = (r < n && c < n) ? s : 0.0;
+        RT s = bv[c] - sv[c];
+        if (r == c) s += (RT)1e-4 * s + (RT)1.0;
+        a[c] = (r < n && c < n) ? s : (RT)0;
     }
     const float v_r = p.v[rc], y_r = p.y[rc];
-    double y = r < n ? (double)(v_r - y_r) : 0.0;
+    RT y = r < n ? (RT)(v_r - y_r) : (RT)0;
     int fail = 0;
 #pragma unroll
     for (int j = 0; j < 64; j++) {
         if (j >= n || fail) break;
         col[r] = a[j];
         wave_lds_fence();
-        const double djj = col[j];
-        if (!(djj > 0.0)) {
+        const RT djj = col[j];
+        if (!(djj > (RT)0)) {
             fail = j + 1;
             break;
         }
-        const double ljj = sqrt(djj);
-        const double l = r > j ? a[j] / ljj : (r == j ? ljj : 0.0);
+        const RT ljj = sqrt(djj);
+        const RT l = r > j ? a[j] / ljj : (r == j ? ljj : (RT)0);
         a[j] = l;
         wave_lds_fence();
         col[r] = l;
@@ -680,22 +684,22 @@ __global__ __launch_bounds__(64) void ba_solve_wave_kernel(BaParams p)
     for (int c = 0; c < 64; c++) Lsh[r * 65 + c] = a[c];
     wave_lds_fence();
     for (int j = 0; j < n; j++) {
-        if (r == j) col[0] = y / a_diag_lds(Lsh, j);
+        if (r == j) col[0] = y / Lsh[j * 65 + j];
         wave_lds_fence();
-        const double zj = col[0];
+        const RT zj = col[0];
         if (r == j) y = zj;
         else if (r > j) y -= Lsh[r * 65 + j] * zj;
         wave_lds_fence();
     }
     for (int j = n - 1; j >= 0; j--) {
-        if (r == j) col[0] = y / a_diag_lds(Lsh, j);
+        if (r == j) col[0] = y / Lsh[j * 65 + j];
         wave_lds_fence();
-        const double xj = col[0];
+        const RT xj = col[0];
         if (r == j) y = xj;
         else if (r < j) y -= Lsh[j * 65 + r] * xj;
         wave_lds_fence();
     }
-    if (r < n) yv[r] = y;
+    if (r < n) yv[r] = (double)y;
     wave_lds_fence();
     ba_retract_and_reset(p, yv, r, 64);
 }
