@@ -94,17 +94,20 @@ class CorrProbe:
         self.pairs = []
 
     def wrap(self, slam):
-        inner = slam.corr
+        """Events bracket exactly the fused-altcorr launch (dpvo.altcorr.corr_pyramid,
+        called by DPVO.corr), on the current stream -- the stream it runs on."""
+        from dpvo import altcorr
+        inner = altcorr.corr_pyramid
 
-        def corr(coords, indicies=None):
+        def corr_pyramid(*a, **k):
             s = torch.cuda.Event(enable_timing=True)
             e = torch.cuda.Event(enable_timing=True)
             s.record()
-            out = inner(coords, indicies)
+            out = inner(*a, **k)
             e.record()
             self.pairs.append((s, e))
             return out
-        slam.corr = corr
+        altcorr.corr_pyramid = corr_pyramid
 
     def mean_ms(self):
         ts = [s.elapsed_time(e) for s, e in self.pairs]
@@ -243,7 +246,7 @@ def main():
                        "patches_per_frame": slam.M, "buffer": args.buffer, "n_keyframes": slam.n, "edges": E,
                        "ba_iterations": slam.cfg.BA_ITERATIONS, "image": "512x384",
                        "parallelism": f"replicas{world}"},
-            "roofline": {"kernel": "corr_fast_kernel<2> (fused 2-level altcorr)", "bound": "hbm",
+            "roofline": {"kernel": "corr_sfast_kernel<2,16> (fused 2-level altcorr)", "bound": "hbm",
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "bytes_per_edge": CORR_BYTES_PER_EDGE, "avg_launch_ms": round(corr_ms, 5)},

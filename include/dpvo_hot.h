@@ -68,12 +68,23 @@ int dpvo_corr_forward_pyramid(int dtype, const void* gmap, const int64_t* gmap_s
 
 /* Same, with consecutive edges `edge_stride` elements apart (0 = packed), so
  * the update operator's first Linear can read 16-byte aligned rows
- * (882 features padded to 896; pad columns are left untouched). */
+ * (882 features padded to 896; pad columns are left untouched), and with the
+ * gmap's packed scalar-operand table from dpvo_corr_pack (NULL: packed
+ * internally into stream-ordered scratch on every call). */
 int dpvo_corr_forward_pyramid_ld(int dtype, const void* gmap, const int64_t* gmap_size, const int64_t* gmap_stride,
                                  int nlev, const void* const* fmaps, const int64_t* fmap_sizes,
                                  const int64_t* fmap_strides, const float* level_scale, const float* coords,
                                  const int64_t* coords_size, const int64_t* coords_stride, const int64_t* ii,
-                                 const int64_t* jj, int radius, void* corr, int64_t edge_stride, void* stream);
+                                 const int64_t* jj, int radius, void* corr, int64_t edge_stride, const void* table,
+                                 void* stream);
+
+/* The fp16 fast path reads patch features as scalar operands from a packed
+ * table [B*N1][C][5] dwords ((p0,p1)(p2,p3)(p4,p5)(p6,p7)(p8,0) per channel).
+ * Pack once per gmap change (a new keyframe) and pass it to
+ * dpvo_corr_forward_pyramid_ld; table is 16-byte aligned, size from
+ * dpvo_corr_table_bytes. */
+size_t dpvo_corr_table_bytes(const int64_t* gmap_size);
+int dpvo_corr_pack(const void* gmap, const int64_t* gmap_size, const int64_t* gmap_stride, void* table, void* stream);
 
 /* cuda_corr.backward (correlation_kernel.cu:236-286): grad is the returned
  * (permuted) view's gradient given as contiguous [B][E][2r+1 (x)][2r+1 (y)][P][P]

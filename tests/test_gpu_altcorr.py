@@ -191,3 +191,15 @@ def test_nan_coordinates_follow_reference_conversion():
     assert np.array_equal(np.isnan(out), np.isnan(ref))
     ok = ~np.isnan(ref)
     assert np.array_equal(out[ok], ref[ok])
+
+
+def test_packed_table_path_is_identical():
+    """dpvo_corr_pack + forward with the table == forward packing internally (bit-exact)."""
+    import cuda_corr
+    d = dev()
+    gmap, f1, f2, ii, jj, coords = dpvo_sized_inputs(7, E=500)
+    args = (gmap.to(d), [channel_last(f1.to(d)), channel_last(f2.to(d))], coords.to(d), ii.to(d), jj.to(d), 3, [1, 4])
+    a = cuda_corr.forward_pyramid(*args)
+    tab = cuda_corr.pack(gmap.to(d))
+    b = cuda_corr.forward_pyramid(*args, table=tab)
+    assert torch.equal(a.view(torch.int16), b.view(torch.int16))

@@ -691,7 +691,7 @@ bool fast_path_ok(int dtype, const int64_t* gsz, const int64_t* fsz, const int64
 int launch_fast(int nlev, const void* gmap, const int64_t* gsz, const int64_t* gst, const void* const* fmaps,
                 const int64_t* fsz, const int64_t* fst, const float* scales, const float* coords, const int64_t* csz,
                 const int64_t* cst, const int64_t* ii, const int64_t* jj, void* out, const int64_t* ostr,
-                hipStream_t stream)
+                hipStream_t stream, const void* table = nullptr)
 {
     CorrFastParams p{};
     p.gmap = (const half_t*)gmap;
@@ -724,21 +724,26 @@ int launch_fast(int nlev, const void* gmap, const int64_t* gsz, const int64_t* g
         return v ? atoi(v) : 3;
     }();
     if (version == 3) {
-        // patch features -> scalar-load table (stream-ordered scratch)
-        const size_t tab_bytes = (size_t)p.B * p.N1 * p.C * 5 * 4;
+        // patch features as a scalar-load table: the caller's (dpvo_corr_pack), or
+        // packed here into stream-ordered scratch
         void* tab = nullptr;
-        if (hipMallocAsync(&tab, tab_bytes, stream) != hipSuccess) return 2;
-        const int64_t np = (int64_t)p.B * p.N1 * p.C;
-        hipLaunchKernelGGL(corr_pack_kernel, dim3(grid_for(np, 256, 8192)), dim3(256), 0, stream, p.gmap, p.g_s[0],
-                           p.g_s[1], p.g_s[2], p.g_s[3], p.g_s[4], p.B, p.N1, p.C, (uint32_t*)tab);
-        p.f1tab = (const uint32_t*)tab;
+        if (table) {
+            p.f1tab = (const uint32_t*)table;
+        } else {
+            const size_t tab_bytes = (size_t)p.B * p.N1 * p.C * 5 * 4;
+            if (hipMallocAsync(&tab, tab_bytes, stream) != hipSuccess) return 2;
+            const int64_t np = (int64_t)p.B * p.N1 * p.C;
+            hipLaunchKernelGGL(corr_pack_kernel, dim3(grid_for(np, 256, 8192)), dim3(256), 0, stream, p.gmap,
+                               p.g_s[0], p.g_s[1], p.g_s[2], p.g_s[3], p.g_s[4], p.B, p.N1, p.C, (uint32_t*)tab);
+            p.f1tab = (const uint32_t*)tab;
+        }
         if (nlev == 2)
             hipLaunchKernelGGL((corr_sfast_kernel<2, 16>), dim3((unsigned)nblk), dim3(FastThreads<2>::value), 0,
                                stream, p);
         else
             hipLaunchKernelGGL((corr_sfast_kernel<1, 16>), dim3((unsigned)nblk), dim3(FastThreads<1>::value), 0,
                                stream, p);
-        (void)hipFreeAsync(tab, stream);
+        if (tab) (void)hipFreeAsync(tab, stream);
         return 0;
     }
     if (nlev == 2)
@@ -825,7 +830,7 @@ extern "C" int dpvo_corr_forward_pyramid(int dtype, const void* gmap, const int6
 {
     return dpvo_corr_forward_pyramid_ld(dtype, gmap, gmap_size, gmap_stride, nlev, fmaps, fmap_sizes, fmap_strides,
                                         level_scale, coords, coords_size, coords_stride, ii, jj, radius, corr, 0,
-                                        stream);
+                                        nullptr, stream);
 }
 
 extern "C" int dpvo_corr_forward_pyramid_ld(int dtype, const void* gmap, const int64_t* gmap_size,
@@ -834,7 +839,7 @@ extern "C" int dpvo_corr_forward_pyramid_ld(int dtype, const void* gmap, const i
                                             const float* level_scale, const float* coords,
                                             const int64_t* coords_size, const int64_t* coords_stride,
                                             const int64_t* ii, const int64_t* jj, int radius, void* corr,
-                                            int64_t edge_stride, void* stream)
+                                            int64_t edge_stride, const void* table, void* stream)
 {
     DPVO_CHECK_ARG(check_common(dtype, gmap, gmap_size, coords_size, ii, jj, radius, corr),
                    "invalid arguments (dtype/radius/shapes)");
@@ -853,7 +858,7 @@ extern "C" int dpvo_corr_forward_pyramid_ld(int dtype, const void* gmap, const i
     if (all_fast) {
         const int64_t ostr[6] = {E * o_e, o_e, 1, Do * P2 * nlev, P2 * nlev, nlev};
         const int rc = launch_fast(nlev, gmap, gmap_size, gmap_stride, fmaps, fmap_sizes, fmap_strides, level_scale,
-                                   coords, coords_size, coords_stride, ii, jj, corr, ostr, as_stream(stream));
+                                   coords, coords_size, coords_stride, ii, jj, corr, ostr, as_stream(stream), table);
         if (rc == 0) { DPVO_CHECK_LAUNCH(); return 0; }
     }
     for (int l = 0; l < nlev; l++) {
@@ -932,6 +937,26 @@ extern "C" int dpvo_patchify_backward(int dtype, const int64_t* nsz, const float
         hipLaunchKernelGGL(patchify_backward_kernel<double>, dim3(grid), dim3(256), 0, as_stream(stream),
                            (int)nsz[0], (int)nsz[1], (int)nsz[2], (int)nsz[3], coords, (int)M, radius,
                            (const double*)grad, (double*)net_grad, total);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" size_t dpvo_corr_table_bytes(const int64_t* gmap_size)
+{
+    return (size_t)(gmap_size[0] * gmap_size[1] * gmap_size[2]) * 5 * 4;
+}
+
+extern "C" int dpvo_corr_pack(const void* gmap, const int64_t* gmap_size, const int64_t* gmap_stride, void* table,
+                              void* stream)
+{
+    DPVO_CHECK_ARG(gmap && table, "null pointer");
+    DPVO_CHECK_ARG(gmap_size[3] == 3 && gmap_size[4] == 3, "the packed table is for 3x3 patches");
+    DPVO_CHECK_ARG(((uintptr_t)table & 15) == 0, "table must be 16-byte aligned");
+    const int64_t np = gmap_size[0] * gmap_size[1] * gmap_size[2];
+    if (np == 0) return 0;
+    hipLaunchKernelGGL(corr_pack_kernel, dim3(grid_for(np, 256, 8192)), dim3(256), 0, as_stream(stream),
+                       (const half_t*)gmap, gmap_stride[0], gmap_stride[1], gmap_stride[2], gmap_stride[3],
+                       gmap_stride[4], (int)gmap_size[0], (int)gmap_size[1], (int)gmap_size[2], (uint32_t*)table);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

@@ -34,7 +34,20 @@ def forward(fmap1, fmap2, coords, ii, jj, radius):
     return [out.permute(0, 1, 3, 2, 4, 5)]
 
 
-def forward_pyramid(fmap1, pyramid, coords, ii, jj, radius, scales, out=None):
+def pack(fmap1, out=None):
+    """Patch features -> the fast path's scalar-operand table (dpvo_corr_pack).
+    Re-pack whenever fmap1 (the gmap ring) changes."""
+    H.on_gpu(fmap1)
+    if fmap1.dtype != torch.float16 or fmap1.dim() != 5:
+        raise RuntimeError("pack: fmap1 must be an fp16 [B, N1, C, 3, 3] tensor")
+    nbytes = H.lib().dpvo_corr_table_bytes(H.sizes(fmap1))
+    if out is None or out.numel() * out.element_size() < nbytes:
+        out = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=fmap1.device)
+    H.check(H.lib().dpvo_corr_pack(H.ptr(fmap1), H.sizes(fmap1), H.strides(fmap1), H.ptr(out), H.stream_of(fmap1)))
+    return out
+
+
+def forward_pyramid(fmap1, pyramid, coords, ii, jj, radius, scales, out=None, table=None):
     """Fused form of DPVO.corr (dpvo/dpvo.py:326-333): all levels in one
     launch, returned in the stacked layout torch.stack([...], -1).view(B, E, -1).
     ``out`` may be a [B, E, F] view of wider rows (e.g. F = 882 of 896)."""
@@ -57,7 +70,7 @@ def forward_pyramid(fmap1, pyramid, coords, ii, jj, radius, scales, out=None):
     H.check(H.lib().dpvo_corr_forward_pyramid_ld(
         H.dtype_code(fmap1), H.ptr(fmap1), H.sizes(fmap1), H.strides(fmap1), L, ptrs, fs, fst, sc, H.ptr(coords),
         H.sizes(coords), H.strides(coords), H.ptr(ii), H.ptr(jj), int(radius), H.ptr(out),
-        out.stride(1) if E > 0 else 0, H.stream_of(fmap1)))
+        out.stride(1) if E > 0 else 0, H.ptr(table), H.stream_of(fmap1)))
     return out
 
 

@@ -53,9 +53,10 @@ def corr(fmap1, fmap2, coords, ii, jj, radius=1, dropout=1):
     return CorrLayer.apply(fmap1, fmap2, coords, ii, jj, radius, dropout)
 
 
-def corr_pyramid(gmap, pyramid, coords, ii, jj, radius=3, levels=(1, 4), out=None):
+def corr_pyramid(gmap, pyramid, coords, ii, jj, radius=3, levels=(1, 4), out=None, table=None):
     """All pyramid levels in one fused launch, already in the stacked layout
     DPVO.corr builds with torch.stack(..., -1).view(1, E, -1) (dpvo.py:326-333).
-    ``out``: optional [1, E, F] destination view (rows may be wider than F).
+    ``out``: optional [1, E, F] destination view (rows may be wider than F);
+    ``table``: gmap packed by cuda_corr.pack (packed per call when None).
     Inference only (no autograd)."""
-    return cuda_corr.forward_pyramid(gmap, list(pyramid), coords, ii, jj, radius, list(levels), out=out)
+    return cuda_corr.forward_pyramid(gmap, list(pyramid), coords, ii, jj, radius, list(levels), out=out, table=table)

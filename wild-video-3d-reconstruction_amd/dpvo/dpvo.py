@@ -16,6 +16,8 @@ MI355X-specific choices (all behind the same API):
 import torch
 import torch.nn.functional as F
 
+import cuda_corr
+
 from . import altcorr, fastba
 from . import projective_ops as pops
 from .lietorch import SE3, stack
@@ -169,13 +171,24 @@ class DPVO:
         ii1 = ii % (self.M * self.pmem)
         jj1 = jj % self.pmem
         E = len(ii)
-        out = None
+        out = table = None
         if self.gmap_.dtype == torch.float16:
             # rows padded to 896 (zeros past 882): the update operator's first
             # Linear reads them as 16-byte aligned GEMM rows without a copy
             buf = self._corr_rows(E)
             out = buf[:E, :CORR_DIM].unsqueeze(0)
-        return altcorr.corr_pyramid(self.gmap, self.pyramid, coords, ii1, jj1, 3, (1, 4), out=out).view(1, E, -1)
+            table = self._gmap_table()
+        return altcorr.corr_pyramid(self.gmap, self.pyramid, coords, ii1, jj1, 3, (1, 4), out=out,
+                                    table=table).view(1, E, -1)
+
+    def _gmap_table(self):
+        """The gmap ring packed for altcorr's scalar-operand path, re-packed only
+        when the ring changed (torch's in-place version counter: new keyframes)."""
+        key = (self.gmap_.data_ptr(), self.gmap_._version)
+        if getattr(self, "_gtab_key", None) != key:
+            self._gtab = cuda_corr.pack(self.gmap, out=getattr(self, "_gtab", None))
+            self._gtab_key = key
+        return self._gtab
 
     def _corr_rows(self, E):
         buf = getattr(self, "_corr_buf", None)
