@@ -137,6 +137,17 @@ size_t dpvo_neighbors_workspace_bytes(int64_t num_edges);
 int dpvo_neighbors(const int64_t* ii, const int64_t* jj, int64_t num_edges, int64_t* ix, int64_t* jx,
                    void* workspace, size_t workspace_bytes, void* stream);
 
+/* cuda_ba.solve_system (ba.cpp:174-234), normal equations on the device:
+ * J_i, J_j [r][7][7] float, ii, jj [r] int64, res [r][7] float ->
+ * A = J^T J (m x m, fp64, row-major) and b = -J^T res (fp64), with
+ * diag(A) <- diag(A) (1 + lm) + ep; rows/columns >= m are dropped (m = 7n,
+ * or 7 * freen for the reference's top-left solve).  *status = 1 when an
+ * edge has ii == jj (the reference exits the process there).  The factor /
+ * solve is a dense fp64 Cholesky (the shim uses rocSOLVER through torch). */
+int dpvo_solve_system_assemble(const float* J_i, const float* J_j, const int64_t* ii, const int64_t* jj,
+                               const float* res, int64_t r, int64_t m, float ep, float lm, double* A, double* b,
+                               int* status, void* stream);
+
 /* ------------------------------------------------------------------------
  * lietorch -- replaces lietorch_backends (reference lietorch.cpp:286-316)
  * group: 1 = SO3, 3 = SE3 (dispatch.h:16-31); dtype F32 or F64.

@@ -243,3 +243,29 @@ def gather_rows(x, idx):
     ok = idx >= 0
     out[ok] = x[idx[ok]]
     return out
+
+
+def solve_system(Ji, Jj, ii, jj, res, ep, lm, freen):
+    """cuda_ba.solve_system (reference dpvo/fastba/ba.cpp:174-234) in float64
+    numpy: J (7r x 7n) from the per-edge 7x7 blocks, A = J^T J, b = -J^T res,
+    diag(A) += lm diag(A) + ep; solves all of A (freen < 0) or its top-left
+    7*freen block (rest of delta zero).  Eigen's SimplicialCholesky there; a
+    dense solve here (same solution up to rounding)."""
+    Ji = np.asarray(Ji, np.float64)
+    Jj = np.asarray(Jj, np.float64)
+    res = np.asarray(res, np.float64).reshape(-1, 7)
+    ii = np.asarray(ii, np.int64)
+    jj = np.asarray(jj, np.int64)
+    r = len(ii)
+    n = int(max(ii.max(), jj.max())) + 1
+    J = np.zeros((7 * r, 7 * n))
+    for x in range(r):
+        J[7 * x:7 * x + 7, 7 * ii[x]:7 * ii[x] + 7] += Ji[x]
+        J[7 * x:7 * x + 7, 7 * jj[x]:7 * jj[x] + 7] += Jj[x]
+    A = J.T @ J
+    b = -(J.T @ res.reshape(-1))
+    A[np.diag_indices_from(A)] += A.diagonal() * lm + ep
+    m = 7 * n if freen < 0 else 7 * freen
+    delta = np.zeros(7 * n)
+    delta[:m] = np.linalg.solve(A[:m, :m], b[:m])
+    return delta.reshape(n, 7).astype(np.float32)

@@ -184,3 +184,23 @@ def test_softagg_oracle_matches_torch_scatter_composition():
     want = scatter_sum(f * scatter_softmax(s, lab, 1, G), lab, 1, G)[0].numpy()
     got = oracle.softagg(f[0].numpy(), s[0].numpy(), lab.numpy(), G)
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=1e-12)
+
+
+def test_solve_system_oracle_normal_equations():
+    """oracle.solve_system solves (J^T J + lm diag + ep I) delta = -J^T res -- the
+    restatement of ba.cpp:174-234 (Eigen absent: parity unpinned by fixtures)."""
+    g = np.random.default_rng(0)
+    n, r = 6, 8
+    ii = np.array([0, 1, 2, 3, 4, 0, 1, 2])
+    jj = np.array([1, 2, 3, 4, 5, 3, 4, 5])
+    Ji = g.normal(size=(r, 7, 7))
+    Jj = g.normal(size=(r, 7, 7))
+    res = g.normal(size=(r, 7))
+    d = oracle.solve_system(Ji, Jj, ii, jj, res, 1e-4, 1e-3, -1).astype(np.float64).reshape(-1)
+    J = np.zeros((7 * r, 7 * n))
+    for x in range(r):
+        J[7 * x:7 * x + 7, 7 * ii[x]:7 * ii[x] + 7] = Ji[x]
+        J[7 * x:7 * x + 7, 7 * jj[x]:7 * jj[x] + 7] = Jj[x]
+    A = J.T @ J
+    A += np.diag(np.diag(A) * 1e-3 + 1e-4)
+    np.testing.assert_allclose(A @ d, -J.T @ res.reshape(-1), rtol=1e-4, atol=1e-4)

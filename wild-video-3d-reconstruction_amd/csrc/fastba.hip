@@ -986,3 +986,90 @@ extern "C" int dpvo_neighbors(const int64_t* ii, const int64_t* jj, int64_t num_
     DPVO_CHECK_LAUNCH();
     return 0;
 }
+
+// ---------------------------------------------------------------------------
+// cuda_ba.solve_system (ba.cpp:174-234): loop-closure pose-graph normal
+// equations.  J (7r x 7n) has per-edge 7x7 blocks J_i at (x, i) and J_j at
+// (x, j); A = J^T J and b = -J^T res in fp64 (the reference's Eigen double
+// sparse matrices), diag(A) <- diag(A) (1 + lm) + ep.  Rows / columns >= m
+// (= 7 * freen, or 7n) are dropped: the reference solves only the top-left
+// block there.  One thread per (edge, 7x7 output entry); fp64 atomics.
+// ---------------------------------------------------------------------------
+namespace dpvo {
+__global__ __launch_bounds__(256) void ss_assemble_kernel(const float* __restrict__ Ji, const float* __restrict__ Jj,
+                                                          const int64_t* __restrict__ ii,
+                                                          const int64_t* __restrict__ jj,
+                                                          const float* __restrict__ res, int64_t r, int64_t m,
+                                                          double* __restrict__ A, double* __restrict__ b,
+                                                          int* __restrict__ status)
+{
+    const int64_t total = r * 49;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x = t / 49;
+        const int kl = (int)(t - x * 49), k = kl / 7, l = kl - k * 7;   // output entry (row l of block, column k)
+        const int64_t i = ii[x], j = jj[x];
+        if (i == j) {   // the reference calls exit(1) here (ba.cpp:205-206)
+            atomicExch(status, 1);
+            continue;
+        }
+        const float* Ai = Ji + x * 49;
+        const float* Aj = Jj + x * 49;
+        // (J^T J) entries: sum over the 7 residual rows q of J[q][l] J[q][k]
+        double sii = 0, sjj = 0, sij = 0, sji = 0;
+#pragma unroll
+        for (int q = 0; q < 7; q++) {
+            const double il = Ai[q * 7 + l], ik = Ai[q * 7 + k], jl = Aj[q * 7 + l], jk = Aj[q * 7 + k];
+            sii += il * ik;
+            sjj += jl * jk;
+            sij += il * jk;
+            sji += jl * ik;
+        }
+        const int64_t ri = 7 * i + l, rj = 7 * j + l, ci = 7 * i + k, cj = 7 * j + k;
+        if (ri < m && ci < m) atomicAdd(&A[ri * m + ci], sii);
+        if (rj < m && cj < m) atomicAdd(&A[rj * m + cj], sjj);
+        if (ri < m && cj < m) atomicAdd(&A[ri * m + cj], sij);
+        if (rj < m && ci < m) atomicAdd(&A[rj * m + ci], sji);
+        if (k == 0) {   // b = -J^T res, row l of both blocks
+            double bi = 0, bj = 0;
+#pragma unroll
+            for (int q = 0; q < 7; q++) {
+                const double rq = res[x * 7 + q];
+                bi += Ai[q * 7 + l] * rq;
+                bj += Aj[q * 7 + l] * rq;
+            }
+            if (ri < m) atomicAdd(&b[ri], -bi);
+            if (rj < m) atomicAdd(&b[rj], -bj);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void ss_damp_kernel(double* A, int64_t m, double ep, double lm)
+{
+    for (int64_t d = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; d < m; d += (int64_t)gridDim.x * blockDim.x) {
+        double& a = A[d * m + d];
+        a = a + a * lm + ep;
+    }
+}
+}  // namespace dpvo
+
+extern "C" int dpvo_solve_system_assemble(const float* J_i, const float* J_j, const int64_t* ii, const int64_t* jj,
+                                          const float* res, int64_t r, int64_t m, float ep, float lm, double* A,
+                                          double* b, int* status, void* stream)
+{
+    DPVO_CHECK_ARG(r >= 0 && m >= 0, "bad sizes");
+    DPVO_CHECK_ARG(m == 0 || (A && b), "A / b missing");
+    hipStream_t s = as_stream(stream);
+    if (m > 0) {
+        DPVO_CHECK_HIP(hipMemsetAsync(A, 0, (size_t)(m * m) * sizeof(double), s));
+        DPVO_CHECK_HIP(hipMemsetAsync(b, 0, (size_t)m * sizeof(double), s));
+    }
+    if (status) DPVO_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
+    if (r > 0 && m > 0) {
+        hipLaunchKernelGGL(ss_assemble_kernel, dim3(grid_for(r * 49, 256, 8192)), dim3(256), 0, s, J_i, J_j, ii, jj,
+                           res, r, m, A, b, status);
+    }
+    if (m > 0) hipLaunchKernelGGL(ss_damp_kernel, dim3(grid_for(m, 256, 1024)), dim3(256), 0, s, A, m, (double)ep,
+                                  (double)lm);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}

@@ -82,6 +82,34 @@ def reproject(poses, patches, intrinsics, ii, jj, kk):
 
 
 def solve_system(J_Ginv_i, J_Ginv_j, ii, jj, res, ep, lm, freen):
-    """ba.cpp:181-241 (loop-closure PGO, Eigen sparse Cholesky) -- not built yet
-    for MI355X (a later-round item)."""
-    raise NotImplementedError("cuda_ba.solve_system is not implemented in the MI355X build yet")
+    """ba.cpp:174-234 (loop-closure PGO): -> [delta [n, 7]] on res.device.
+
+    A = J^T J, b = -J^T res (fp64) are assembled on the device
+    (dpvo_solve_system_assemble); the reference's Eigen SimplicialCholesky is a
+    dense fp64 Cholesky here (rocSOLVER via torch.linalg).  freen >= 0 solves
+    only the top-left 7*freen block (the rest of delta is zero), like the
+    reference.  An edge with ii == jj raises (the reference calls exit(1))."""
+    H.on_gpu(J_Ginv_i, J_Ginv_j, ii, jj, res)
+    dev = res.device
+    Ji = J_Ginv_i.to(dev, torch.float32).contiguous()
+    Jj = J_Ginv_j.to(dev, torch.float32).contiguous()
+    rr = res.to(dev, torch.float32).contiguous().view(-1, 7)
+    ii, jj = H.idx64(ii.to(dev)), H.idx64(jj.to(dev))
+    r = rr.shape[0]
+    if Ji.shape != (r, 7, 7) or Jj.shape != (r, 7, 7) or ii.numel() != r or jj.numel() != r:
+        raise RuntimeError("solve_system: J_Ginv_i/J_Ginv_j must be [r, 7, 7], ii/jj [r], res [r, 7]")
+    n = int(torch.maximum(ii.max(), jj.max()).item()) + 1 if r else 0
+    m = 7 * n if int(freen) < 0 else min(7 * int(freen), 7 * n)
+    A = torch.empty(m, m, dtype=torch.float64, device=dev)
+    b = torch.empty(m, dtype=torch.float64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    H.check(H.lib().dpvo_solve_system_assemble(H.ptr(Ji), H.ptr(Jj), H.ptr(ii), H.ptr(jj), H.ptr(rr), r, m,
+                                               float(ep), float(lm), H.ptr(A), H.ptr(b), H.ptr(status),
+                                               H.stream_of(res)))
+    if int(status.item()):
+        raise RuntimeError("solve_system: an edge with ii == jj (the reference exits the process, ba.cpp:205)")
+    delta = torch.zeros(7 * n, dtype=torch.float32, device=dev)
+    if m:
+        L = torch.linalg.cholesky(A)
+        delta[:m] = torch.cholesky_solve(b[:, None], L)[:, 0].float()
+    return [delta.view(n, 7)]
