@@ -80,6 +80,7 @@ struct LevelMeta {
     int fy[corr::NP], fx[corr::NP];
     float xs[corr::NP], ys[corr::NP];
     int fast, oy, ox, bw, bh, nslots, first_slot, pad;
+    float rbw;   // 1 / bw (v3 decode: exact floor((loc + 0.5) / bw) for loc < 128)
 };
 
 template <int NLEV, int C8>
@@ -325,6 +326,11 @@ __global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_sfast_kernel(Co
     constexpr int C = C8 * 8;
     __shared__ half_t raw[NLEV][NP][BOX * BOX];
     __shared__ LevelMeta meta[NLEV];
+    // per (patch pixel, level): the reference's bilinear weights (each product
+    // rounded to binary16 exactly as correlation_kernel.cu:221-232 forms them)
+    // and the raw-tile offset of the window origin
+    struct EpiQ { half_t w00, w01, w10, w11; int base, bw; };
+    __shared__ EpiQ epq[NP * NLEV];
 
     const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
     const int b = bid / p.E, e = bid - b * p.E;
@@ -360,8 +366,28 @@ __global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_sfast_kernel(Co
         m.bh = m.fast ? (ymax - ymin) + D : D;
         m.bw = m.fast ? (xmax - xmin) + D : D;
         m.nslots = m.fast ? m.bh * m.bw : NP * D * D;
+        m.rbw = 1.0f / (float)m.bw;
     }
     __syncthreads();
+    if (tid < NP * NLEV) {   // epilogue constants, index qi = q * NLEV + lev (output order)
+        const int q = tid / NLEV, lev = tid - q * NLEV;
+        const LevelMeta& m = meta[lev];
+        const int bw = m.fast ? m.bw : D;
+        const int oy = m.fast ? m.fy[q] - (int)wrap_add(m.oy, R) : 0;
+        const int ox = m.fast ? m.fx[q] - (int)wrap_add(m.ox, R) : 0;
+        const float xq = m.xs[q], yq = m.ys[q];
+        const half_t dx = (half_t)(xq - floorf(xq));
+        const half_t dy = (half_t)(yq - floorf(yq));
+        const half_t one = (half_t)1.0f;
+        const half_t omdx = one - dx, omdy = one - dy;
+        EpiQ& t = epq[tid];
+        t.w00 = hmul(omdx, omdy);
+        t.w01 = hmul(dx, omdy);
+        t.w10 = hmul(omdx, dy);
+        t.w11 = hmul(dx, dy);
+        t.base = oy * bw + ox;
+        t.bw = bw;
+    }
     const int n0 = meta[0].nslots;
     const int total = NLEV == 2 ? n0 + meta[NLEV - 1].nslots : n0;
 
@@ -375,7 +401,7 @@ __global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_sfast_kernel(Co
         const int loc = s.lev ? sl - n0 : sl;
         int gy, gx;
         if (m.fast) {
-            const int uy = loc / m.bw, ux = loc - uy * m.bw;
+            const int uy = (int)(((float)loc + 0.5f) * m.rbw), ux = loc - uy * m.bw;
             gy = wrap_add(m.oy, uy); gx = wrap_add(m.ox, ux);
             s.u = loc;
         } else {
@@ -474,28 +500,23 @@ __global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_sfast_kernel(Co
     __syncthreads();
 
     half_t* ob = p.out + b * p.o_b + (int64_t)e * p.o_e;
-    for (int o = tid; o < NLEV * NP * DO * DO; o += NT) {
-        const int lev = o % NLEV;
-        int r = o / NLEV;
-        const int q = r % NP; r /= NP;
-        const int a = r % DO;
-        const int bx = r / DO;
-        const LevelMeta& m = meta[lev];
-        const int bw = m.fast ? m.bw : D;
-        const int oy = m.fast ? m.fy[q] - (int)wrap_add(m.oy, R) : 0;
-        const int ox = m.fast ? m.fx[q] - (int)wrap_add(m.ox, R) : 0;
-        const half_t* t = &raw[lev][q][(oy + a) * bw + (ox + bx)];
-        const half_t c00 = t[0], c01 = t[1], c10 = t[bw], c11 = t[bw + 1];
-        const float xq = m.xs[q], yq = m.ys[q];
-        const half_t dx = (half_t)(xq - floorf(xq));
-        const half_t dy = (half_t)(yq - floorf(yq));
-        const half_t one = (half_t)1.0f;
-        const half_t omdx = one - dx, omdy = one - dy;
-        half_t v = hmul(hmul(omdx, omdy), c00);
-        v = hadd(v, hmul(hmul(dx, omdy), c01));
-        v = hadd(v, hmul(hmul(omdx, dy), c10));
-        v = hadd(v, hmul(hmul(dx, dy), c11));
-        ob[bx * p.o_x + a * p.o_y + q * p.o_p + lev * p.o_l] = v;
+    // thread -> fixed (patch pixel, level) qi, walking the 49 window positions
+    constexpr int NQ = NP * NLEV, GR = NT / NQ;
+    if (tid < NQ * GR) {
+        const int qi = tid % NQ, g = tid / NQ;
+        const int q = qi / NLEV, lev = qi - q * NLEV;
+        const EpiQ t = epq[qi];
+        const half_t* rt = &raw[lev][q][t.base];
+        half_t* oq = ob + q * p.o_p + lev * p.o_l;
+        for (int pos = g; pos < DO * DO; pos += GR) {
+            const int bx = pos / DO, a = pos - bx * DO;
+            const half_t* c = rt + a * t.bw + bx;
+            half_t v = hmul(t.w00, c[0]);
+            v = hadd(v, hmul(t.w01, c[1]));
+            v = hadd(v, hmul(t.w10, c[t.bw]));
+            v = hadd(v, hmul(t.w11, c[t.bw + 1]));
+            oq[bx * p.o_x + a * p.o_y] = v;
+        }
     }
 }
 
