@@ -381,21 +381,33 @@ static int64_t unique_sorted(const int64_t* kk, int64_t E, int64_t** kx_out, int
 }
 
 /* dense Cholesky (lower) in double; returns 0 on success, k+1 if the leading
- * minor of order k+1 is not positive definite (torch.linalg.cholesky info). */
+ * minor of order k+1 is not positive definite (torch.linalg.cholesky info).
+ * Row i's leading zeros (columns < first[i]) stay zero in L, so the inner
+ * products start at the later of the two rows' first nonzero: the terms
+ * skipped are exact zeros and the result equals the plain dense loop's. */
 static int cholesky_d(double* A, int n)
 {
+    int* first = (int*)malloc(sizeof(int) * (n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) {
+        int f = i;
+        for (int k = 0; k < i; k++)
+            if (A[i * n + k] != 0.0) { f = k; break; }
+        first[i] = f;
+    }
     for (int j = 0; j < n; j++) {
         double s = A[j * n + j];
-        for (int k = 0; k < j; k++) s -= A[j * n + k] * A[j * n + k];
-        if (!(s > 0.0)) return j + 1;
+        for (int k = first[j]; k < j; k++) s -= A[j * n + k] * A[j * n + k];
+        if (!(s > 0.0)) { free(first); return j + 1; }
         const double l = sqrt(s);
         A[j * n + j] = l;
         for (int i = j + 1; i < n; i++) {
+            if (first[i] > j) continue; /* A[i][j] is and stays 0 */
             double t = A[i * n + j];
-            for (int k = 0; k < j; k++) t -= A[i * n + k] * A[j * n + k];
+            for (int k = first[i] > first[j] ? first[i] : first[j]; k < j; k++) t -= A[i * n + k] * A[j * n + k];
             A[i * n + j] = t / l;
         }
     }
+    free(first);
     return 0;
 }
 
@@ -428,6 +440,7 @@ int oracle_ba_forward(float* poses, float* patches, const float* intrinsics, con
     float* dX = (float*)calloc((size_t)n6 + 1, sizeof(float));
     float* dZ = (float*)calloc((size_t)Mu + 1, sizeof(float));
     float* Q = (float*)calloc((size_t)Mu + 1, sizeof(float));
+    int* rows = (int*)calloc((size_t)n6 + 1, sizeof(int));
     int status = 0;
     const float fx = intrinsics[0], fy = intrinsics[1], cx = intrinsics[2], cy = intrinsics[3];
 
@@ -505,15 +518,26 @@ int oracle_ba_forward(float* poses, float* patches, const float* intrinsics, con
         if (N == 0) {
             for (int64_t k = 0; k < Mu; k++) dZ[k] = Q[k] * u[k];
         } else {
-            for (int a = 0; a < n6; a++) {
-                for (int b = 0; b < n6; b++) {
-                    double s = 0.0;
-                    for (int64_t k = 0; k < Mu; k++) s += (double)(Em[a * Mu + k] * Q[k]) * Em[b * Mu + k];
-                    S[a * n6 + b] = (double)Bm[a * n6 + b] - s;
+            /* S = B - (E Q) E^T, y = v - (E Q) u (ba_cuda.cu:510-515), summed
+             * over patches k in ascending order as the dense loop does, but
+             * visiting only each patch's nonzero E rows (the skipped products
+             * are exact zeros, so every sum is the dense loop's) */
+            memset(S, 0, sizeof(double) * n6 * n6);
+            memset(y, 0, sizeof(double) * n6);
+            for (int64_t k = 0; k < Mu; k++) {
+                int nr = 0;
+                for (int a = 0; a < n6; a++)
+                    if (Em[a * Mu + k] != 0.0f) rows[nr++] = a;
+                for (int i = 0; i < nr; i++) {
+                    const int a = rows[i];
+                    const double ea = (double)(Em[a * Mu + k] * Q[k]);
+                    for (int j = 0; j < nr; j++) S[a * n6 + rows[j]] += ea * Em[rows[j] * Mu + k];
+                    y[a] += ea * u[k];
                 }
-                double s = 0.0;
-                for (int64_t k = 0; k < Mu; k++) s += (double)(Em[a * Mu + k] * Q[k]) * u[k];
-                y[a] = (double)v[a] - s;
+            }
+            for (int a = 0; a < n6; a++) {
+                for (int b = 0; b < n6; b++) S[a * n6 + b] = (double)Bm[a * n6 + b] - S[a * n6 + b];
+                y[a] = (double)v[a] - y[a];
             }
             for (int a = 0; a < n6; a++) S[a * n6 + a] += 1e-4 * S[a * n6 + a] + 1.0;
             const int info = cholesky_d(S, n6);
@@ -553,7 +577,7 @@ int oracle_ba_forward(float* poses, float* patches, const float* intrinsics, con
             for (int64_t q = 0; q < PP; q++) pd[q] = dd;
         }
     }
-    free(Bm); free(Em); free(Cv); free(v); free(u); free(S); free(y); free(dX); free(dZ); free(Q);
+    free(Bm); free(Em); free(Cv); free(v); free(u); free(S); free(y); free(dX); free(dZ); free(Q); free(rows);
     free(kx); free(ku);
     return status;
 }

@@ -27,7 +27,21 @@ def dpvo_edges(n, M, lifetime=13, removal=None):
     return ii.astype(np.int64), jj.astype(np.int64), kk.astype(np.int64)
 
 
-def dpvo_state(seed, n=40, M=16, lifetime=13, removal=22, wd=128, ht=96, intr=(80.0, 80.0, 80.0, 60.0)):
+def global_edges(n):
+    """Frame pairs of the global BA's fixed pattern (dpvo.py:448-458):
+    i -> i+1, and every 5th frame i -> i+10 .. i+19."""
+    ie = list(range(n - 1))
+    je = list(range(1, n))
+    for i in range(0, n, 5):
+        for j in range(i + 10, min(i + 20, n)):
+            ie.append(i)
+            je.append(j)
+    return np.asarray(ie, np.int64), np.asarray(je, np.int64)
+
+
+def dpvo_frames(seed, n, M, wd=128, ht=96, intr=(80.0, 80.0, 80.0, 60.0)):
+    """Random-walk poses and random patches (centres on the 1/4-res grid,
+    inverse depth U[0.2, 1], constant over 3x3)."""
     g = np.random.default_rng(seed)
     poses = np.zeros((n, 7))
     poses[:, 6] = 1.0
@@ -45,10 +59,31 @@ def dpvo_state(seed, n=40, M=16, lifetime=13, removal=22, wd=128, ht=96, intr=(8
     patches[:, :, 2] = d[:, :, None, None]
     patches = patches.reshape(n * M, 3, 3, 3)
     intrinsics = np.tile(np.asarray(intr), (n, 1))
-    ii, jj, kk = dpvo_edges(n, M, lifetime, removal)
+    return g, poses, patches, intrinsics
+
+
+def with_edges(g, n, M, poses, patches, intrinsics, ii, jj, kk):
+    """targets = reprojected centres + N(0, 1) px, weights U[0, 1]."""
     coords = oracle.transform(poses, patches, intrinsics, ii, jj, kk)[0]
     target = coords[:, 1, 1, :] + g.normal(0, 1.0, size=(len(ii), 2))
     weight = g.uniform(0.0, 1.0, size=(len(ii), 2))
     return dict(n=n, M=M, poses=poses.astype(np.float32), patches=patches.astype(np.float32),
                 intrinsics=intrinsics.astype(np.float32), ii=ii, jj=jj, kk=kk,
                 target=target.astype(np.float32)[None], weight=weight.astype(np.float32)[None])
+
+
+def dpvo_state(seed, n=40, M=16, lifetime=13, removal=22, wd=128, ht=96, intr=(80.0, 80.0, 80.0, 60.0)):
+    g, poses, patches, intrinsics = dpvo_frames(seed, n, M, wd, ht, intr)
+    ii, jj, kk = dpvo_edges(n, M, lifetime, removal)
+    return with_edges(g, n, M, poses, patches, intrinsics, ii, jj, kk)
+
+
+def global_state(seed, n=160, M=6):
+    """The global BA's patch edges (dpvo.py:461-474): every patch of frame i
+    on every frame pair (i, j) of the fixed pattern."""
+    g, poses, patches, intrinsics = dpvo_frames(seed, n, M)
+    ie, je = global_edges(n)
+    ii = np.repeat(ie, M)
+    jj = np.repeat(je, M)
+    kk = (ie[:, None] * M + np.arange(M)[None]).reshape(-1).astype(np.int64)
+    return with_edges(g, n, M, poses, patches, intrinsics, ii, jj, kk)

@@ -144,7 +144,9 @@ __device__ __forceinline__ void retrSE3(const float* xi, const float* t, const f
 // ---------------------------------------------------------------------------
 constexpr int BA_LDS_NMAX = 12;  // optimised poses whose B fits in LDS (72x72 fp32)
 constexpr int BA_SOLVE_NMAX = 64;  // up to 384 x 384 (fp64 Cholesky in global scratch beyond BA_LDS_NMAX)
-constexpr int HDR_MU = 0, HDR_STATUS = 1, HDR_WORDS = 16;
+constexpr int HDR_MU = 0, HDR_STATUS = 1, HDR_BW = 2, HDR_WORDS = 16;
+constexpr int BS_TILE = 64;            // tile edge of the banded reduced camera system
+constexpr int BS_NMAX = 32767;         // pose keys are packed as 16-bit pairs in the Schur reduction
 
 struct BaLayout {
     size_t hdr, bits, wordbase, kx, B, v, C, u, E, S, y, dX, Sd, yd, total;
@@ -205,6 +207,15 @@ struct BaParams {
     double* Sd;
     double* yd;
     int red_iters;   // wave reductions of the pose-block terms per wave (0 = per-lane atomics only)
+    // sparse (band) path only -- see "large pose windows" below
+    float* ent;      // [E][16] per-edge Schur entries: E_i row (6), E_j row (6), C, u
+    const int* kptr; // [Mu + 1] CSR of the edges of each unique patch (into eord)
+    const int* eord; // [E] edge ids sorted by unique-patch rank
+    float* Qk;       // [Mu] 1 / (C + lmbda)
+    float* uk;       // [Mu]
+    double* St;      // band tiles of the reduced camera system, lower triangle (fp64)
+    double* ys;      // [T * 64] right-hand side, then the solution dX (fp64)
+    int T, bt;       // 64-wide tiles per side, tile bandwidth
 };
 
 __device__ __forceinline__ bool failed(const BaParams& p) { return *(volatile int*)p.status != 0; }
@@ -283,6 +294,17 @@ __device__ __forceinline__ int unique_rank(const BaParams& p, int64_t k)
     return p.wordbase[k >> 5] + __popc(w & ((1u << (k & 31)) - 1u));
 }
 
+// element (A, B), A >= B, of the banded lower-triangle tile storage: tile
+// (r, c), 0 <= r - c <= bt, lives at index c * (bt + 1) + (r - c), row-major 64 x 64
+__device__ __forceinline__ double* bs_tile(const BaParams& p, int r, int c)
+{
+    return p.St + (((int64_t)c * (p.bt + 1) + (r - c)) << 12);
+}
+__device__ __forceinline__ double* bs_elem(const BaParams& p, int A, int B)
+{
+    return bs_tile(p, A >> 6, B >> 6) + ((A & 63) << 6) + (B & 63);
+}
+
 __global__ __launch_bounds__(256) void ba_zero_kernel(BaParams p)
 {
     const int Mu = p.hdr[HDR_MU];
@@ -303,7 +325,9 @@ __global__ __launch_bounds__(256) void ba_zero_kernel(BaParams p)
 // ---------------------------------------------------------------------------
 // residuals + normal equations (ba_cuda.cu:214-365)
 // ---------------------------------------------------------------------------
-template <bool LDS_B>
+// SPARSE: the large-window path -- B goes straight into the band tiles of S,
+// v into y, and the patch terms are stored per edge (no dense E).
+template <bool LDS_B, bool SPARSE>
 __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
 {
     extern __shared__ __attribute__((aligned(16))) float sB[];  // [n6*n6] B upper triangle + [n6] v
@@ -311,6 +335,16 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
     if (failed(p)) return;
     float* Bacc = LDS_B ? sB : p.B;
     float* vacc = LDS_B ? sB + n6 * n6 : p.v;
+    // pose-block element (r, c), r <= c: upper triangle of the dense B, or
+    // its mirror in the lower-triangle fp64 band tiles; v -> the fp64 y there
+    auto bptr = [&](int r, int c) {
+        if constexpr (SPARSE) return bs_elem(p, c, r);
+        else return &Bacc[r * n6 + c];
+    };
+    auto vptr = [&](int r) {
+        if constexpr (SPARSE) return p.ys + r;
+        else return vacc + r;
+    };
     if (LDS_B) {
         for (int i = threadIdx.x; i < n6 * n6 + n6; i += blockDim.x) sB[i] = 0.f;
         __syncthreads();
@@ -370,7 +404,29 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
         adjSE3(tij, qij, Jj[1], Ji[1]);
 
         // patch terms: E rows (device atomics; a wave's lanes mostly hold different patches), C, u
-        if (valid) {
+        if constexpr (SPARSE) {
+            if (n < p.E) {
+                float Ei[6], Ej[6], Ck = 0.f, uk = 0.f;
+#pragma unroll
+                for (int t = 0; t < 6; t++) { Ei[t] = 0.f; Ej[t] = 0.f; }
+#pragma unroll
+                for (int row = 0; row < 2; row++) {
+#pragma unroll
+                    for (int t = 0; t < 6; t++) {
+                        Ei[t] += -w[row] * Jz[row] * Ji[row][t];
+                        Ej[t] += w[row] * Jz[row] * Jj[row][t];
+                    }
+                    Ck += w[row] * Jz[row] * Jz[row];
+                    uk += w[row] * r[row] * Jz[row];
+                }
+                const float z = 0.f;
+                float4* o = reinterpret_cast<float4*>(p.ent + n * 16);
+                o[0] = make_float4(iv ? Ei[0] : z, iv ? Ei[1] : z, iv ? Ei[2] : z, iv ? Ei[3] : z);
+                o[1] = make_float4(iv ? Ei[4] : z, iv ? Ei[5] : z, jv ? Ej[0] : z, jv ? Ej[1] : z);
+                o[2] = make_float4(jv ? Ej[2] : z, jv ? Ej[3] : z, jv ? Ej[4] : z, jv ? Ej[5] : z);
+                o[3] = make_float4(valid ? Ck : z, valid ? uk : z, z, z);
+            }
+        } else if (valid) {
             float Ei[6], Ej[6], Ck = 0.f, uk = 0.f;
 #pragma unroll
             for (int t = 0; t < 6; t++) { Ei[t] = 0.f; Ej[t] = 0.f; }
@@ -440,11 +496,14 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
                 bij[a * 6 + b] = s;
             }
         const bool has = iv || jv;
-        const int key = has ? ((ix & 0x3ff) << 12 | (jx & 0x3ff) << 2 | (iv ? 2 : 0) | (jv ? 1 : 0)) : -1;
+        // (ix, jx) < 2^15 (BS_NMAX); an index outside the window is not used, so it keys as 0x7fff
+        const uint32_t key = has ? ((uint32_t)(iv ? ix : 0x7fff) << 17 | (uint32_t)(jv ? jx : 0x7fff) << 2 |
+                                    (iv ? 2u : 0u) | (jv ? 1u : 0u))
+                                 : 0xffffffffu;
         uint64_t pending = __ballot(has);
         for (int iter = 0; pending && iter < p.red_iters; iter++) {
             const int leader = __ffsll((unsigned long long)pending) - 1;
-            const int lkey = __shfl(key, leader);
+            const uint32_t lkey = __shfl(key, leader);
             const bool mine = key == lkey;
             const int lix = __shfl(ix, leader), ljx = __shfl(jx, leader);
             const bool liv = (lkey & 2) != 0, ljv = (lkey & 1) != 0;
@@ -455,7 +514,7 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
 #pragma unroll
                 for (int t = 0; t < 6; t++) {
                     const float s = red(vi[t]);
-                    if (lane == leader) atomicAdd(&vacc[6 * lix + t], s);
+                    if (lane == leader) atomicAdd(vptr(6 * lix + t), s);
                 }
                 int u = 0;
 #pragma unroll
@@ -463,14 +522,14 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
 #pragma unroll
                     for (int b = a; b < 6; b++, u++) {
                         const float s = red(bii[u]);
-                        if (lane == leader) atomicAdd(&Bacc[(6 * lix + a) * n6 + 6 * lix + b], s);
+                        if (lane == leader) atomicAdd(bptr(6 * lix + a, 6 * lix + b), s);
                     }
             }
             if (ljv) {
 #pragma unroll
                 for (int t = 0; t < 6; t++) {
                     const float s = red(vj[t]);
-                    if (lane == leader) atomicAdd(&vacc[6 * ljx + t], s);
+                    if (lane == leader) atomicAdd(vptr(6 * ljx + t), s);
                 }
             }
             if (ljv && !lself) {
@@ -480,7 +539,7 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
 #pragma unroll
                     for (int b = a; b < 6; b++, u++) {
                         const float s = red(bjj[u]);
-                        if (lane == leader) atomicAdd(&Bacc[(6 * ljx + a) * n6 + 6 * ljx + b], s);
+                        if (lane == leader) atomicAdd(bptr(6 * ljx + a, 6 * ljx + b), s);
                     }
             }
             if (liv && ljv && !lself) {
@@ -490,7 +549,7 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
 #pragma unroll
                     for (int b = 0; b < 6; b++) {
                         const float s = red(bij[a * 6 + b]);
-                        if (lane == leader) atomicAdd(&Bacc[(6 * r0 + a) * n6 + 6 * c0 + b], s);
+                        if (lane == leader) atomicAdd(bptr(6 * r0 + a, 6 * c0 + b), s);
                     }
             }
             pending &= ~__ballot(mine);
@@ -500,30 +559,30 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
         if ((pending >> lane) & 1) {
             if (iv) {
 #pragma unroll
-                for (int t = 0; t < 6; t++) atomicAdd(&vacc[6 * ix + t], vi[t]);
+                for (int t = 0; t < 6; t++) atomicAdd(vptr(6 * ix + t), vi[t]);
                 int u = 0;
 #pragma unroll
                 for (int a = 0; a < 6; a++)
 #pragma unroll
-                    for (int b = a; b < 6; b++, u++) atomicAdd(&Bacc[(6 * ix + a) * n6 + 6 * ix + b], bii[u]);
+                    for (int b = a; b < 6; b++, u++) atomicAdd(bptr(6 * ix + a, 6 * ix + b), bii[u]);
             }
             if (jv) {
 #pragma unroll
-                for (int t = 0; t < 6; t++) atomicAdd(&vacc[6 * jx + t], vj[t]);
+                for (int t = 0; t < 6; t++) atomicAdd(vptr(6 * jx + t), vj[t]);
             }
             if (jv && !self) {
                 int u = 0;
 #pragma unroll
                 for (int a = 0; a < 6; a++)
 #pragma unroll
-                    for (int b = a; b < 6; b++, u++) atomicAdd(&Bacc[(6 * jx + a) * n6 + 6 * jx + b], bjj[u]);
+                    for (int b = a; b < 6; b++, u++) atomicAdd(bptr(6 * jx + a, 6 * jx + b), bjj[u]);
             }
             if (iv && jv && !self) {
                 const int r0 = up ? ix : jx, c0 = up ? jx : ix;
 #pragma unroll
                 for (int a = 0; a < 6; a++)
 #pragma unroll
-                    for (int b = 0; b < 6; b++) atomicAdd(&Bacc[(6 * r0 + a) * n6 + 6 * c0 + b], bij[a * 6 + b]);
+                    for (int b = 0; b < 6; b++) atomicAdd(bptr(6 * r0 + a, 6 * c0 + b), bij[a * 6 + b]);
             }
         }
     }
@@ -803,6 +862,537 @@ __global__ __launch_bounds__(256) void ba_patch_kernel(BaParams p, int structure
 }
 
 // ---------------------------------------------------------------------------
+// Large pose windows: global BA (dpvo.py:436-505 calls fastba.BA with t0 = 1,
+// t1 = n, i.e. thousands of poses).  The reference's dense E (6N x Mu: 77 GB
+// at 4096 keyframes, past its int32 accessors) and dense E Q E^T GEMM are
+// replaced by the same algebra on the graph's structure:
+//   * per-edge Schur entries (E_i row, E_j row, C and u terms) instead of E,
+//     with the edges of each unique patch found through a radix-sorted CSR;
+//   * S = B - sum_k Q_k E_k E_k^T accumulated directly into 64 x 64 tiles of
+//     its lower band -- the bandwidth is the widest pose span of one patch's
+//     edges (19 poses for the reference's fixed global edge pattern) --
+//     with keyed per-wave reductions ahead of the atomics;
+//   * a tiled band Cholesky (one launch each of potrf / trsm / syrk per tile
+//     column) and one-workgroup band triangular solves.
+// fp32 throughout, like the reference's float S and cholesky (ba_cuda.cu:
+// 510-523); only the summation order differs from the dense path.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void bs_keys_kernel(BaParams p, uint32_t* keys, int* vals)
+{
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < p.E; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = p.kk[e];
+        keys[e] = (k >= 0 && k < p.num_patches) ? (uint32_t)unique_rank(p, k) : 0u;
+        vals[e] = (int)e;
+    }
+}
+
+// kptr[rank] = first sorted position of the rank (every rank has an edge)
+__global__ __launch_bounds__(256) void bs_ptr_kernel(const uint32_t* keys, int64_t E, int* kptr)
+{
+    for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s < E; s += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t key = keys[s];
+        if (s == 0 || keys[s - 1] != key) kptr[key] = (int)s;
+        if (s == E - 1) kptr[key + 1] = (int)E;
+    }
+}
+
+// bandwidth of S in poses: the widest span of optimised poses one patch's edges touch
+__global__ __launch_bounds__(256) void bs_span_kernel(BaParams p)
+{
+    const int Mu = p.hdr[HDR_MU];
+    int best = 0;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < Mu; k += (int64_t)gridDim.x * blockDim.x) {
+        int lo = 0x7fffffff, hi = -1;
+        for (int q = p.kptr[k]; q < p.kptr[k + 1]; q++) {
+            const int e = p.eord[q];
+            const int64_t a = p.ii[e] - p.t0, b = p.jj[e] - p.t0;
+            if (a >= 0 && a < p.N) { lo = min(lo, (int)a); hi = max(hi, (int)a); }
+            if (b >= 0 && b < p.N) { lo = min(lo, (int)b); hi = max(hi, (int)b); }
+        }
+        if (hi > lo) best = max(best, hi - lo);
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) best = max(best, __shfl_xor(best, o));
+    if ((threadIdx.x & 63) == 0 && best > 0) atomicMax(&p.hdr[HDR_BW], best);
+}
+
+__global__ __launch_bounds__(256) void bs_zero_kernel(BaParams p)
+{
+    const int64_t nS = (int64_t)p.T * (p.bt + 1) * (BS_TILE * BS_TILE / 2), ny = (int64_t)p.T * (BS_TILE / 2);
+    const double2 z = make_double2(0.0, 0.0);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nS + ny; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i < nS) reinterpret_cast<double2*>(p.St)[i] = z;
+        else reinterpret_cast<double2*>(p.ys)[i - nS] = z;
+    }
+}
+
+// Per unique patch k (one lane each; consecutive patches share their pose
+// structure, so a wave's lanes mostly hold the same pose pairs):
+//   Q_k = 1 / (C_k + lmbda);  y -= Q_k u_k E_k;  S -= Q_k E_k E_k^T.
+// E_k's entries are the host row summed over the patch's edges (when they
+// share ii, as DPVO's do) plus one E_j row per edge; the pair products are
+// accumulated without merging equal poses (the sum is the same).
+__global__ __launch_bounds__(256) void bs_schur_kernel(BaParams p)
+{
+    if (failed(p)) return;
+    const int Mu = p.hdr[HDR_MU];
+    const float lm = p.lmbda[0];
+    const int lane = threadIdx.x & 63;
+    for (int64_t k0 = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) & ~int64_t(63); k0 < Mu;
+         k0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = k0 + lane;
+        const bool live = k < Mu;
+        const int s0 = live ? p.kptr[k] : 0, s1 = live ? p.kptr[k + 1] : 0;
+        const int64_t hpose = live ? p.ii[p.eord[s0]] : 0;
+        float C = 0.f, u = 0.f, H[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        bool uniform = true;
+        for (int q = s0; q < s1; q++) {
+            const int e = p.eord[q];
+            const float4* en = reinterpret_cast<const float4*>(p.ent + (int64_t)e * 16);
+            const float4 a = en[0], b = en[1], d = en[3];
+            H[0] += a.x; H[1] += a.y; H[2] += a.z; H[3] += a.w; H[4] += b.x; H[5] += b.y;
+            C += d.x;
+            u += d.y;
+            uniform = uniform && p.ii[e] == hpose;
+        }
+        const float Q = 1.0f / (C + lm);
+        if (live) {
+            p.Qk[k] = Q;
+            p.uk[k] = u;
+        }
+        const int deg = s1 - s0;
+        const int nent = live ? (uniform ? 1 + deg : 2 * deg) : 0;
+        // entry t -> (window pose or -1, row)
+        auto entry = [&](int t, float* v) -> int {
+            int64_t pose;
+            if (uniform && t == 0) {
+#pragma unroll
+                for (int x = 0; x < 6; x++) v[x] = H[x];
+                pose = hpose;
+            } else {
+                const int q = uniform ? t - 1 : (t >> 1);
+                const bool jside = uniform || (t & 1);
+                const int e = p.eord[s0 + q];
+                const float* src = p.ent + (int64_t)e * 16 + (jside ? 6 : 0);
+#pragma unroll
+                for (int x = 0; x < 6; x++) v[x] = src[x];
+                pose = jside ? p.jj[e] : p.ii[e];
+            }
+            pose -= p.t0;
+            return (pose >= 0 && pose < p.N) ? (int)pose : -1;
+        };
+        int maxn = nent, maxp = nent * (nent + 1) / 2;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            maxn = max(maxn, __shfl_xor(maxn, o));
+            maxp = max(maxp, __shfl_xor(maxp, o));
+        }
+        // y -= Q u E_k, one entry per lane per round
+        const float qu = Q * u;
+        for (int t = 0; t < maxn; t++) {
+            float ev[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            const int pose = t < nent ? entry(t, ev) : -1;
+            uint64_t pending = __ballot(pose >= 0);
+            while (pending) {
+                const int leader = __ffsll((unsigned long long)pending) - 1;
+                const int lpose = __shfl(pose, leader);
+                const bool mine = pose == lpose;
+#pragma unroll
+                for (int x = 0; x < 6; x++) {
+                    const float s = wave64_sum(mine ? qu * ev[x] : 0.f);
+                    if (lane == leader) atomicAdd(&p.ys[6 * lpose + x], -(double)s);
+                }
+                pending &= ~__ballot(mine);
+            }
+        }
+        // S -= Q E_k E_k^T over entry pairs ta <= tb, one pair per lane per round
+        int ta = 0, tb = 0;
+        for (int it = 0; it < maxp; it++) {
+            float ea[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, eb[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            int pa = -1, pb = -1;
+            if (ta < nent) {
+                pa = entry(ta, ea);
+                pb = entry(tb, eb);
+            }
+            uint32_t key = 0xffffffffu;
+            if (pa >= 0 && pb >= 0) {
+                if (pa < pb) {
+                    const int t = pa; pa = pb; pb = t;
+#pragma unroll
+                    for (int x = 0; x < 6; x++) { const float v = ea[x]; ea[x] = eb[x]; eb[x] = v; }
+                }
+                key = (uint32_t)pa << 16 | (uint32_t)pb;
+            }
+            const bool same = ta == tb;
+            uint64_t pending = __ballot(key != 0xffffffffu);
+            while (pending) {
+                const int leader = __ffsll((unsigned long long)pending) - 1;
+                const uint32_t lkey = __shfl(key, leader);
+                const bool mine = key == lkey;
+                const int hi = (int)(lkey >> 16), lo = (int)(lkey & 0xffff);
+                if (hi != lo) {
+#pragma unroll
+                    for (int x = 0; x < 6; x++)
+#pragma unroll
+                        for (int z = 0; z < 6; z++) {
+                            const float s = wave64_sum(mine ? -Q * ea[x] * eb[z] : 0.f);
+                            if (lane == leader) atomicAdd(bs_elem(p, 6 * hi + x, 6 * lo + z), (double)s);
+                        }
+                } else {
+#pragma unroll
+                    for (int x = 0; x < 6; x++)
+#pragma unroll
+                        for (int z = 0; z <= x; z++) {
+                            const float v = same ? ea[x] * ea[z] : ea[x] * eb[z] + eb[x] * ea[z];
+                            const float s = wave64_sum(mine ? -Q * v : 0.f);
+                            if (lane == leader) atomicAdd(bs_elem(p, 6 * hi + x, 6 * hi + z), (double)s);
+                        }
+                }
+                pending &= ~__ballot(mine);
+            }
+            if (ta < nent && ++tb == nent) {
+                ta++;
+                tb = ta;
+            }
+        }
+    }
+}
+
+// S += diag(1e-4 S + 1) (ba_cuda.cu:517-518); identity on the padding past 6N
+__global__ __launch_bounds__(256) void bs_damp_kernel(BaParams p)
+{
+    if (failed(p)) return;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < p.T * BS_TILE; i += gridDim.x * blockDim.x) {
+        double* d = bs_elem(p, i, i);
+        *d = i < p.n6 ? *d + (1e-4 * *d + 1.0) : 1.0;
+    }
+}
+
+// Cholesky of diagonal tile c, one wave: lane r holds row r, column j of L is
+// broadcast through LDS (as ba_solve_wave_kernel).  Upper entries written 0.
+__global__ __launch_bounds__(64) void bs_potrf_kernel(BaParams p, int c)
+{
+    __shared__ double col[64];
+    if (failed(p)) return;
+    const int r = threadIdx.x;
+    double* A = bs_tile(p, c, c) + r * 64;
+    double a[64];
+#pragma unroll
+    for (int j = 0; j < 64; j += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(A + j);
+        a[j] = v.x; a[j + 1] = v.y;
+    }
+    int fail = 0;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        col[r] = a[j];
+        wave_lds_fence();
+        const double djj = col[j];
+        if (!(djj > 0.0)) {
+            fail = j + 1;
+            break;
+        }
+        const double ljj = sqrt(djj);
+        const double l = r > j ? a[j] / ljj : (r == j ? ljj : 0.0);
+        a[j] = l;
+        wave_lds_fence();
+        col[r] = l;
+        wave_lds_fence();
+#pragma unroll
+        for (int cc = j + 1; cc < 64; cc++) a[cc] -= l * col[cc];
+        wave_lds_fence();
+    }
+    if (fail) {
+        if (r == 0) atomicExch(p.status, c * BS_TILE + fail);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 64; j += 2)
+        *reinterpret_cast<double2*>(A + j) = make_double2(j <= r ? a[j] : 0.0, j + 1 <= r ? a[j + 1] : 0.0);
+}
+
+// panel: A_rc <- A_rc L_cc^{-T} for r = c + 1 + blockIdx.x; lane i solves row i
+__global__ __launch_bounds__(64) void bs_trsm_kernel(BaParams p, int c)
+{
+    __shared__ double Ls[64 * 65];
+    if (failed(p)) return;
+    const int r = c + 1 + blockIdx.x, i = threadIdx.x;
+    const double* L = bs_tile(p, c, c);
+    for (int q = i; q < 4096; q += 64) Ls[(q >> 6) * 65 + (q & 63)] = L[q];
+    double* A = bs_tile(p, r, c) + i * 64;
+    double x[64];
+#pragma unroll
+    for (int j = 0; j < 64; j += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(A + j);
+        x[j] = v.x; x[j + 1] = v.y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        x[j] = x[j] / Ls[j * 65 + j];
+#pragma unroll
+        for (int t = j + 1; t < 64; t++) x[t] -= x[j] * Ls[t * 65 + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 64; j += 2) *reinterpret_cast<double2*>(A + j) = make_double2(x[j], x[j + 1]);
+}
+
+// trailing update inside the band: A_rq -= A_rc A_qc^T for c < q <= r <= c + nb
+__global__ __launch_bounds__(256) void bs_syrk_kernel(BaParams p, int c)
+{
+    __shared__ double Xs[64 * 65], Ys[64 * 65];
+    if (failed(p)) return;
+    const int idx = blockIdx.x;
+    int i = (int)((sqrtf(8.f * (float)idx + 1.f) - 1.f) * 0.5f);
+    while ((i + 1) * (i + 2) / 2 <= idx) i++;
+    while (i * (i + 1) / 2 > idx) i--;
+    const int k = idx - i * (i + 1) / 2;
+    const int r = c + 1 + i, q = c + 1 + k;
+    const double* X = bs_tile(p, r, c);
+    const double* Y = bs_tile(p, q, c);
+    for (int t = threadIdx.x; t < 4096; t += 256) {
+        Xs[(t >> 6) * 65 + (t & 63)] = X[t];
+        Ys[(t >> 6) * 65 + (t & 63)] = Y[t];
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    double acc[4][4] = {};
+#pragma unroll 4
+    for (int t = 0; t < 64; t++) {
+        double xa[4], yb[4];
+#pragma unroll
+        for (int a = 0; a < 4; a++) xa[a] = Xs[(ty * 4 + a) * 65 + t];
+#pragma unroll
+        for (int b = 0; b < 4; b++) yb[b] = Ys[(tx * 4 + b) * 65 + t];
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) acc[a][b] += xa[a] * yb[b];
+    }
+    double* O = bs_tile(p, r, q);
+#pragma unroll
+    for (int a = 0; a < 4; a++) {
+        double2* o = reinterpret_cast<double2*>(O + (ty * 4 + a) * 64 + tx * 4);
+        double2 v0 = o[0], v1 = o[1];
+        v0.x -= acc[a][0]; v0.y -= acc[a][1]; v1.x -= acc[a][2]; v1.y -= acc[a][3];
+        o[0] = v0;
+        o[1] = v1;
+    }
+}
+
+// L L^T x = y in place on ys, band-aware forward / backward substitution (one workgroup)
+__global__ __launch_bounds__(256) void bs_trsv_kernel(BaParams p)
+{
+    __shared__ double Ls[64 * 65];
+    __shared__ double zs[64];
+    __shared__ double part[256];
+    if (failed(p)) return;
+    const int tid = threadIdx.x, T = p.T, bt = p.bt;
+    double* y = p.ys;
+    for (int c = 0; c < T; c++) {
+        const double* Lcc = bs_tile(p, c, c);
+        for (int q = tid; q < 4096; q += 256) Ls[(q >> 6) * 65 + (q & 63)] = Lcc[q];
+        __syncthreads();
+        if (tid < 64) {
+            double yi = y[c * 64 + tid];
+            for (int j = 0; j < 64; j++) {
+                const double zj = __shfl(yi / Ls[j * 65 + j], j);
+                if (tid == j) yi = zj;
+                else if (tid > j) yi -= Ls[tid * 65 + j] * zj;
+            }
+            zs[tid] = yi;
+            y[c * 64 + tid] = yi;
+        }
+        __syncthreads();
+        const int rows = (min(T - 1, c + bt) - c) * 64;
+        for (int q = tid; q < rows; q += 256) {
+            const int r = c + 1 + (q >> 6), a = q & 63;
+            const double* Lrc = bs_tile(p, r, c) + a * 64;
+            double s = 0.0;
+            for (int t = 0; t < 64; t++) s += Lrc[t] * zs[t];
+            y[r * 64 + a] -= s;
+        }
+        __syncthreads();
+    }
+    for (int c = T - 1; c >= 0; c--) {
+        const int rows = (min(T - 1, c + bt) - c) * 64;
+        const int t = tid & 63;
+        double s = 0.0;
+        for (int q = tid >> 6; q < rows; q += 4) {
+            const int r = c + 1 + (q >> 6), a = q & 63;
+            s += bs_tile(p, r, c)[a * 64 + t] * y[r * 64 + a];
+        }
+        part[tid] = s;
+        const double* Lcc = bs_tile(p, c, c);
+        for (int q = tid; q < 4096; q += 256) Ls[(q >> 6) * 65 + (q & 63)] = Lcc[q];
+        __syncthreads();
+        if (tid < 64) {
+            double xi = y[c * 64 + tid] - (part[tid] + part[tid + 64] + part[tid + 128] + part[tid + 192]);
+            for (int j = 63; j >= 0; j--) {
+                const double xj = __shfl(xi / Ls[j * 65 + j], j);
+                if (tid == j) xi = xj;
+                else if (tid < j) xi -= Ls[j * 65 + tid] * xj;
+            }
+            y[c * 64 + tid] = xi;
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void bs_retract_kernel(BaParams p)
+{
+    if (failed(p)) return;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < p.N; i += gridDim.x * blockDim.x) {
+        float* P = p.poses + (int64_t)(p.t0 + i) * 7;
+        const float t0v[3] = {P[0], P[1], P[2]}, q0v[4] = {P[3], P[4], P[5], P[6]};
+        float xi[6], t1v[3], q1v[4];
+        for (int k = 0; k < 6; k++) xi[k] = (float)p.ys[6 * i + k];
+        retrSE3(xi, t0v, q0v, t1v, q1v);
+        P[0] = t1v[0]; P[1] = t1v[1]; P[2] = t1v[2];
+        P[3] = q1v[0]; P[4] = q1v[1]; P[5] = q1v[2]; P[6] = q1v[3];
+    }
+}
+
+// dZ_k = Q_k (u_k - E_k^T dX) over the patch's edge entries; depth retraction (ba_cuda.cu:191-211)
+__global__ __launch_bounds__(256) void bs_patch_kernel(BaParams p)
+{
+    if (failed(p)) return;
+    const int Mu = p.hdr[HDR_MU];
+    const int64_t PP = (int64_t)p.P * p.P;
+    for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < Mu; k += (int64_t)gridDim.x * blockDim.x) {
+        // the reference rounds dX to float before E^T dX (ba_cuda.cu:523)
+        float s = 0.f;
+        for (int q = p.kptr[k]; q < p.kptr[k + 1]; q++) {
+            const int e = p.eord[q];
+            const float* en = p.ent + (int64_t)e * 16;
+            const int64_t a = p.ii[e] - p.t0, b = p.jj[e] - p.t0;
+            if (a >= 0 && a < p.N)
+                for (int t = 0; t < 6; t++) s += en[t] * (float)p.ys[6 * a + t];
+            if (b >= 0 && b < p.N)
+                for (int t = 0; t < 6; t++) s += en[6 + t] * (float)p.ys[6 * b + t];
+        }
+        const float dZ = p.Qk[k] * (p.uk[k] - s);
+        float* pd = p.patches + ((int64_t)p.kx[k] * 3 + 2) * PP;
+        float d = pd[0] + dZ;
+        d = (d > 20.f) ? 1.0f : d;
+        d = fmaxf(d, 1e-4f);
+        for (int64_t q = 0; q < PP; q++) pd[q] = d;
+    }
+}
+
+struct BsLayout {
+    size_t hdr, bits, wordbase, kx, kin, kout, vin, vout, tmp, tmp_bytes, kptr, ent, Qk, uk, y, St, total;
+    int64_t nwords, mu_max;
+    int n6, T;
+};
+
+static size_t bs_sort_temp_bytes(int64_t E)
+{
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (int*)nullptr,
+                                             (int*)nullptr, (int)E);
+    return bytes;
+}
+
+static BsLayout bs_layout(int64_t E, int64_t num_patches, int N)
+{
+    BsLayout L{};
+    L.nwords = (num_patches + 31) / 32;
+    L.mu_max = std::max<int64_t>(1, std::min(E, num_patches));
+    L.n6 = 6 * N;
+    L.T = std::max(1, (L.n6 + BS_TILE - 1) / BS_TILE);
+    const size_t e = (size_t)std::max<int64_t>(E, 1);
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += align256(bytes); return o; };
+    L.hdr = take(HDR_WORDS * 4);
+    L.bits = take((size_t)L.nwords * 4);
+    L.wordbase = take((size_t)L.nwords * 4);
+    L.kx = take((size_t)L.mu_max * 4);
+    L.kin = take(e * 4);
+    L.kout = take(e * 4);
+    L.vin = take(e * 4);
+    L.vout = take(e * 4);
+    L.tmp_bytes = bs_sort_temp_bytes((int64_t)e);
+    L.tmp = take(L.tmp_bytes);
+    L.kptr = take((size_t)(L.mu_max + 1) * 4);
+    L.ent = take(e * 64);
+    L.Qk = take((size_t)L.mu_max * 4);
+    L.uk = take((size_t)L.mu_max * 4);
+    L.y = take((size_t)L.T * BS_TILE * 8);
+    L.St = take((size_t)L.T * L.T * BS_TILE * BS_TILE * 8);   // the band can be the whole matrix
+    L.total = off;
+    return L;
+}
+
+// one call of the sparse path; p carries the operands, status and sizes
+static int ba_forward_sparse(BaParams p, char* ws, const BsLayout& L, int iterations, hipStream_t s)
+{
+    p.hdr = (int*)(ws + L.hdr);
+    if (!p.status) p.status = p.hdr + HDR_STATUS;
+    p.bits = (uint32_t*)(ws + L.bits);
+    p.wordbase = (int*)(ws + L.wordbase);
+    p.kx = (int*)(ws + L.kx);
+    int* kptr = (int*)(ws + L.kptr);
+    p.kptr = kptr;
+    p.eord = (const int*)(ws + L.vout);
+    p.ent = (float*)(ws + L.ent);
+    p.Qk = (float*)(ws + L.Qk);
+    p.uk = (float*)(ws + L.uk);
+    p.ys = (double*)(ws + L.y);
+    p.St = (double*)(ws + L.St);
+    p.T = L.T;
+    p.red_iters = 2;
+    DPVO_CHECK_HIP(hipMemsetAsync(ws + L.hdr, 0, L.wordbase - L.hdr, s));  // header + bitmap
+    DPVO_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int), s));
+    const unsigned gE = grid_for(p.E, 256, 2048);
+    const unsigned gM = grid_for(L.mu_max, 256, 2048);
+    hipLaunchKernelGGL(ba_mark_kernel, dim3(gE), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(ba_scan_kernel, dim3(1), dim3(1024), 0, s, p, L.nwords);
+    hipLaunchKernelGGL(bs_keys_kernel, dim3(gE), dim3(256), 0, s, p, (uint32_t*)(ws + L.kin), (int*)(ws + L.vin));
+    DPVO_CHECK_LAUNCH();
+    int bits = 1;
+    while (bits < 32 && (int64_t(1) << bits) < L.mu_max) bits++;
+    size_t tmp_bytes = L.tmp_bytes;
+    DPVO_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(ws + L.tmp, tmp_bytes, (uint32_t*)(ws + L.kin),
+                                                      (uint32_t*)(ws + L.kout), (int*)(ws + L.vin),
+                                                      (int*)(ws + L.vout), (int)p.E, 0, bits, s));
+    hipLaunchKernelGGL(bs_ptr_kernel, dim3(gE), dim3(256), 0, s, (const uint32_t*)(ws + L.kout), p.E, kptr);
+    hipLaunchKernelGGL(bs_span_kernel, dim3(gM), dim3(256), 0, s, p);
+    DPVO_CHECK_LAUNCH();
+    // the band decides the factorisation's launch shapes: one host read per call
+    int hdr[HDR_WORDS], st = 0;
+    DPVO_CHECK_HIP(hipMemcpyAsync(hdr, p.hdr, sizeof hdr, hipMemcpyDeviceToHost, s));
+    DPVO_CHECK_HIP(hipMemcpyAsync(&st, p.status, sizeof st, hipMemcpyDeviceToHost, s));
+    DPVO_CHECK_HIP(hipStreamSynchronize(s));
+    if (st != 0) return 0;   // bad patch index: reported through status, state untouched
+    const int bw = hdr[HDR_BW];
+    p.bt = std::min(L.T - 1, (6 * bw + 5 + BS_TILE - 1) / BS_TILE);
+    const unsigned gH = grid_for(p.E, 256, 1024);
+    const unsigned gZ = grid_for((int64_t)L.T * (p.bt + 1) * (BS_TILE * BS_TILE / 2), 256, 8192);
+    for (int it = 0; it < iterations; it++) {
+        hipLaunchKernelGGL(bs_zero_kernel, dim3(gZ), dim3(256), 0, s, p);
+        hipLaunchKernelGGL((ba_hessian_kernel<false, true>), dim3(gH), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(bs_schur_kernel, dim3(gM), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(bs_damp_kernel, dim3(grid_for((int64_t)L.T * BS_TILE, 256, 1024)), dim3(256), 0, s, p);
+        DPVO_CHECK_LAUNCH();
+        for (int c = 0; c < L.T; c++) {
+            hipLaunchKernelGGL(bs_potrf_kernel, dim3(1), dim3(64), 0, s, p, c);
+            const int nb = std::min(p.bt, L.T - 1 - c);
+            if (nb > 0) {
+                hipLaunchKernelGGL(bs_trsm_kernel, dim3(nb), dim3(64), 0, s, p, c);
+                hipLaunchKernelGGL(bs_syrk_kernel, dim3(nb * (nb + 1) / 2), dim3(256), 0, s, p, c);
+            }
+        }
+        DPVO_CHECK_LAUNCH();
+        hipLaunchKernelGGL(bs_trsv_kernel, dim3(1), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(bs_retract_kernel, dim3(grid_for(p.N, 256)), dim3(256), 0, s, p);
+        hipLaunchKernelGGL(bs_patch_kernel, dim3(gM), dim3(256), 0, s, p);
+        DPVO_CHECK_LAUNCH();
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
 // fastba.reproject (ba_cuda.cu:368-418)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void reproject_kernel(const float* poses, const float* patches, int P,
@@ -870,28 +1460,49 @@ static size_t nb_sort_temp_bytes(int64_t E)
 
 using namespace dpvo;
 
-extern "C" size_t dpvo_ba_workspace_bytes(int64_t num_edges, int64_t num_patches, int num_opt_poses)
+static bool ba_sparse(int N, int flags) { return N > 0 && ((flags & DPVO_BA_SPARSE) || N > BA_SOLVE_NMAX); }
+
+extern "C" size_t dpvo_ba_workspace_bytes_ex(int64_t num_edges, int64_t num_patches, int num_opt_poses, int flags)
 {
-    return ba_layout(num_edges, num_patches, num_opt_poses < 0 ? 0 : num_opt_poses).total;
+    const int N = num_opt_poses < 0 ? 0 : num_opt_poses;
+    if (ba_sparse(N, flags)) return bs_layout(num_edges, num_patches, N).total;
+    return ba_layout(num_edges, num_patches, N).total;
 }
 
-extern "C" int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
-                               const float* target, const float* weight, const float* lmbda, const int64_t* ii,
-                               const int64_t* jj, const int64_t* kk, int64_t num_edges, int t0, int t1,
-                               int iterations, void* workspace, size_t workspace_bytes, int* status, void* stream)
+extern "C" size_t dpvo_ba_workspace_bytes(int64_t num_edges, int64_t num_patches, int num_opt_poses)
+{
+    return dpvo_ba_workspace_bytes_ex(num_edges, num_patches, num_opt_poses, 0);
+}
+
+extern "C" int dpvo_ba_forward_ex(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
+                                  const float* target, const float* weight, const float* lmbda, const int64_t* ii,
+                                  const int64_t* jj, const int64_t* kk, int64_t num_edges, int t0, int t1,
+                                  int iterations, int flags, void* workspace, size_t workspace_bytes, int* status,
+                                  void* stream)
 {
     const int N = t1 - t0;
     DPVO_CHECK_ARG(N >= 0, "t1 must be >= t0");
-    DPVO_CHECK_ARG(N <= BA_SOLVE_NMAX, "more than 64 optimised poses is not supported by the dense solver");
+    DPVO_CHECK_ARG(N <= BS_NMAX, "more than 32767 optimised poses");
     DPVO_CHECK_ARG(P >= 1 && num_patches >= 0 && iterations >= 0, "bad sizes");
-    const BaLayout L = ba_layout(num_edges, num_patches, N);
-    DPVO_CHECK_ARG(workspace && workspace_bytes >= L.total, "workspace too small");
     hipStream_t s = as_stream(stream);
     char* ws = (char*)workspace;
     BaParams p{};
     p.poses = poses; p.patches = patches; p.intrinsics = intrinsics; p.target = target; p.weight = weight;
     p.lmbda = lmbda; p.ii = ii; p.jj = jj; p.kk = kk; p.E = num_edges; p.num_patches = num_patches;
     p.P = P; p.t0 = t0; p.N = N; p.n6 = 6 * N;
+    if (ba_sparse(N, flags)) {
+        const BsLayout L = bs_layout(num_edges, num_patches, N);
+        DPVO_CHECK_ARG(workspace && workspace_bytes >= L.total, "workspace too small");
+        DPVO_CHECK_ARG(num_edges < 0x7fffffff, "too many edges");
+        if (num_edges == 0 || iterations == 0) {
+            if (status) DPVO_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
+            return 0;
+        }
+        p.status = status;
+        return ba_forward_sparse(p, ws, L, iterations, s);
+    }
+    const BaLayout L = ba_layout(num_edges, num_patches, N);
+    DPVO_CHECK_ARG(workspace && workspace_bytes >= L.total, "workspace too small");
     p.hdr = (int*)(ws + L.hdr);
     p.status = status ? status : p.hdr + HDR_STATUS;
     {
@@ -928,9 +1539,9 @@ extern "C" int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches
     const size_t lds_v = lds_b ? (size_t)(p.n6 * (p.n6 + 1) + p.n6) * 8 : 0;
     for (int it = 0; it < iterations; it++) {
         if (lds_b)
-            hipLaunchKernelGGL(ba_hessian_kernel<true>, dim3(gH), dim3(256), lds_h, s, p);
+            hipLaunchKernelGGL((ba_hessian_kernel<true, false>), dim3(gH), dim3(256), lds_h, s, p);
         else
-            hipLaunchKernelGGL(ba_hessian_kernel<false>, dim3(gH), dim3(256), 0, s, p);
+            hipLaunchKernelGGL((ba_hessian_kernel<false, false>), dim3(gH), dim3(256), 0, s, p);
         if (N > 0) {
             hipLaunchKernelGGL(ba_schur_kernel, dim3(gS), dim3(256), lds_s, s, p);
             static const bool block_solve = getenv("DPVO_BA_BLOCK_SOLVE") != nullptr;  // A/B switch
@@ -943,6 +1554,15 @@ extern "C" int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches
         DPVO_CHECK_LAUNCH();
     }
     return 0;
+}
+
+extern "C" int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
+                               const float* target, const float* weight, const float* lmbda, const int64_t* ii,
+                               const int64_t* jj, const int64_t* kk, int64_t num_edges, int t0, int t1,
+                               int iterations, void* workspace, size_t workspace_bytes, int* status, void* stream)
+{
+    return dpvo_ba_forward_ex(poses, patches, num_patches, P, intrinsics, target, weight, lmbda, ii, jj, kk,
+                              num_edges, t0, t1, iterations, 0, workspace, workspace_bytes, status, stream);
 }
 
 extern "C" int dpvo_reproject(const float* poses, const float* patches, int P, const float* intrinsics,

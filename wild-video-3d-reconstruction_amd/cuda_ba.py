@@ -9,12 +9,18 @@ when the Schur system is not positive definite (torch::linalg::cholesky in
 ba_cuda.cu:521 raises); it costs one device->host read of a status word per
 call.  Set it to False for fully asynchronous / graph-captured use; the
 status is then left in ``last_status`` (a device tensor).
+
+Windows of more than 64 optimised poses (the global BA of dpvo.py:436-505)
+take the sparse path automatically: per-edge Schur entries and a tiled band
+Cholesky instead of the dense E / S (see include/dpvo_hot.h).  ``SPARSE =
+True`` forces it for any window (used by the parity tests).
 """
 import torch
 
 import _dpvo_hot as H
 
 CHECK_CHOLESKY = True
+SPARSE = False
 last_status = None
 
 
@@ -34,13 +40,14 @@ def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t
     lmbda = lmbda.to(device=poses.device, dtype=torch.float32).contiguous()
     E = ii.numel()
     N = int(t1) - int(t0)
-    nbytes = H.lib().dpvo_ba_workspace_bytes(E, num_patches, max(N, 0))
+    flags = 1 if SPARSE else 0
+    nbytes = H.lib().dpvo_ba_workspace_bytes_ex(E, num_patches, max(N, 0), flags)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=poses.device)
     status = torch.zeros(1, dtype=torch.int32, device=poses.device)
-    H.check(H.lib().dpvo_ba_forward(
+    H.check(H.lib().dpvo_ba_forward_ex(
         H.ptr(poses), H.ptr(patches), num_patches, P, H.ptr(intrinsics), H.ptr(target), H.ptr(weight), H.ptr(lmbda),
-        H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(t0), int(t1), int(iterations), H.ptr(ws), nbytes, H.ptr(status),
-        H.stream_of(poses)))
+        H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(t0), int(t1), int(iterations), flags, H.ptr(ws), nbytes,
+        H.ptr(status), H.stream_of(poses)))
     last_status = status
     if CHECK_CHOLESKY:
         s = int(status.item())
