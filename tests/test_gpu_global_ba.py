@@ -67,8 +67,12 @@ def check(st, t0, t1, iters, sparse=True):
     return gp, gq
 
 
-def check_within_reorder_spread(st, t0, t1, iters, sparse=True, nperm=2):
-    """|gpu - oracle| <= 3 x the oracle's own spread over permuted edge orders."""
+def check_within_reorder_spread(st, t0, t1, iters, sparse=True, nperm=6):
+    """|gpu - oracle| <= 3 x the oracle's own spread over permuted edge orders.
+
+    The spread estimate needs several orders: at n=50 the max-abs pose spread
+    of single permutations ranges over 3e-4 .. 1.6e-3 (12 orders measured),
+    so two orders can under-estimate it 5x."""
     gp, gq = run_gpu_ba(st["poses"], st["patches"], st["intrinsics"], st["target"], st["weight"], st["ii"], st["jj"],
                         st["kk"], t0, t1, iters, sparse=sparse)
     rp, rq, status = oracle_ba(st, t0, t1, iters)
@@ -117,7 +121,7 @@ def test_global_ba_c4_shape_n1024():
     """C4's formulation at the largest size the reference's dense E is
     representable at (n <= 1024), M reduced to keep the oracle fast."""
     st = global_state(11, n=1024, M=2)
-    check_within_reorder_spread(st, 1, 1024, 2, nperm=1)
+    check_within_reorder_spread(st, 1, 1024, 2, nperm=2)
 
 
 @pytest.mark.parametrize("sparse", [True, False])
