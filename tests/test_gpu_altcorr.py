@@ -111,6 +111,19 @@ def test_pyramid_dpvo_sized_bitexact(seed):
     assert np.array_equal(got, bits(ref))
 
 
+@pytest.mark.parametrize("spread", [1.4, 1.8, 2.3])
+def test_pyramid_wide_boxes_bitexact(spread):
+    """Scaled patches (perspective between distant frames): floor spreads of
+    3-4 px take the 11x11 / 12x12 shared box, wider ones the per-pixel windows."""
+    import cuda_corr
+    d = dev()
+    gmap, f1, f2, ii, jj, coords = dpvo_sized_inputs(7, E=1200, spread=spread, edge_cases=False)
+    out = cuda_corr.forward_pyramid(gmap.to(d), [channel_last(f1.to(d)), channel_last(f2.to(d))], coords.to(d),
+                                    ii.to(d), jj.to(d), 3, [1, 4])
+    ref = oracle.corr_pyramid(gmap.numpy(), [f1.numpy(), f2.numpy()], coords.numpy(), ii.numpy(), jj.numpy())
+    assert np.array_equal(bits(out.cpu().numpy()), bits(ref))
+
+
 def test_fast_and_generic_paths_agree():
     import cuda_corr
     d = dev()

@@ -31,6 +31,10 @@ namespace dpvo {
 
 namespace corr {
 constexpr int R = 3, D = 8, DO = 7, PS = 3, NP = 9, BOX = 10, NPAIR = 5;
+// v3's shared box: floor spreads up to 4 px (12 x 12).  At level 1 about 1 edge
+// in 9 of the C3 workload spreads by 3 px (perspective scale ~1.4 between
+// frames up to 35 apart); per-pixel windows would cost it 4x the common pass.
+constexpr int SBOX = 12;
 }
 
 struct CorrFastParams {
@@ -80,7 +84,7 @@ struct LevelMeta {
     int fy[corr::NP], fx[corr::NP];
     float xs[corr::NP], ys[corr::NP];
     int fast, oy, ox, bw, bh, nslots, first_slot, pad;
-    float rbw;   // 1 / bw (v3 decode: exact floor((loc + 0.5) / bw) for loc < 128)
+    float rbw;   // 1 / bw (v3 decode: exact floor((loc + 0.5) / bw) for loc < 256, bw <= 12)
 };
 
 template <int NLEV, int C8>
@@ -324,7 +328,7 @@ __global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_sfast_kernel(Co
     using namespace corr;
     constexpr int NT = FastThreads<NLEV>::value;
     constexpr int C = C8 * 8;
-    __shared__ half_t raw[NLEV][NP][BOX * BOX];
+    __shared__ half_t raw[NLEV][NP][SBOX * SBOX];
     __shared__ LevelMeta meta[NLEV];
     // per (patch pixel, level): the reference's bilinear weights (each product
     // rounded to binary16 exactly as correlation_kernel.cu:221-232 forms them)
@@ -360,7 +364,7 @@ __global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_sfast_kernel(Co
             ymin = min(ymin, m.fy[q]); ymax = max(ymax, m.fy[q]);
             xmin = min(xmin, m.fx[q]); xmax = max(xmax, m.fx[q]);
         }
-        m.fast = ((int64_t)ymax - ymin) <= 2 && ((int64_t)xmax - xmin) <= 2;
+        m.fast = ((int64_t)ymax - ymin) <= SBOX - D && ((int64_t)xmax - xmin) <= SBOX - D;
         m.oy = wrap_add(ymin, -R);
         m.ox = wrap_add(xmin, -R);
         m.bh = m.fast ? (ymax - ymin) + D : D;
@@ -423,6 +427,7 @@ __global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_sfast_kernel(Co
     const uint32_t* T = p.f1tab + ((int64_t)b * p.N1 + (ix_ok ? ix : 0)) * C * 5;
 
     for (int base = 0; base < total; base += NT) {
+        if (base + (tid & ~63) >= total) continue;   // a wave with no slot in this pass skips it
         const Slot cur = decode(base + tid);
         half2_t acc[NPAIR];
 #pragma unroll
@@ -472,8 +477,16 @@ __global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_sfast_kernel(Co
                         const int c = 2 * j + hsel;
                         const half_t ws = hsel ? wv.y : wv.x;
                         const half2_t wb = {ws, ws};
+                        // all five products first, then the five sums (same per-op
+                        // rounding): a product feeding the very next instruction costs
+                        // an s_nop on gfx950 when its src0 carries op_sel_hi = 1 (the
+                        // hi-half broadcast), ~300 wait states per pass otherwise
+                        half2_t pr[NPAIR];
 #pragma unroll
-                        for (int q = 0; q < NPAIR; q++) acc[q] = acc[q] + wb * as_h2(fs[c * 5 + q]);
+                        for (int q = 0; q < NPAIR; q++) pr[q] = wb * as_h2(fs[c * 5 + q]);
+                        __builtin_amdgcn_sched_barrier(0);   // (an asm fence would itself cost the s_nop)
+#pragma unroll
+                        for (int q = 0; q < NPAIR; q++) acc[q] = acc[q] + pr[q];
                     }
                 }
                 // keep this step's arithmetic ahead of the next step's (volatile) loads:
@@ -500,7 +513,28 @@ __global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_sfast_kernel(Co
     __syncthreads();
 
     half_t* ob = p.out + b * p.o_b + (int64_t)e * p.o_e;
-    // thread -> fixed (patch pixel, level) qi, walking the 49 window positions
+    // DPVO's stacked row [x][y][P][P][level] (dpvo.py:333; what corr_pyramid
+    // writes): thread t owns the two levels of output pair t = (x, y, pixel), one
+    // half2 op per bilinear step (each lane rounds exactly like the scalar
+    // sequence) and one 4-byte store; a wave stores 256 contiguous bytes.
+    const bool stacked = NLEV == 2 && p.o_l == 1 && p.o_p == 2 && p.o_y == 18 && p.o_x == 126 &&
+                         ((uintptr_t)ob & 3) == 0;
+    if (stacked) {
+        for (int t = tid; t < DO * DO * NP; t += NT) {
+            const int pos = t / NP, q = t - pos * NP;
+            const int bx = pos / DO, a = pos - bx * DO;
+            const EpiQ t0 = epq[q * NLEV], t1 = epq[q * NLEV + 1];
+            const half_t* c0 = &raw[0][q][t0.base + a * t0.bw + bx];
+            const half_t* c1 = &raw[NLEV - 1][q][t1.base + a * t1.bw + bx];
+            half2_t v = half2_t{t0.w00, t1.w00} * half2_t{c0[0], c1[0]};
+            v = v + half2_t{t0.w01, t1.w01} * half2_t{c0[1], c1[1]};
+            v = v + half2_t{t0.w10, t1.w10} * half2_t{c0[t0.bw], c1[t1.bw]};
+            v = v + half2_t{t0.w11, t1.w11} * half2_t{c0[t0.bw + 1], c1[t1.bw + 1]};
+            *(half2_t*)(ob + 2 * t) = v;
+        }
+        return;
+    }
+    // general strides: thread -> fixed (patch pixel, level) qi, walking the 49 window positions
     constexpr int NQ = NP * NLEV, GR = NT / NQ;
     if (tid < NQ * GR) {
         const int qi = tid % NQ, g = tid / NQ;
