@@ -546,6 +546,189 @@ __global__ __launch_bounds__(R2_THREADS, 2) void rowgemm2_kernel(dpvo_rowgemm_ar
     }
 }
 
+// ---------------------------------------------------------------------------
+// v3: the v1 tiling (128 x 384, 8 waves, BK = 64) with the A stream prefetched
+// TWO stages ahead instead of one.  A (the activations, 73 MB per layer at C3)
+// is the HBM stream; W (295 KB) is L2-resident.  In v1 a stage holds A and W
+// together, so one stage of lookahead leaves only 16 KB of A in flight per CU
+// (4 MB chip-wide, ~2 TB/s at HBM latency).  Here W has 2 slots (48 KB) and A
+// a ring of 3 (16 KB), issued in the order W(i+1), A(i+2): the wait for step i
+// (vmcnt 10) then leaves A(i+1) and A(i+2) in flight.  The 96 KB y tile no
+// longer fits beside the rings, so the epilogue runs in two 64-row halves
+// through the consumed W slot.
+// ---------------------------------------------------------------------------
+constexpr int R3_W_SLOT = RG_W_STAGE;            // 48 KB
+constexpr int R3_A_BASE = 2 * R3_W_SLOT;         // A ring after the two W slots
+constexpr int R3_LDS = R3_A_BASE + 3 * RG_A_STAGE;   // 144 KB
+
+struct YMapSlot {   // 64 rows x 768 B in one W slot, 32-B granules XOR (row/4)&3
+    int base;
+    __device__ int off(int r, int byte) const { return base + r * 768 + (byte ^ (((r >> 2) & 3) << 5)); }
+};
+
+template <int FLAGS>
+__global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_args p)
+{
+    __shared__ __attribute__((aligned(16))) char smem[R3_LDS];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int K = p.K;
+    const int ksteps = K / RG_BK;
+    const int64_t Mrows = p.M_dev ? min(*p.M_dev, p.M) : p.M;
+    const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
+    if ((int64_t)blockIdx.x >= ntiles) return;
+    const int64_t my_tiles = (ntiles - 1 - blockIdx.x) / gridDim.x + 1;
+    const int64_t total = my_tiles * ksteps;
+
+    const half_t* __restrict__ Wt = (const half_t*)p.W;
+    const half_t* __restrict__ zero = (const half_t*)p.zero_row;
+    const int srow = lane >> 3, pch = lane & 7;
+    const half_t* wsrc[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+        const int n = (wave * 6 + j) * 8 + srow;
+        wsrc[j] = Wt + (int64_t)n * K + 8 * (pch ^ ((n >> 1) & 7));
+    }
+    // A rows of the tile a flat step belongs to (two tiles can be in flight)
+    auto a_src = [&](int64_t tile, int j) {
+        const int r = (wave * 2 + j) * 8 + srow;
+        const int64_t m = tile * RG_BM + r;
+        const half_t* row = zero;
+        if (m < Mrows) {
+            const int64_t s = p.a_idx ? p.a_idx[m] : m;
+            if (s >= 0 && s < p.a_rows) row = (const half_t*)p.A + s * p.lda;
+        }
+        return row + 8 * (pch ^ ((r >> 1) & 7));
+    };
+    // flat step f -> (tile, k-step) of this block
+    auto tile_of = [&](int64_t f) { return (int64_t)blockIdx.x + (f / ksteps) * gridDim.x; };
+    const half_t* asrc[2];
+    int64_t asrc_tile = -1;
+    auto issue_a = [&](int64_t f) {
+        const int64_t t = tile_of(f);
+        if (t != asrc_tile) {
+            asrc[0] = a_src(t, 0);
+            asrc[1] = a_src(t, 1);
+            asrc_tile = t;
+        }
+        char* sA = smem + R3_A_BASE + (int)(f % 3) * RG_A_STAGE;
+        const int k0 = (int)(f % ksteps) * RG_BK;
+        glds16(asrc[0] + k0, sA + (wave * 2 + 0) * 1024);
+        glds16(asrc[1] + k0, sA + (wave * 2 + 1) * 1024);
+    };
+    auto issue_w = [&](int64_t f) {
+        char* sW = smem + (int)(f & 1) * R3_W_SLOT;
+        const int k0 = (int)(f % ksteps) * RG_BK;
+#pragma unroll
+        for (int j = 0; j < 6; j++) glds16(wsrc[j] + k0, sW + (wave * 6 + j) * 1024);
+    };
+
+    f4_t acc[4][6];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+    const int fr = lane & 15, fq = lane >> 4;
+    int a_off[4], w_off[6], a_sw[4], w_sw[6];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++) {
+        const int row = wm * 64 + mt * 16 + fr;
+        a_off[mt] = row * 128;
+        a_sw[mt] = (row >> 1) & 7;
+    }
+#pragma unroll
+    for (int nt = 0; nt < 6; nt++) {
+        const int n = wn * 96 + nt * 16 + fr;
+        w_off[nt] = n * 128;
+        w_sw[nt] = (n >> 1) & 7;
+    }
+
+    EpiConsts kc;
+    load_consts<FLAGS>(p, lane, kc);
+    // prologue: A(0), W(0), A(1) -- then every step issues W(i+1), A(i+2)
+    issue_a(0);
+    issue_w(0);
+    if (total > 1) issue_a(1);
+    for (int64_t i = 0; i < total; i++) {
+        const bool w_next = i + 1 < total, a_next = i + 2 < total;
+        if (w_next) issue_w(i + 1);
+        if (a_next) issue_a(i + 2);
+        // outstanding after W(i): A(i+1) [2], W(i+1) [6], A(i+2) [2]
+        if (a_next)
+            asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        else if (w_next)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        const char* sA = smem + R3_A_BASE + (int)(i % 3) * RG_A_STAGE;
+        const char* sW = smem + (int)(i & 1) * R3_W_SLOT;
+#pragma unroll
+        for (int kk = 0; kk < 2; kk++) {
+            const int c = kk * 4 + fq;
+            h8_t a[4], b[6];
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(sA + a_off[mt] + 16 * (c ^ a_sw[mt]));
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(sW + w_off[nt] + 16 * (c ^ w_sw[nt]));
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                for (int nt = 0; nt < 6; nt++)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_barrier();
+        if ((int)(i % ksteps) != ksteps - 1) continue;
+
+        // ---- epilogue of tile t: two 64-row halves through the consumed W slot.
+        // Half h holds tile rows {64 w + 32 h + [0, 32)}, w = 0, 1: every wave
+        // contributes its m-tiles 2h, 2h+1, so only half of the (fp16) y values
+        // stay in registers across the first half's row pass.
+        const int64_t cur_tile = tile_of(i);
+        const YMapSlot ym{(int)(i & 1) * R3_W_SLOT};
+        half_t y16[4][6][4];
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) {
+            const float bias = (float)((const half_t*)p.bias)[wn * 96 + nt * 16 + fr];
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    half_t y = (half_t)(acc[mt][nt][r] + bias);
+                    if (FLAGS & RG_RELU) y = y > (half_t)0 ? y : (half_t)0;
+                    if (FLAGS & RG_SIGMOID) y = (half_t)fast_sigmoid((float)y);
+                    y16[mt][nt][r] = y;
+                    acc[mt][nt][r] = 0.f;
+                }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) {
+                const int cl = wn * 96 + nt * 16 + fr;
+#pragma unroll
+                for (int mm = 0; mm < 2; mm++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++)
+                        *(half_t*)(smem + ym.off(wm * 32 + mm * 16 + fq * 4 + r, cl * 2)) = y16[2 * h + mm][nt][r];
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            constexpr int RB = (FLAGS & (RG_RES | RG_GATE)) ? 4 : 8;   // rows per batch (register budget)
+            const int lr = wave * 8;                                    // 8 rows inside one 32-row block
+            const int64_t row0 = cur_tile * RG_BM + (lr >> 5) * 64 + h * 32 + (lr & 31);
+#pragma unroll
+            for (int q0 = 0; q0 < 8; q0 += RB)
+                epilogue_rows<FLAGS, RB>(p, Mrows, smem, ym, lr + q0, row0 + q0, lane, kc);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+    }
+}
+
 // v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16   (one wave per row)
 __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
 {
@@ -640,8 +823,10 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
         if (g_num_cus <= 0) g_num_cus = 256;
     }
     static const int version = [] {
-        const char* v = getenv("DPVO_ROWGEMM");   // 1 (default): one 128-row workgroup per CU; 2: two 64-row
-        return v ? atoi(v) : 1;
+        // 1: one 128-row workgroup per CU; 2: two 64-row workgroups per CU;
+        // 3 (default): v1 tiling with the A stream two stages ahead
+        const char* v = getenv("DPVO_ROWGEMM");
+        return v ? atoi(v) : 3;
     }();
     if (version == 2) {
         const int64_t nt2 = (a->M + R2_BM - 1) / R2_BM;
@@ -670,6 +855,29 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
     }
     const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
     const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+    if (version == 3) {
+        switch (f) {
+#define R3_CASE(F)                                                                                            \
+    case (F):                                                                                                 \
+        hipLaunchKernelGGL(rowgemm3_kernel<(F)>, dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a); \
+        break;
+            R3_CASE(0)
+            R3_CASE(DPVO_RG_RELU)
+            R3_CASE(DPVO_RG_SIGMOID)
+            R3_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
+            R3_CASE(DPVO_RG_RES)
+            R3_CASE(DPVO_RG_RES | DPVO_RG_LN)
+            R3_CASE(DPVO_RG_GATE | DPVO_RG_LN)
+            R3_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
+            R3_CASE(DPVO_RG_GATE)
+#undef R3_CASE
+        default:
+            set_error("dpvo_rowgemm: unsupported epilogue flag combination " + std::to_string(f));
+            return -1;
+        }
+        DPVO_CHECK_LAUNCH();
+        return 0;
+    }
     switch (f) {
         RG_CASE(0)
         RG_CASE(DPVO_RG_RELU)
