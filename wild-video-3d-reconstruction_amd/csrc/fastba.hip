@@ -258,14 +258,26 @@ __global__ __launch_bounds__(256) void ba_mark_kernel(BaParams p)
     }
 }
 
+constexpr int SCAN_LDS_WORDS = 16384;   // 64 KB: the bitmap of up to 524,288 patches
+
 __global__ __launch_bounds__(1024) void ba_scan_kernel(BaParams p, int64_t nwords)
 {
     __shared__ int part[1024];
+    __shared__ uint32_t sbits[SCAN_LDS_WORDS];
     const int tid = threadIdx.x;
     const int64_t per = (nwords + 1023) / 1024;
     const int64_t w0 = tid * per, w1 = min(nwords, w0 + per);
+    // Each thread owns a contiguous run of words; reading them in place is a
+    // chain of dependent-latency loads per thread, so the bitmap is first
+    // staged through LDS with coalesced, independent loads.
+    const bool staged = nwords <= SCAN_LDS_WORDS;
+    if (staged) {
+        for (int64_t w = tid; w < nwords; w += 1024) sbits[w] = p.bits[w];
+        __syncthreads();
+    }
+    auto word = [&](int64_t w) { return staged ? sbits[w] : p.bits[w]; };
     int cnt = 0;
-    for (int64_t w = w0; w < w1; w++) cnt += __popc(p.bits[w]);
+    for (int64_t w = w0; w < w1; w++) cnt += __popc(word(w));
     part[tid] = cnt;
     __syncthreads();
     // inclusive Hillis-Steele scan over 1024 partials
@@ -277,7 +289,7 @@ __global__ __launch_bounds__(1024) void ba_scan_kernel(BaParams p, int64_t nword
     }
     int base = part[tid] - cnt;
     for (int64_t w = w0; w < w1; w++) {
-        uint32_t m = p.bits[w];
+        uint32_t m = word(w);
         p.wordbase[w] = base;
         while (m) {
             const int bit = __ffs(m) - 1;

@@ -672,52 +672,57 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_ar
             for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(sA + a_off[mt] + 16 * (c ^ a_sw[mt]));
 #pragma unroll
             for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(sW + w_off[nt] + 16 * (c ^ w_sw[nt]));
+            // W as the first operand: the accumulator is the transposed tile, lane
+            // (fr, fq) holding row fr, columns 4 fq .. 4 fq + 3 of each 16 x 16 block
 #pragma unroll
             for (int mt = 0; mt < 4; mt++)
 #pragma unroll
                 for (int nt = 0; nt < 6; nt++)
-                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt], b[nt], acc[mt][nt], 0, 0, 0);
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
         }
         __builtin_amdgcn_s_barrier();
         if ((int)(i % ksteps) != ksteps - 1) continue;
 
-        // ---- epilogue of tile t: two 64-row halves through the consumed W slot.
-        // Half h holds tile rows {64 w + 32 h + [0, 32)}, w = 0, 1: every wave
-        // contributes its m-tiles 2h, 2h+1, so only half of the (fp16) y values
-        // stay in registers across the first half's row pass.
+        // ---- epilogue of tile t.  y16 = act(fp16(acc + b)): four consecutive
+        // columns of one row per (m-tile, n-tile) and lane.
         const int64_t cur_tile = tile_of(i);
-        const YMapSlot ym{(int)(i & 1) * R3_W_SLOT};
-        half_t y16[4][6][4];
+        typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+        h4_t y16[4][6];
 #pragma unroll
         for (int nt = 0; nt < 6; nt++) {
-            const float bias = (float)((const half_t*)p.bias)[wn * 96 + nt * 16 + fr];
+            const h4_t bias = *(const h4_t*)((const half_t*)p.bias + wn * 96 + nt * 16 + 4 * fq);
 #pragma unroll
-            for (int mt = 0; mt < 4; mt++)
+            for (int mt = 0; mt < 4; mt++) {
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
-                    half_t y = (half_t)(acc[mt][nt][r] + bias);
+                    half_t y = (half_t)(acc[mt][nt][r] + (float)bias[r]);
                     if (FLAGS & RG_RELU) y = y > (half_t)0 ? y : (half_t)0;
                     if (FLAGS & RG_SIGMOID) y = (half_t)fast_sigmoid((float)y);
                     y16[mt][nt][r] = y;
                     acc[mt][nt][r] = 0.f;
                 }
+            }
         }
+        // Two 64-row halves through the consumed W slot (whole-row stores are
+        // coalesced; 8-byte stores straight from the accumulator layout measured
+        // slower even with no row-wise op).  Half h holds tile rows
+        // {64 w + 32 h + [0, 32)}, w = 0, 1: every wave writes its m-tiles 2h,
+        // 2h+1, so only half of y16 stays live across the first half's row pass.
+        const YMapSlot ym{(int)(i & 1) * R3_W_SLOT};
 #pragma unroll
         for (int h = 0; h < 2; h++) {
 #pragma unroll
             for (int nt = 0; nt < 6; nt++) {
-                const int cl = wn * 96 + nt * 16 + fr;
+                const int col = wn * 96 + nt * 16 + 4 * fq;
 #pragma unroll
                 for (int mm = 0; mm < 2; mm++)
-#pragma unroll
-                    for (int r = 0; r < 4; r++)
-                        *(half_t*)(smem + ym.off(wm * 32 + mm * 16 + fq * 4 + r, cl * 2)) = y16[2 * h + mm][nt][r];
+                    *(h4_t*)(smem + ym.off(wm * 32 + mm * 16 + fr, col * 2)) = y16[2 * h + mm][nt];
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            constexpr int RB = (FLAGS & (RG_RES | RG_GATE)) ? 4 : 8;   // rows per batch (register budget)
-            const int lr = wave * 8;                                    // 8 rows inside one 32-row block
+            constexpr int RB = (FLAGS & (RG_RES | RG_GATE | RG_LN)) ? 4 : 8;   // rows per batch (register budget)
+            const int lr = wave * 8;                                             // 8 rows inside one 32-row block
             const int64_t row0 = cur_tile * RG_BM + (lr >> 5) * 64 + h * 32 + (lr & 31);
 #pragma unroll
             for (int q0 = 0; q0 < 8; q0 += RB)
@@ -815,6 +820,11 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
     DPVO_CHECK_ARG(!(f & DPVO_RG_GATE) || a->gate16, "rowgemm: gate input missing");
     DPVO_CHECK_ARG(!(f & DPVO_RG_LN) || (a->ln_g && a->ln_b), "rowgemm: LayerNorm weights missing");
     DPVO_CHECK_ARG(!(f & DPVO_RG_HEADS) || (a->head_w && a->head_b && a->head_out), "rowgemm: head weights missing");
+    DPVO_CHECK_ARG(!a->out16 || (a->ldo16 % 4 == 0 && ((uintptr_t)a->out16 & 7) == 0),
+                   "rowgemm: out16 needs 8-byte aligned rows (ldo16 % 4 == 0)");
+    DPVO_CHECK_ARG(!a->out32 || (a->ldo32 % 4 == 0 && ((uintptr_t)a->out32 & 15) == 0),
+                   "rowgemm: out32 needs 16-byte aligned rows (ldo32 % 4 == 0)");
+    DPVO_CHECK_ARG(((uintptr_t)a->bias & 7) == 0, "rowgemm: bias must be 8-byte aligned");
     if (a->M <= 0) return 0;
     if (g_num_cus == 0) {
         int dev = 0;
@@ -824,7 +834,9 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
     }
     static const int version = [] {
         // 1: one 128-row workgroup per CU; 2: two 64-row workgroups per CU;
-        // 3 (default): v1 tiling with the A stream two stages ahead
+        // 3 (default): v1 tiling, A stream two stages ahead, transposed accumulators.
+        // (Measured and dropped: stage fills through registers instead of LDS-DMA,
+        // and v2 + register fills -- neither beat v3 on the C3 update operator.)
         const char* v = getenv("DPVO_ROWGEMM");
         return v ? atoi(v) : 3;
     }();
