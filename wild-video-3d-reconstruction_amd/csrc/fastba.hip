@@ -149,7 +149,8 @@ constexpr int BS_TILE = 64;            // tile edge of the banded reduced camera
 constexpr int BS_NMAX = 32767;         // pose keys are packed as 16-bit pairs in the Schur reduction
 
 struct BaLayout {
-    size_t hdr, bits, wordbase, kx, B, v, C, u, E, S, y, dX, Sd, yd, total;
+    size_t hdr, bits, wordbase, kx, B, v, C, u, E, S, y, dX, Sd, yd, Bpart, total;
+    int nbH;   // Hessian workgroups (each leaves one partial B / v in Bpart)
     int64_t nwords, mu_max;
     int n6;
 };
@@ -182,6 +183,9 @@ static BaLayout ba_layout(int64_t E, int64_t num_patches, int N)
     const bool big = L.n6 > 6 * 12;
     L.Sd = take(big ? n6 * (n6 + 1) * 8 : 8);
     L.yd = take(big ? n6 * 8 : 8);
+    // per-workgroup partial B / v of the LDS Hessian path, reduced by ba_breduce_kernel
+    L.nbH = (int)grid_for(E > 0 ? E : 1, 256, 1024);
+    L.Bpart = take(N <= BA_LDS_NMAX ? (size_t)L.nbH * (n6 * n6 + n6) * 4 : 8);
     L.total = off;
     return L;
 }
@@ -207,6 +211,8 @@ struct BaParams {
     double* Sd;
     double* yd;
     int red_iters;   // wave reductions of the pose-block terms per wave (0 = per-lane atomics only)
+    float* Bpart;    // [nbH][n6 * n6 + n6] per-workgroup partial B / v (LDS Hessian path)
+    int nbH;
     // sparse (band) path only -- see "large pose windows" below
     float* ent;      // [E][16] per-edge Schur entries: E_i row (6), E_j row (6), C, u
     const int* kptr; // [Mu + 1] CSR of the edges of each unique patch (into eord)
@@ -599,11 +605,38 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
         }
     }
     if (LDS_B) {
+        // one partial per workgroup, summed by ba_breduce_kernel: every workgroup
+        // adding into the same ~3.7k floats is the slow case of float atomics
+        // (MI355X_MICROARCH.md: every workgroup into one 2.3 KB row, 14x slower)
         __syncthreads();
-        for (int i = threadIdx.x; i < n6 * n6 + n6; i += blockDim.x) {
-            const float s = sB[i];
-            if (s != 0.f) atomicAdd(i < n6 * n6 ? &p.B[i] : &p.v[i - n6 * n6], s);
-        }
+        float* dst = p.Bpart + (int64_t)blockIdx.x * (n6 * n6 + n6);
+        for (int i = threadIdx.x; i < n6 * n6 + n6; i += blockDim.x) dst[i] = sB[i];
+    }
+}
+
+// B / v = sum of the Hessian workgroups' partials.  A workgroup owns 64
+// consecutive entries; its 16 waves stride over the partials (coalesced
+// 256-byte rows) and combine through LDS.  Fixed order: deterministic.
+__global__ __launch_bounds__(1024) void ba_breduce_kernel(BaParams p)
+{
+    __shared__ float red[16][64];
+    if (failed(p)) return;
+    const int n6 = p.n6, ne = n6 * n6 + n6;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + lane;
+    float s = 0.f;
+    if (i < ne) {
+#pragma unroll 8
+        for (int b = wave; b < p.nbH; b += 16) s += p.Bpart[(int64_t)b * ne + i];
+    }
+    red[wave][lane] = s;
+    __syncthreads();
+    if (wave == 0 && i < ne) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < 16; w++) t += red[w][lane];
+        if (i < n6 * n6) p.B[i] = t;
+        else p.v[i - n6 * n6] = t;
     }
 }
 
@@ -613,33 +646,68 @@ __global__ __launch_bounds__(256) void ba_hessian_kernel(BaParams p)
 constexpr int SCHUR_CHUNK = 64;
 
 
+__device__ __forceinline__ int schur_chunk(int n6) { return n6 <= 96 ? SCHUR_CHUNK : 16; }
+static inline size_t schur_lds_bytes(int n6)
+{
+    const int ch = n6 <= 96 ? SCHUR_CHUNK : 16;
+    return ((size_t)2 * n6 * (ch + 4) + ch) * 4;
+}
+
+// The chunk's E rows are staged TRANSPOSED (pose coordinate major, patch
+// minor, 4-float padded pitch), once as E Q and once as E, so an entry's
+// k-sum runs over float4 LDS reads with independent accumulators per entry.
+// (Patch-major staging made every k step a dependent ds_read_b32 round trip:
+// 40 us per call, 65 % parked on s_waitcnt.)
 __global__ __launch_bounds__(256) void ba_schur_kernel(BaParams p)
 {
-    extern __shared__ __attribute__((aligned(16))) float sE[];  // [SCHUR_CHUNK][n6] rows + [SCHUR_CHUNK] Q
+    extern __shared__ __attribute__((aligned(16))) float sm[];  // sEQ [n6][pitch], sEt [n6][pitch], sU [ch]
     if (failed(p)) return;
     const int Mu = p.hdr[HDR_MU];
     const int n6 = p.n6;
     const int nup = n6 * (n6 + 1) / 2;
     const float lm = p.lmbda[0];
-    float* sQ = sE + SCHUR_CHUNK * n6;
-    for (int64_t k0 = (int64_t)blockIdx.x * SCHUR_CHUNK; k0 < Mu; k0 += (int64_t)gridDim.x * SCHUR_CHUNK) {
-        const int cnt = (int)min((int64_t)SCHUR_CHUNK, Mu - k0);
+    const int ch = schur_chunk(n6), pitch = ch + 4;
+    float* sEQ = sm;
+    float* sEt = sm + n6 * pitch;
+    float* sU = sm + 2 * n6 * pitch;
+    for (int64_t k0 = (int64_t)blockIdx.x * ch; k0 < Mu; k0 += (int64_t)gridDim.x * ch) {
+        const int cnt = (int)min((int64_t)ch, Mu - k0);
         __syncthreads();
-        for (int i = threadIdx.x; i < cnt * n6; i += blockDim.x) sE[i] = p.Em[k0 * n6 + i];
-        for (int i = threadIdx.x; i < cnt; i += blockDim.x) sQ[i] = 1.0f / (p.C[k0 + i] + lm);
+        for (int i = threadIdx.x; i < ch * n6; i += blockDim.x) {
+            const int kk = i / n6, a = i - kk * n6;
+            float e = 0.f, q = 0.f;
+            if (kk < cnt) {
+                e = p.Em[(k0 + kk) * n6 + a];
+                q = 1.0f / (p.C[k0 + kk] + lm);
+            }
+            sEQ[a * pitch + kk] = e * q;
+            sEt[a * pitch + kk] = e;
+        }
+        for (int kk = threadIdx.x; kk < ch; kk += blockDim.x) sU[kk] = kk < cnt ? p.u[k0 + kk] : 0.f;
         __syncthreads();
         // upper triangle of sum_k (E_ak Q_k) E_bk, i.e. the reference's matmul(E*Q, E^T)
         for (int idx = threadIdx.x; idx < nup; idx += blockDim.x) {
-            int a = 0, rem = idx;
-            while (rem >= n6 - a) { rem -= n6 - a; a++; }
-            const int b = a + rem;
-            float s = 0.f;
-            for (int kk = 0; kk < cnt; kk++) s += (sE[kk * n6 + a] * sQ[kk]) * sE[kk * n6 + b];
+            // row a of the upper-triangle entry idx (row a holds n6 - a entries)
+            const float t = (float)(2 * n6 + 1);
+            int a = (int)((t - sqrtf(t * t - 8.f * (float)idx)) * 0.5f);
+            a = max(0, min(a, n6 - 1));
+            while (a > 0 && a * (2 * n6 - a + 1) / 2 > idx) a--;
+            while ((a + 1) * (2 * n6 - a) / 2 <= idx) a++;
+            const int b = a + (idx - a * (2 * n6 - a + 1) / 2);
+            const float4* ea = reinterpret_cast<const float4*>(sEQ + a * pitch);
+            const float4* eb = reinterpret_cast<const float4*>(sEt + b * pitch);
+            float s0 = 0.f, s1 = 0.f;
+            for (int q = 0; q < ch / 4; q++) {
+                const float4 x = ea[q], y = eb[q];
+                s0 += x.x * y.x + x.z * y.z;
+                s1 += x.y * y.y + x.w * y.w;
+            }
+            const float s = s0 + s1;
             if (s != 0.f) atomicAdd(&p.S[a * n6 + b], s);
         }
         for (int a = threadIdx.x; a < n6; a += blockDim.x) {
             float s = 0.f;
-            for (int kk = 0; kk < cnt; kk++) s += (sE[kk * n6 + a] * sQ[kk]) * p.u[k0 + kk];
+            for (int kk = 0; kk < cnt; kk++) s += sEQ[a * pitch + kk] * sU[kk];
             if (s != 0.f) atomicAdd(&p.y[a], s);
         }
     }
@@ -690,7 +758,9 @@ __device__ __forceinline__ double readlane_d(double v, int lane)
 // forward / backward substitution in fp32 -- the precision of the reference,
 // which factors the float32 S with torch::linalg::cholesky (ba_cuda.cu:518-521).
 // A single wave has no partner to hide latency behind, so the short fp32
-// sqrt / div chains (vs fp64) are what sets this kernel's time.
+// sqrt / div chains (vs fp64) are what sets this kernel's time.  (Measured
+// alternative: v_readlane broadcasts instead of LDS -- no waits, but ~14k
+// instructions through one wave's issue slot: no faster.)
 __device__ __forceinline__ void wave_lds_fence()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1531,6 +1601,8 @@ extern "C" int dpvo_ba_forward_ex(float* poses, float* patches, int64_t num_patc
     p.Em = (float*)(ws + L.E); p.S = (float*)(ws + L.S); p.y = (float*)(ws + L.y); p.dX = (float*)(ws + L.dX);
     p.Sd = (double*)(ws + L.Sd);
     p.yd = (double*)(ws + L.yd);
+    p.Bpart = (float*)(ws + L.Bpart);
+    p.nbH = L.nbH;
     if (num_edges == 0 || iterations == 0) {
         if (status) DPVO_CHECK_HIP(hipMemsetAsync(status, 0, sizeof(int), s));
         return 0;
@@ -1544,15 +1616,18 @@ extern "C" int dpvo_ba_forward_ex(float* poses, float* patches, int64_t num_patc
     DPVO_CHECK_LAUNCH();
     const bool lds_b = N <= BA_LDS_NMAX;
     const size_t lds_h = lds_b ? (size_t)(p.n6 * p.n6 + p.n6) * 4 : 0;
-    const unsigned gH = grid_for(num_edges, 256, 1024);
+    const unsigned gH = (unsigned)L.nbH;
     const unsigned gP = grid_for(L.mu_max, 256, 1024);
-    const unsigned gS = (unsigned)std::min<int64_t>((L.mu_max + SCHUR_CHUNK - 1) / SCHUR_CHUNK, 512);
-    const size_t lds_s = (size_t)(SCHUR_CHUNK * p.n6 + SCHUR_CHUNK) * 4;
+    const int sch = p.n6 <= 96 ? SCHUR_CHUNK : 16;
+    const unsigned gS = (unsigned)std::min<int64_t>((L.mu_max + sch - 1) / sch, 512);
+    const size_t lds_s = schur_lds_bytes(p.n6);
     const size_t lds_v = lds_b ? (size_t)(p.n6 * (p.n6 + 1) + p.n6) * 8 : 0;
     for (int it = 0; it < iterations; it++) {
-        if (lds_b)
+        if (lds_b) {
             hipLaunchKernelGGL((ba_hessian_kernel<true, false>), dim3(gH), dim3(256), lds_h, s, p);
-        else
+            if (p.n6 > 0)
+                hipLaunchKernelGGL(ba_breduce_kernel, dim3((p.n6 * p.n6 + p.n6 + 63) / 64), dim3(1024), 0, s, p);
+        } else
             hipLaunchKernelGGL((ba_hessian_kernel<false, false>), dim3(gH), dim3(256), 0, s, p);
         if (N > 0) {
             hipLaunchKernelGGL(ba_schur_kernel, dim3(gS), dim3(256), lds_s, s, p);
