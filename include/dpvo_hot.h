@@ -235,6 +235,13 @@ size_t dpvo_group_by_workspace_bytes(int64_t n);
 int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_t* gid, int* offs, int* perm, int64_t* groups,
                   void* workspace, size_t workspace_bytes, void* stream);
 
+/* cuda_ba.neighbors(kk, jj) (ba.cpp:113-158) over the CSR of dpvo_group_by(kk):
+ * within each group, the previous / next edge in (jj, edge) order, -1 at the
+ * ends -- the same result as dpvo_neighbors without its 64-bit radix sort.
+ * ix, jx [num_edges] int64; *groups read on the device (<= max_groups). */
+int dpvo_neighbors_csr(const int64_t* jj, const int* offs, const int* perm, const int64_t* groups,
+                       int64_t max_groups, int64_t num_edges, int64_t* ix, int64_t* jx, void* stream);
+
 /* dpvo_softagg_forward over a CSR from dpvo_group_by; the group count is read
  * from device memory (*groups <= max_groups); y rows >= *groups are untouched.
  * Sums run in ascending edge order: deterministic for every group size. */

@@ -114,6 +114,38 @@ def test_neighbors_large_matches_oracle():
     assert np.array_equal(jx.cpu().numpy(), rjx)
 
 
+def _neighbors_csr(kk, jj):
+    import update_ops as U
+    kk, jj = T(kk), T(jj)
+    _, offs, perm, G = U.group_by(kk, key_bits=32)
+    ix, jx = U.neighbors_csr(jj, offs, perm, G, kk.numel())
+    return ix.cpu().numpy(), jx.cpu().numpy()
+
+
+@pytest.mark.parametrize("pre", ["", "r_"])
+def test_neighbors_csr_golden(pre):
+    """The fused update operator's neighbours (over the kk group-by CSR) are the
+    reference's fastba.neighbors bit for bit."""
+    g = np.load(os.path.join(GOLDEN, "neighbors_ref.npz"))
+    ix, jx = _neighbors_csr(g[pre + "kk"], g[pre + "jj"])
+    assert np.array_equal(ix, g[pre + "ix"])
+    assert np.array_equal(jx, g[pre + "jx"])
+
+
+def test_neighbors_csr_large_and_big_groups():
+    st = synth_dpvo_state(3, n=60, M=32)
+    ix, jx = _neighbors_csr(st["kk"], st["jj"])
+    rix, rjx = oracle.neighbors(st["kk"], st["jj"])
+    assert np.array_equal(ix, rix) and np.array_equal(jx, rjx)
+    # groups larger than a wave (> 64 members) and repeated (kk, jj) pairs
+    rng = np.random.default_rng(0)
+    kk = rng.integers(0, 5, 700)
+    jj = rng.integers(0, 40, 700)
+    ix, jx = _neighbors_csr(kk, jj)
+    rix, rjx = oracle.neighbors(kk, jj)
+    assert np.array_equal(ix, rix) and np.array_equal(jx, rjx)
+
+
 def test_reproject_matches_oracle():
     import cuda_ba
     st = synth_dpvo_state(4)

@@ -433,6 +433,60 @@ extern "C" int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_
     return 0;
 }
 
+// neighbors over the kk group-by CSR: one wave per group; member i's
+// predecessor / successor in (jj, edge) order by an O(s^2) scan of the group
+// (s ~ 25 in DPVO's steady state), 64 members at a time, broadcast by shuffles.
+__global__ __launch_bounds__(256) void nb_csr_kernel(const int64_t* __restrict__ jj, const int* __restrict__ offs,
+                                                     const int* __restrict__ perm, const int64_t* __restrict__ groups,
+                                                     int64_t max_groups, int64_t* __restrict__ ix,
+                                                     int64_t* __restrict__ jx)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t G = min(*groups, max_groups);
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < G; g += nw) {
+        const int start = offs[g], s = offs[g + 1] - start;
+        for (int i0 = 0; i0 < s; i0 += 64) {
+            const bool mine = i0 + lane < s;
+            const int ei = mine ? perm[start + i0 + lane] : 0;
+            const int64_t ji = mine ? jj[ei] : 0;
+            // best predecessor (largest key below mine) / successor (smallest above)
+            int64_t pj = INT64_MIN, nj = INT64_MAX;
+            int pe = -1, ne = -1;
+            for (int t0 = 0; t0 < s; t0 += 64) {
+                const int cnt = min(64, s - t0);
+                const int et = t0 + lane < s ? perm[start + t0 + lane] : 0;
+                const int64_t jt = t0 + lane < s ? jj[et] : 0;
+                for (int k = 0; k < cnt; k++) {
+                    const int ek = __shfl(et, k);
+                    const int64_t jk = __shfl(jt, k);
+                    const bool below = jk < ji || (jk == ji && ek < ei);
+                    const bool above = jk > ji || (jk == ji && ek > ei);
+                    if (below && (jk > pj || (jk == pj && ek > pe))) { pj = jk; pe = ek; }
+                    if (above && (jk < nj || (jk == nj && ek < ne))) { nj = jk; ne = ek; }
+                }
+            }
+            if (mine) {
+                ix[ei] = pe;
+                jx[ei] = ne;
+            }
+        }
+    }
+}
+
+extern "C" int dpvo_neighbors_csr(const int64_t* jj, const int* offs, const int* perm, const int64_t* groups,
+                                  int64_t max_groups, int64_t num_edges, int64_t* ix, int64_t* jx, void* stream)
+{
+    DPVO_CHECK_ARG(groups != nullptr && offs != nullptr && perm != nullptr, "CSR missing");
+    DPVO_CHECK_ARG(num_edges >= 0 && num_edges < (int64_t(1) << 31), "bad size");
+    if (num_edges == 0 || max_groups <= 0) return 0;
+    const unsigned grid = grid_for(max_groups * 64, 256, 4096);
+    hipLaunchKernelGGL(nb_csr_kernel, dim3(grid), dim3(256), 0, as_stream(stream), jj, offs, perm, groups,
+                       max_groups, ix, jx);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
 extern "C" int dpvo_softagg_csr(int dtype, const void* f, int64_t ldf, const void* s, int64_t lds, const int* offs,
                                 const int* perm, const int64_t* groups, int64_t max_groups, int D, float eps, void* y,
                                 void* stream)

@@ -86,14 +86,17 @@ class Update(nn.Module):
         _, h, _ = U.rowgemm(h, *c1, flags=U.LN | U.LN_RELU, ln=cln)
         n32, n16, _ = U.rowgemm(h, *c2, flags=U.RES | U.LN, res32=net[0], res16=inp[0].contiguous(),
                                 ln=pk["norm"], want32=True)
-        ix, jx = fastba.neighbors(kk, jj)
+        # the kk group-by (SoftAgg below) also yields the temporal neighbours:
+        # fastba.neighbors(kk, jj) without a second sort
+        kk_groups = U.group_by(kk, key_bits=32)
+        ix, jx = U.neighbors_csr(jj, kk_groups[1], kk_groups[2], kk_groups[3], E)
         for (la, lb), nb in ((pk["c1"], ix), (pk["c2"], jx)):
             _, h, _ = U.rowgemm(n16, *la, flags=U.RELU, a_idx=nb)
             n32, n16, _ = U.rowgemm(h, *lb, flags=U.RES, res32=n32, want32=True)
         ln0, gr1, ln1, gr2 = pk["gru"]
-        for (pf, pg_, ph), key, ln in ((pk["agg_kk"], kk, None), (pk["agg_ij"], ii * 12345 + jj, ln0)):
+        for (pf, pg_, ph), key, ln in ((pk["agg_kk"], None, None), (pk["agg_ij"], ii * 12345 + jj, ln0)):
             # unique(key) + CSR on the device (no host sync); G stays on the device
-            gid, offs, perm, G = U.group_by(key, key_bits=32)
+            gid, offs, perm, G = kk_groups if key is None else U.group_by(key, key_bits=32)
             _, f16, _ = U.rowgemm(n16, *pf)
             _, g16, _ = U.rowgemm(n16, *pg_)
             y = U.softagg_csr(f16, g16, offs, perm, G, E)

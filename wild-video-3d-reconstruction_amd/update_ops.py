@@ -67,6 +67,20 @@ def softagg_csr(f, s, offs, perm, groups, max_groups, eps=1e-12):
     return y
 
 
+def neighbors_csr(jj, offs, perm, groups, max_groups):
+    """cuda_ba.neighbors(kk, jj) from the CSR of group_by(kk): -> (ix, jx) int64,
+    the previous / next edge of the same patch in (jj, edge) order, -1 at the
+    ends (ba.cpp:113-158) -- no radix sort of its own."""
+    H.on_gpu(jj, offs, perm, groups)
+    jj = H.idx64(jj)
+    E = jj.numel()
+    ix = torch.empty(E, dtype=torch.int64, device=jj.device)
+    jx = torch.empty(E, dtype=torch.int64, device=jj.device)
+    H.check(H.lib().dpvo_neighbors_csr(H.ptr(jj), H.ptr(offs), H.ptr(perm), H.ptr(groups), int(max_groups), E,
+                                       H.ptr(ix), H.ptr(jx), H.stream_of(jj)))
+    return ix, jx
+
+
 def gather_rows(x, idx, dtype=None):
     """out[e] = x[idx[e]] if idx[e] >= 0 else 0, cast to ``dtype`` (default x's).
     x: [R, D] with unit channel stride; idx: [n] int64."""
