@@ -129,9 +129,9 @@ def phase_breakdown(slam, reps=5):
         with torch.autocast("cuda", enabled=True):
             corr = slam.corr(coords)
             e[2].record()
-            ctx = slam.imap[:, slam.pg.kk % (slam.M * slam.pmem)]
-            net, (delta, weight, _) = slam.network.update(slam.pg.net, ctx, corr, None, slam.pg.ii, slam.pg.jj,
-                                                          slam.pg.kk)
+            ctx_idx = slam.pg.kk % (slam.M * slam.pmem)
+            net, (delta, weight, _) = slam.network.update(slam.pg.net, slam.imap, corr, None, slam.pg.ii, slam.pg.jj,
+                                                          slam.pg.kk, inp_idx=ctx_idx)
         target = coords[..., 1, 1] + delta.float()
         e[3].record()
         fastba.BA(slam.poses, slam.patches, slam.intrinsics, target, weight.float(), slam._lmbda, slam.pg.ii,

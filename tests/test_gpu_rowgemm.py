@@ -181,3 +181,24 @@ def test_fused_update_operator_matches_torch_path():
     assert err < 2e-2, err
     torch.testing.assert_close(df.float(), dt.float(), rtol=5e-2, atol=5e-2)
     torch.testing.assert_close(wf.float(), wt.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_fused_update_operator_context_index_is_the_gathered_context():
+    """DPVO.update passes the context ring + kk % (M pmem) (dpvo.py:718) and the
+    fused operator gathers the rows in its epilogue: identical to passing the
+    gathered ctx."""
+    from dpvo.net import Update
+    from dpvo.synthetic import steady_state_edges
+    torch.manual_seed(1)
+    upd = Update(3).cuda()
+    ii, jj, kk = steady_state_edges(40, 16, 13, 22, "cuda")
+    E = ii.numel()
+    net = torch.randn(1, E, 384, device="cuda")
+    ring = torch.randn(1, 36 * 16, 384, device="cuda").half()
+    idx = kk % (36 * 16)
+    corr = torch.randn(1, E, 882, device="cuda").half()
+    with torch.no_grad(), torch.autocast("cuda", enabled=True):
+        a = upd(net, ring[:, idx], corr, None, ii, jj, kk)
+        b = upd(net, ring, corr, None, ii, jj, kk, inp_idx=idx)
+    assert torch.equal(a[0], b[0])
+    assert torch.equal(a[1][0], b[1][0]) and torch.equal(a[1][1], b[1][1])

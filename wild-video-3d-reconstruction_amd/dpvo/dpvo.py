@@ -247,9 +247,10 @@ class DPVO:
             coords = self.reproject()
             with torch.autocast("cuda", enabled=True):
                 corr = self.corr(coords)
-                ctx = self.imap[:, self.pg.kk % (self.M * self.pmem)]
-                self.pg.net, (delta, weight, _) = self.network.update(self.pg.net, ctx, corr, None, self.pg.ii,
-                                                                      self.pg.jj, self.pg.kk)
+                # ctx = imap[:, kk % (M pmem)] (dpvo.py:718), gathered by the consumer
+                ctx_idx = self.pg.kk % (self.M * self.pmem)
+                self.pg.net, (delta, weight, _) = self.network.update(self.pg.net, self.imap, corr, None, self.pg.ii,
+                                                                      self.pg.jj, self.pg.kk, inp_idx=ctx_idx)
             weight = weight.float()
             target = coords[..., self.P // 2, self.P // 2] + delta.float()
         self.pg.target = target

@@ -68,7 +68,7 @@ class Update(nn.Module):
                 torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16 and
                 self.FUSED)
 
-    def _forward_fused(self, net, inp, corr, ii, jj, kk):
+    def _forward_fused(self, net, inp, corr, ii, jj, kk, inp_idx=None):
         """The same dataflow as the reference under autocast, in 19 full-row
         fused GEMMs (csrc/rowgemm.hip) + 2 SoftAggs: every Linear is an fp16
         GEMM with fp32 accumulate; residual adds, LayerNorms, gating and the
@@ -84,7 +84,10 @@ class Update(nn.Module):
         c0, c1, cln, c2 = pk["corr"]
         _, h, _ = U.rowgemm(c, *c0, flags=U.RELU)
         _, h, _ = U.rowgemm(h, *c1, flags=U.LN | U.LN_RELU, ln=cln)
-        n32, n16, _ = U.rowgemm(h, *c2, flags=U.RES | U.LN, res32=net[0], res16=inp[0].contiguous(),
+        # inp rows gathered inside the epilogue when the caller passes the index
+        # (DPVO.update: imap[:, kk % (M pmem)], dpvo.py:718) -- no E x 384 copy
+        res16, res16_idx = (inp[0], inp_idx) if inp_idx is not None else (inp[0].contiguous(), None)
+        n32, n16, _ = U.rowgemm(h, *c2, flags=U.RES | U.LN, res32=net[0], res16=res16, res16_idx=res16_idx,
                                 ln=pk["norm"], want32=True)
         # the kk group-by (SoftAgg below) also yields the temporal neighbours:
         # fastba.neighbors(kk, jj) without a second sort
@@ -115,10 +118,15 @@ class Update(nn.Module):
                                         want32=True)
         return n32[None], (heads[None, :, :2], heads[None, :, 2:], None)
 
-    def forward(self, net, inp, corr, flow, ii, jj, kk):
-        """edge hidden state -> (new state, (delta, weight, None)) (net.py:75-93)."""
-        if self._fusable(net, inp, corr):
-            return self._forward_fused(net, inp, corr, ii, jj, kk)
+    def forward(self, net, inp, corr, flow, ii, jj, kk, inp_idx=None):
+        """edge hidden state -> (new state, (delta, weight, None)) (net.py:75-93).
+
+        inp_idx (optional, not in the reference): inp is then the un-gathered
+        context ring and the rows are inp[:, inp_idx]."""
+        if self._fusable(net, inp, corr) and (inp_idx is None or inp.is_contiguous()):
+            return self._forward_fused(net, inp, corr, ii, jj, kk, inp_idx)
+        if inp_idx is not None:
+            inp = inp[:, inp_idx]
         net = self.norm(net + inp + self.corr(corr))
         ix, jx = fastba.neighbors(kk, jj)  # temporal neighbours of the same patch, on the device
         net = net + self.c1(self._neighbour(net, ix))
