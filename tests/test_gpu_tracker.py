@@ -98,3 +98,70 @@ def test_frame_by_frame_api():
         poses, tstamps = slam.terminate()
     assert poses.shape == (24, 7) and np.isfinite(poses).all()
     assert len(tstamps) == 24
+
+
+def _reference_keyframe(slam):
+    """The reference's keyframe() (dpvo.py:605-658) written out loop by loop:
+    boolean-mask edge removal and the per-frame buffer shift."""
+    from dpvo.lietorch import SE3
+    k = slam.n - slam.cfg.KEYFRAME_INDEX
+    i, j = k - 1, k + 1
+    m = slam.motionmag(i, j) + slam.motionmag(j, i)
+    if m / 2 < slam.cfg.KEYFRAME_THRESH:
+        t0, t1 = int(slam.pg.tstamps_[k - 1]), int(slam.pg.tstamps_[k])
+        slam.pg.delta[t1] = (t0, SE3(slam.pg.poses_[k]) * SE3(slam.pg.poses_[k - 1]).inv())
+        keep = ~((slam.pg.ii == k) | (slam.pg.jj == k))
+        slam.pg.weight, slam.pg.target = slam.pg.weight[:, keep], slam.pg.target[:, keep]
+        slam.pg.ii, slam.pg.jj, slam.pg.kk = slam.pg.ii[keep], slam.pg.jj[keep], slam.pg.kk[keep]
+        slam.pg.net = slam.pg.net[:, keep]
+        slam.pg.kk[slam.pg.ii > k] -= slam.M
+        slam.pg.ii[slam.pg.ii > k] -= 1
+        slam.pg.jj[slam.pg.jj > k] -= 1
+        for f in range(k, slam.n - 1):
+            g = f + 1
+            slam.pg.tstamps_[f] = slam.pg.tstamps_[g]
+            for buf in (slam.pg.colors_, slam.pg.poses_, slam.pg.patches_, slam.pg.patches_est_, slam.pg.intrinsics_):
+                buf[f] = buf[g]
+            slam.imap_[f % slam.pmem] = slam.imap_[g % slam.pmem]
+            slam.gmap_[f % slam.pmem] = slam.gmap_[g % slam.pmem]
+            slam.fmap1_[0, f % slam.pmem] = slam.fmap1_[0, g % slam.pmem]
+            slam.fmap2_[0, f % slam.pmem] = slam.fmap2_[0, g % slam.pmem]
+            slam.image_buffer_[f % slam.mem] = slam.image_buffer_[g % slam.mem]
+        slam.n -= 1
+        slam.pg.m -= slam.M
+    old = slam.ix[slam.pg.kk] < slam.n - slam.cfg.REMOVAL_WINDOW
+    keep = ~old
+    slam.pg.ii_inac = torch.cat((slam.pg.ii_inac, slam.pg.ii[old]))
+    slam.pg.jj_inac = torch.cat((slam.pg.jj_inac, slam.pg.jj[old]))
+    slam.pg.kk_inac = torch.cat((slam.pg.kk_inac, slam.pg.kk[old]))
+    slam.pg.weight_inac = torch.cat((slam.pg.weight_inac, slam.pg.weight[:, old]), dim=1)
+    slam.pg.target_inac = torch.cat((slam.pg.target_inac, slam.pg.target[:, old]), dim=1)
+    slam.pg.weight, slam.pg.target = slam.pg.weight[:, keep], slam.pg.target[:, keep]
+    slam.pg.ii, slam.pg.jj, slam.pg.kk = slam.pg.ii[keep], slam.pg.jj[keep], slam.pg.kk[keep]
+    slam.pg.net = slam.pg.net[:, keep]
+
+
+@pytest.mark.parametrize("drop", [True, False])
+def test_keyframe_matches_reference_loop(drop):
+    """keyframe() with index-based compaction and gathered buffer shifts ==
+    the reference's mask-and-loop version, buffer for buffer."""
+    from dpvo.synthetic import steady_state_tracker
+    with torch.no_grad():
+        a = steady_state_tracker("fast", buffer=96, n=70, seed=4)
+        b = steady_state_tracker("fast", buffer=96, n=70, seed=4)
+        w, t = torch.rand_like(a.pg.weight), torch.rand_like(a.pg.target)
+        for s in (a, b):
+            s.cfg.KEYFRAME_THRESH = 1e9 if drop else -1.0
+            s.pg.weight, s.pg.target = w.clone(), t.clone()
+        a.keyframe()
+        _reference_keyframe(b)
+    assert a.n == b.n and a.pg.m == b.pg.m
+    for name in ("ii", "jj", "kk", "net", "weight", "target", "ii_inac", "jj_inac", "kk_inac", "weight_inac",
+                 "target_inac"):
+        assert torch.equal(getattr(a.pg, name), getattr(b.pg, name)), name
+    for name in ("poses_", "patches_", "intrinsics_", "colors_", "patches_est_"):
+        assert torch.equal(getattr(a.pg, name), getattr(b.pg, name)), name
+    assert np.array_equal(a.pg.tstamps_, b.pg.tstamps_)
+    for name in ("imap_", "gmap_", "fmap1_", "fmap2_", "image_buffer_"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert a.pg.delta.keys() == b.pg.delta.keys()

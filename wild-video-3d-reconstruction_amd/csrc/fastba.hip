@@ -759,8 +759,9 @@ __device__ __forceinline__ double readlane_d(double v, int lane)
 // which factors the float32 S with torch::linalg::cholesky (ba_cuda.cu:518-521).
 // A single wave has no partner to hide latency behind, so the short fp32
 // sqrt / div chains (vs fp64) are what sets this kernel's time.  (Measured
-// alternative: v_readlane broadcasts instead of LDS -- no waits, but ~14k
-// instructions through one wave's issue slot: no faster.)
+// alternatives, both no faster: v_readlane broadcasts instead of LDS -- no
+// waits, but ~14k instructions through one wave's issue slot; four waves with
+// 4 x 4 register blocks -- two barriers per column cost what they save.)
 __device__ __forceinline__ void wave_lds_fence()
 {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

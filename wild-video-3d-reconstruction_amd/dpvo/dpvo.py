@@ -209,14 +209,19 @@ class DPVO:
         self.pg.net = torch.cat([self.pg.net, torch.zeros(1, len(kk), self.DIM, **self.kwargs)], dim=1)
 
     def remove_factors(self, m, store: bool):
+        """Boolean-mask compaction of the edge state (dpvo.py:349-364).  Each
+        ``x[mask]`` is a host synchronisation (the output size); here the mask
+        becomes an index once (one sync per side) and every tensor is
+        gathered with it."""
         assert self.pg.ii.numel() == self.pg.weight.shape[1]
         if store:
-            self.pg.ii_inac = torch.cat((self.pg.ii_inac, self.pg.ii[m]))
-            self.pg.jj_inac = torch.cat((self.pg.jj_inac, self.pg.jj[m]))
-            self.pg.kk_inac = torch.cat((self.pg.kk_inac, self.pg.kk[m]))
-            self.pg.weight_inac = torch.cat((self.pg.weight_inac, self.pg.weight[:, m]), dim=1)
-            self.pg.target_inac = torch.cat((self.pg.target_inac, self.pg.target[:, m]), dim=1)
-        keep = ~m
+            rem = torch.nonzero(m).squeeze(1)
+            self.pg.ii_inac = torch.cat((self.pg.ii_inac, self.pg.ii[rem]))
+            self.pg.jj_inac = torch.cat((self.pg.jj_inac, self.pg.jj[rem]))
+            self.pg.kk_inac = torch.cat((self.pg.kk_inac, self.pg.kk[rem]))
+            self.pg.weight_inac = torch.cat((self.pg.weight_inac, self.pg.weight[:, rem]), dim=1)
+            self.pg.target_inac = torch.cat((self.pg.target_inac, self.pg.target[:, rem]), dim=1)
+        keep = torch.nonzero(~m).squeeze(1)
         self.pg.weight = self.pg.weight[:, keep]
         self.pg.target = self.pg.target[:, keep]
         self.pg.ii, self.pg.jj, self.pg.kk = self.pg.ii[keep], self.pg.jj[keep], self.pg.kk[keep]
@@ -236,10 +241,14 @@ class DPVO:
         return torch.quantile(delta.norm(dim=-1).float(), 0.5)
 
     def motionmag(self, i, j):
-        k = (self.pg.ii == i) & (self.pg.jj == j)
+        return self._motionmag_dev(i, j).item()
+
+    def _motionmag_dev(self, i, j):
+        """mean flow of the (i -> j) edges (dpvo.py:507-514), left on the device."""
+        k = torch.nonzero((self.pg.ii == i) & (self.pg.jj == j)).squeeze(1)
         flow = pops.flow_mag(SE3(self.poses), self.patches, self.intrinsics, self.pg.ii[k], self.pg.jj[k],
                              self.pg.kk[k], beta=0.5)
-        return flow.mean().item()
+        return flow.mean()
 
     def update(self):
         """One keyframe of the hot loop (dpvo.py:711-749)."""
@@ -268,26 +277,34 @@ class DPVO:
         """drop a redundant keyframe, retire old edges (dpvo.py:605-658)."""
         k = self.n - self.cfg.KEYFRAME_INDEX
         i, j = k - 1, k + 1
-        m = self.motionmag(i, j) + self.motionmag(j, i)
+        # one host read for both directions (the reference reads each, :609)
+        m = (self._motionmag_dev(i, j) + self._motionmag_dev(j, i)).item()
         if m / 2 < self.cfg.KEYFRAME_THRESH:
-            t0, t1 = self.pg.tstamps_[k - 1].item(), self.pg.tstamps_[k].item()
+            t0, t1 = self.pg.tstamps_[k - 1:k + 1].tolist()
             dP = SE3(self.pg.poses_[k]) * SE3(self.pg.poses_[k - 1]).inv()
             self.pg.delta[t1] = (t0, dP)
             self.remove_factors((self.pg.ii == k) | (self.pg.jj == k), store=False)
-            self.pg.kk[self.pg.ii > k] -= self.M
-            self.pg.ii[self.pg.ii > k] -= 1
-            self.pg.jj[self.pg.jj > k] -= 1
-            for f in range(k, self.n - 1):
-                g = f + 1
-                self.pg.tstamps_[f] = self.pg.tstamps_[g]
+            # x[x > k] -= 1 as selects: no mask-size synchronisation
+            later = self.pg.ii > k
+            self.pg.kk = torch.where(later, self.pg.kk - self.M, self.pg.kk)
+            self.pg.ii = torch.where(later, self.pg.ii - 1, self.pg.ii)
+            self.pg.jj = torch.where(self.pg.jj > k, self.pg.jj - 1, self.pg.jj)
+            # frames k+1 .. n-1 move down by one: one gather per buffer (the
+            # reference's per-frame loop, :626-639, reads each source before
+            # overwriting it, so a simultaneous shift is the same)
+            n = self.n
+            if n - 1 > k:
+                self.pg.tstamps_[k:n - 1] = self.pg.tstamps_[k + 1:n].copy()
                 for buf in (self.pg.colors_, self.pg.poses_, self.pg.patches_, self.pg.patches_est_,
                             self.pg.intrinsics_):
-                    buf[f] = buf[g]
-                self.imap_[f % self.pmem] = self.imap_[g % self.pmem]
-                self.gmap_[f % self.pmem] = self.gmap_[g % self.pmem]
-                self.fmap1_[0, f % self.pmem] = self.fmap1_[0, g % self.pmem]
-                self.fmap2_[0, f % self.pmem] = self.fmap2_[0, g % self.pmem]
-                self.image_buffer_[f % self.mem] = self.image_buffer_[g % self.mem]
+                    buf[k:n - 1] = buf[k + 1:n].clone()
+                dst = torch.arange(k, n - 1, device=self.device)
+                src = dst + 1
+                for ring, size in ((self.imap_, self.pmem), (self.gmap_, self.pmem)):
+                    ring[dst % size] = ring[src % size]
+                for ring in (self.fmap1_, self.fmap2_):
+                    ring[0, dst % self.pmem] = ring[0, src % self.pmem]
+                self.image_buffer_[dst % self.mem] = self.image_buffer_[src % self.mem]
             self.n -= 1
             self.pg.m -= self.M
         elif torch.isnan(self.pg.poses_[k]).any():
