@@ -284,6 +284,14 @@ typedef struct dpvo_rowgemm_args {
 } dpvo_rowgemm_args;
 int dpvo_rowgemm(const dpvo_rowgemm_args* args, void* stream);
 
+/* Two chained rowgemms, Y = epi2(act1(A W1^T + b1) W2^T + b2), with the 384-wide
+ * intermediate kept on chip (the update operator's Linear -> ReLU -> Linear
+ * pairs).  g1: A, lda, a_idx, a_rows, W (K1 % 32 == 0), bias, zero_row, M,
+ * M_dev and flags (DPVO_RG_RELU / DPVO_RG_SIGMOID only); its outputs are not
+ * written.  g2: W ([384][384]), bias, flags and every epilogue input / output
+ * of dpvo_rowgemm (its A, M and M_dev are taken from g1). */
+int dpvo_rowchain(const dpvo_rowgemm_args* first, const dpvo_rowgemm_args* second, void* stream);
+
 /* Row add + LayerNorm over 384-wide rows (one pass):
  *   v = a[m] (+ b16[b_idx[m]])  [-> LayerNorm]  -> out32 [M][384] / out16 [M][384]
  * a is fp16 (a_f16=1) or fp32 with row stride lda; b_idx[m] < 0 adds nothing.

@@ -734,6 +734,212 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_ar
     }
 }
 
+// ---------------------------------------------------------------------------
+// Chained pair: Y = epi2(act1(A W1^T + b1) W2^T + b2) with the 128 x 384
+// intermediate kept in LDS -- the update operator's Linear -> ReLU -> Linear
+// pairs (corr0/corr1, c1, c2, the GRU res branches; net.py:53-56,
+// blocks.py:27-30), whose 73 MB intermediates otherwise round-trip HBM.
+// LDS: the y tile (96 KB; GEMM2's A operand, then its output for the row
+// epilogue) + two 32 KB stages (BK = 32: A 8 KB | W 24 KB for GEMM1, W only
+// for GEMM2).  Transposed accumulators as in v3.
+// ---------------------------------------------------------------------------
+constexpr int RC_BK = 32;
+constexpr int RC_A_STAGE = RG_BM * RC_BK * 2;      // 8 KB
+constexpr int RC_W_STAGE = RG_BN * RC_BK * 2;      // 24 KB
+constexpr int RC_STAGE = RC_A_STAGE + RC_W_STAGE;  // 32 KB
+constexpr int RC_Y = RG_BM * 768;                  // 96 KB
+constexpr int RC_LDS = RC_Y + 2 * RC_STAGE;        // 160 KB
+
+struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflict-free
+    // ds_read_b128 fragment reads down 16 rows and 256-byte row sweeps
+    __device__ int off(int r, int byte) const { return r * 768 + (((byte >> 4) ^ (r & 15)) << 4) + (byte & 15); }
+};
+
+template <int F2>
+__global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p)
+{
+    __shared__ __attribute__((aligned(16))) char smem[RC_LDS];
+    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int K1 = p1.K, ks1 = K1 / RC_BK, ks2 = RG_BN / RC_BK;
+    const int64_t Mrows = p1.M_dev ? min(*p1.M_dev, p1.M) : p1.M;
+    const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
+    if ((int64_t)blockIdx.x >= ntiles) return;
+    const half_t* __restrict__ W1 = (const half_t*)p1.W;
+    const half_t* __restrict__ W2 = (const half_t*)p.W;
+    const half_t* __restrict__ zero = (const half_t*)p1.zero_row;
+    const YMapChunk ym;
+    // piece (1 KB = 16 rows x 64 B) lane mapping: row base + L/4, physical chunk
+    // L%4 holding logical chunk (L%4) ^ ((row>>2)&3)
+    const int srow = lane >> 2, pch = lane & 3;
+    // GEMM1 stage: pieces 4 wave .. 4 wave + 3 of 32 (0-7 A rows, 8-31 W1 rows)
+    const half_t* g1src[4];
+    auto set_tile = [&](int64_t tile) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int pc = 4 * wave + j;
+            if (pc < 8) {
+                const int r = pc * 16 + srow;
+                const int64_t m = tile * RG_BM + r;
+                const half_t* row = zero;
+                if (m < Mrows) {
+                    const int64_t s = p1.a_idx ? p1.a_idx[m] : m;
+                    if (s >= 0 && s < p1.a_rows) row = (const half_t*)p1.A + s * p1.lda;
+                }
+                g1src[j] = row + 8 * (pch ^ ((r >> 2) & 3));
+            }
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int pc = 4 * wave + j;   // A pieces then W pieces, contiguous within the stage
+        if (pc >= 8) {
+            const int n = (pc - 8) * 16 + srow;
+            g1src[j] = W1 + (int64_t)n * K1 + 8 * (pch ^ ((n >> 2) & 3));
+        }
+    }
+    // GEMM2 stage: W2 pieces 3 wave .. 3 wave + 2 of 24
+    const half_t* w2src[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const int n = (3 * wave + j) * 16 + srow;
+        w2src[j] = W2 + (int64_t)n * RG_BN + 8 * (pch ^ ((n >> 2) & 3));
+    }
+    auto issue1 = [&](int ks, int buf) {
+        char* st = smem + RC_Y + buf * RC_STAGE;
+        const int k0 = ks * RC_BK;
+#pragma unroll
+        for (int j = 0; j < 4; j++) glds16(g1src[j] + k0, st + (4 * wave + j) * 1024);
+    };
+    auto issue2 = [&](int ks, int buf) {
+        char* st = smem + RC_Y + buf * RC_STAGE + RC_A_STAGE;
+        const int k0 = ks * RC_BK;
+#pragma unroll
+        for (int j = 0; j < 3; j++) glds16(w2src[j] + k0, st + (3 * wave + j) * 1024);
+    };
+    auto sync_lds = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    f4_t acc[4][6];
+    const int fr = lane & 15, fq = lane >> 4;
+    int a_off[4], w_off[6];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++) {
+        const int row = wm * 64 + mt * 16 + fr;
+        a_off[mt] = row * 64 + 16 * (fq ^ ((row >> 2) & 3));
+    }
+#pragma unroll
+    for (int nt = 0; nt < 6; nt++) {
+        const int n = wn * 96 + nt * 16 + fr;
+        w_off[nt] = RC_A_STAGE + n * 64 + 16 * (fq ^ ((n >> 2) & 3));
+    }
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+    };
+    auto mfma_step = [&](const h8_t (&a)[4], const h8_t (&b)[6]) {
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++)
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+    };
+    // acc + bias -> act -> fp16 -> y tile (row mt*16+fr, columns 4 fq.. of block nt)
+    // (called before any stage prefetch is in flight: its bias loads would
+    // otherwise wait behind the prefetch in the in-order vmcnt)
+    auto acc_to_y = [&](const half_t* bias_p, bool relu, bool sigm) {
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) {
+            const int col = wn * 96 + nt * 16 + 4 * fq;
+            const h4_t bias = *(const h4_t*)(bias_p + col);
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) {
+                h4_t y;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    half_t v = (half_t)(acc[mt][nt][r] + (float)bias[r]);
+                    if (relu) v = v > (half_t)0 ? v : (half_t)0;
+                    if (sigm) v = (half_t)fast_sigmoid((float)v);
+                    y[r] = v;
+                }
+                *(h4_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, col * 2)) = y;
+            }
+        }
+    };
+    EpiConsts kc;
+    load_consts<F2>(p, lane, kc);
+
+    int64_t tile = blockIdx.x;
+    set_tile(tile);
+    issue1(0, 0);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const bool more = tile + gridDim.x < ntiles;
+        // ---- GEMM1: A (global, gathered) x W1
+        zero_acc();
+        for (int ks = 0; ks < ks1; ks++) {
+            if (ks + 1 < ks1) {
+                issue1(ks + 1, (ks + 1) & 1);
+                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const char* st = smem + RC_Y + (ks & 1) * RC_STAGE;
+            h8_t a[4], b[6];
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(st + a_off[mt]);
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+            mfma_step(a, b);
+            __builtin_amdgcn_s_barrier();
+        }
+        // ---- intermediate -> y tile; W2's first stage into the released stage 0
+        acc_to_y((const half_t*)p1.bias, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
+        issue2(0, 0);
+        sync_lds();
+        // ---- GEMM2: y tile x W2
+        zero_acc();
+#pragma unroll 1
+        for (int ks = 0; ks < ks2; ks++) {
+            if (ks + 1 < ks2) {
+                issue2(ks + 1, (ks + 1) & 1);
+                asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const char* st = smem + RC_Y + (ks & 1) * RC_STAGE;
+            h8_t a[4], b[6];
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, (ks * 4 + fq) * 16));
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+            mfma_step(a, b);
+            __builtin_amdgcn_s_barrier();
+        }
+        acc_to_y((const half_t*)p.bias, F2 & RG_RELU, F2 & RG_SIGMOID);
+        // ---- the next tile's first GEMM1 stage loads under this epilogue
+        if (more) {
+            set_tile(tile + gridDim.x);
+            issue1(0, 0);
+        }
+        sync_lds();
+        constexpr int RB = (F2 & (RG_RES | RG_GATE | RG_LN)) ? 4 : 8;
+#pragma unroll 1
+        for (int q0 = 0; q0 < 16; q0 += RB)   // one batch live at a time (register budget)
+            epilogue_rows<F2, RB>(p, Mrows, smem, ym, wave * 16 + q0, tile * RG_BM + wave * 16 + q0, lane, kc);
+        sync_lds();
+    }
+}
+
 // v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16   (one wave per row)
 __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
 {
@@ -902,6 +1108,57 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
         RG_CASE(DPVO_RG_GATE)
     default:
         set_error("dpvo_rowgemm: unsupported epilogue flag combination " + std::to_string(f));
+        return -1;
+    }
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_rowchain(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args* g2, void* stream)
+{
+    DPVO_CHECK_ARG(g1 != nullptr && g2 != nullptr, "null args");
+    DPVO_CHECK_ARG(g1->N == RG_BN && g2->N == RG_BN, "rowchain: output widths must be 384");
+    DPVO_CHECK_ARG(g1->K > 0 && g1->K % RC_BK == 0, "rowchain: K1 must be a positive multiple of 32");
+    DPVO_CHECK_ARG(g2->K == RG_BN, "rowchain: the second GEMM's K must be 384 (the intermediate width)");
+    DPVO_CHECK_ARG(g1->A && g1->W && g1->bias && g1->zero_row && g2->W && g2->bias,
+                   "rowchain: A, W1, W2, both biases and zero_row are required");
+    DPVO_CHECK_ARG(g1->lda >= g1->K && g1->lda % 8 == 0, "rowchain: lda must be >= K1 and a multiple of 8");
+    DPVO_CHECK_ARG(((uintptr_t)g1->A & 15) == 0 && ((uintptr_t)g1->W & 15) == 0 && ((uintptr_t)g2->W & 15) == 0 &&
+                       ((uintptr_t)g1->zero_row & 15) == 0,
+                   "rowchain: A, W1, W2 and zero_row must be 16-byte aligned");
+    DPVO_CHECK_ARG(((uintptr_t)g1->bias & 7) == 0 && ((uintptr_t)g2->bias & 7) == 0,
+                   "rowchain: biases must be 8-byte aligned");
+    DPVO_CHECK_ARG((g1->flags & ~(DPVO_RG_RELU | DPVO_RG_SIGMOID)) == 0,
+                   "rowchain: the first GEMM takes only an activation");
+    const int f = g2->flags;
+    DPVO_CHECK_ARG(!((f & DPVO_RG_RES) || (f & DPVO_RG_GATE)) || g2->res32, "rowchain: residual input missing");
+    DPVO_CHECK_ARG(!(f & DPVO_RG_GATE) || g2->gate16, "rowchain: gate input missing");
+    DPVO_CHECK_ARG(!(f & DPVO_RG_LN) || (g2->ln_g && g2->ln_b), "rowchain: LayerNorm weights missing");
+    DPVO_CHECK_ARG(!(f & DPVO_RG_HEADS) || (g2->head_w && g2->head_b && g2->head_out), "rowchain: head weights missing");
+    if (g1->M <= 0) return 0;
+    if (g_num_cus == 0) {
+        int dev = 0;
+        DPVO_CHECK_HIP(hipGetDevice(&dev));
+        DPVO_CHECK_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+        if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    const int64_t ntiles = (g1->M + RG_BM - 1) / RG_BM;
+    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+    dpvo_rowgemm_args a2 = *g2;
+    a2.M = g1->M;
+    a2.M_dev = g1->M_dev;
+    switch (f) {
+#define RCH_CASE(F)                                                                                              \
+    case (F):                                                                                                    \
+        hipLaunchKernelGGL(rowchain_kernel<(F)>, dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *g1, a2); \
+        break;
+        RCH_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
+        RCH_CASE(DPVO_RG_RES)
+        RCH_CASE(DPVO_RG_GATE | DPVO_RG_LN)
+        RCH_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
+#undef RCH_CASE
+    default:
+        set_error("dpvo_rowchain: unsupported epilogue flag combination " + std::to_string(f));
         return -1;
     }
     DPVO_CHECK_LAUNCH();

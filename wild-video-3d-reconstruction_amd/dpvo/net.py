@@ -70,7 +70,8 @@ class Update(nn.Module):
 
     def _forward_fused(self, net, inp, corr, ii, jj, kk, inp_idx=None):
         """The same dataflow as the reference under autocast, in 19 full-row
-        fused GEMMs (csrc/rowgemm.hip) + 2 SoftAggs: every Linear is an fp16
+        fused GEMMs (csrc/rowgemm.hip; 5 Linear->ReLU->Linear pairs chained,
+        14 launches) + 2 SoftAggs: every Linear is an fp16
         GEMM with fp32 accumulate; residual adds, LayerNorms, gating and the
         d/w heads run in fp32 in the GEMM epilogues."""
         U = update_ops
@@ -82,8 +83,8 @@ class Update(nn.Module):
             padded[:, :c.shape[1]] = c
             c = padded
         c0, c1, cln, c2 = pk["corr"]
-        _, h, _ = U.rowgemm(c, *c0, flags=U.RELU)
-        _, h, _ = U.rowgemm(h, *c1, flags=U.LN | U.LN_RELU, ln=cln)
+        # Linear -> ReLU -> Linear pairs run chained, the intermediate in LDS
+        _, h, _ = U.rowchain(c, *c0, *c1, flags1=U.RELU, flags=U.LN | U.LN_RELU, ln=cln)
         # inp rows gathered inside the epilogue when the caller passes the index
         # (DPVO.update: imap[:, kk % (M pmem)], dpvo.py:718) -- no E x 384 copy
         res16, res16_idx = (inp[0], inp_idx) if inp_idx is not None else (inp[0].contiguous(), None)
@@ -94,8 +95,7 @@ class Update(nn.Module):
         kk_groups = U.group_by(kk, key_bits=32)
         ix, jx = U.neighbors_csr(jj, kk_groups[1], kk_groups[2], kk_groups[3], E)
         for (la, lb), nb in ((pk["c1"], ix), (pk["c2"], jx)):
-            _, h, _ = U.rowgemm(n16, *la, flags=U.RELU, a_idx=nb)
-            n32, n16, _ = U.rowgemm(h, *lb, flags=U.RES, res32=n32, want32=True)
+            n32, n16, _ = U.rowchain(n16, *la, *lb, flags1=U.RELU, a_idx=nb, flags=U.RES, res32=n32, want32=True)
         ln0, gr1, ln1, gr2 = pk["gru"]
         for (pf, pg_, ph), key, ln in ((pk["agg_kk"], None, None), (pk["agg_ij"], ii * 12345 + jj, ln0)):
             # unique(key) + CSR on the device (no host sync); G stays on the device
@@ -109,13 +109,12 @@ class Update(nn.Module):
         for gr, last in ((gr1, False), (gr2, True)):
             pgate, pr1, pr2 = gr
             _, g16, _ = U.rowgemm(n16, *pgate, flags=U.SIGMOID)
-            _, h, _ = U.rowgemm(n16, *pr1, flags=U.RELU)
             if last:
-                n32, _, heads = U.rowgemm(h, *pr2, flags=U.GATE | U.HEADS, res32=n32, gate16=g16,
-                                          heads=pk["heads"], want32=True, want16=False)
+                n32, _, heads = U.rowchain(n16, *pr1, *pr2, flags1=U.RELU, flags=U.GATE | U.HEADS, res32=n32,
+                                           gate16=g16, heads=pk["heads"], want32=True, want16=False)
             else:
-                n32, n16, _ = U.rowgemm(h, *pr2, flags=U.GATE | U.LN, res32=n32, gate16=g16, ln=ln1,
-                                        want32=True)
+                n32, n16, _ = U.rowchain(n16, *pr1, *pr2, flags1=U.RELU, flags=U.GATE | U.LN, res32=n32,
+                                         gate16=g16, ln=ln1, want32=True)
         return n32[None], (heads[None, :, :2], heads[None, :, 2:], None)
 
     def forward(self, net, inp, corr, flow, ii, jj, kk, inp_idx=None):

@@ -67,6 +67,63 @@ def softagg_csr(f, s, offs, perm, groups, max_groups, eps=1e-12):
     return y
 
 
+def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=None, res16=None, res16_idx=None,
+             gate16=None, ln=None, heads=None, want32=False, want16=True, M_dev=None):
+    """rowgemm(rowgemm(A, W1, b1, flags1, a_idx).y16, W2, b2, flags, ...) in one
+    launch, the 384-wide intermediate kept on chip (dpvo_rowchain).
+    Returns (out32, out16, head_out) of the second GEMM."""
+    H.on_gpu(A, W1, b1, W2, b2)
+    if flags1 is None:
+        flags1 = RELU
+    if any(t.dtype != torch.float16 for t in (A, W1, b1, W2, b2)):
+        raise RuntimeError("rowchain: A, weights and biases must be fp16")
+    if A.dim() != 2 or A.stride(1) != 1 or W1.shape[0] != WIDTH or not W1.is_contiguous():
+        raise RuntimeError("rowchain: A must be [rows, K] row-contiguous and W1 [384, Kp] contiguous")
+    if tuple(W2.shape) != (WIDTH, WIDTH) or not W2.is_contiguous():
+        raise RuntimeError("rowchain: W2 must be a contiguous [384, 384]")
+    Kp = W1.shape[1]
+    if A.stride(0) < Kp:
+        raise RuntimeError(f"rowchain: A's row stride {A.stride(0)} < padded K {Kp}")
+    dev = A.device
+    if a_idx is not None:
+        a_idx = H.idx64(a_idx)
+        M = a_idx.numel()
+    elif M is None:
+        M = A.shape[0]
+    out32 = torch.empty(M, WIDTH, dtype=torch.float32, device=dev) if want32 else None
+    out16 = torch.empty(M, WIDTH, dtype=torch.float16, device=dev) if want16 else None
+    head_out = torch.empty(M, 4, dtype=torch.float16, device=dev) if heads is not None else None
+    if res16_idx is not None:
+        res16_idx = H.idx64(res16_idx)
+    g1 = RowGemmArgs()
+    g1.A, g1.lda, g1.a_idx, g1.a_rows = _p(A), A.stride(0), _p(a_idx), A.shape[0]
+    g1.W, g1.K, g1.N, g1.bias, g1.zero_row = _p(W1), Kp, WIDTH, _p(b1), _p(zero_row(dev, Kp))
+    g1.M, g1.flags = M, int(flags1)
+    if M_dev is not None:
+        if M_dev.dtype != torch.int64 or not M_dev.is_cuda:
+            raise RuntimeError("rowchain: M_dev must be a device int64 scalar")
+        g1.M_dev = M_dev.data_ptr()
+    g2 = RowGemmArgs()
+    g2.W, g2.K, g2.N, g2.bias = _p(W2), WIDTH, WIDTH, _p(b2)
+    g2.res32, g2.ldr = _p(res32), (res32.stride(0) if res32 is not None else 0)
+    g2.res16, g2.res16_idx, g2.gate16 = _p(res16), _p(res16_idx), _p(gate16)
+    if ln is not None:
+        g2.ln_g, g2.ln_b, g2.ln_eps = _p(ln[0]), _p(ln[1]), float(ln[2])
+    if heads is not None:
+        g2.head_w, g2.head_b, g2.head_out = _p(heads[0]), _p(heads[1]), _p(head_out)
+    g2.out32, g2.ldo32 = _p(out32), (out32.stride(0) if out32 is not None else 0)
+    g2.out16, g2.ldo16 = _p(out16), (out16.stride(0) if out16 is not None else 0)
+    g2.flags = int(flags)
+    for t, nm in ((res32, "res32"), (out32, "out32")):
+        if t is not None and (t.dtype != torch.float32 or t.stride(1) != 1):
+            raise RuntimeError(f"rowchain: {nm} must be fp32 with contiguous rows")
+    for t, nm in ((res16, "res16"), (gate16, "gate16")):
+        if t is not None and (t.dtype != torch.float16 or not t.is_contiguous() or t.shape[-1] != WIDTH):
+            raise RuntimeError(f"rowchain: {nm} must be contiguous fp16 [*, 384]")
+    H.check(H.lib().dpvo_rowchain(_ct.byref(g1), _ct.byref(g2), H.stream_of(A)))
+    return out32, out16, head_out
+
+
 def neighbors_csr(jj, offs, perm, groups, max_groups):
     """cuda_ba.neighbors(kk, jj) from the CSR of group_by(kk): -> (ix, jx) int64,
     the previous / next edge of the same patch in (jj, edge) order, -1 at the
