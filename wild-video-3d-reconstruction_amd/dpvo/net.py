@@ -153,6 +153,10 @@ class Patchifier(nn.Module):
         self.patch_size = patch_size
         self.fnet = BasicEncoder4(output_dim=128, norm_fn="instance")
         self.inet = BasicEncoder4(output_dim=DIM, norm_fn="none")
+        # inference ingest from one captured HIP graph (see _forward_graphed);
+        # False = the eager launches
+        self.graphed = True
+        self._graph = self._graph_key = None
 
     def _image_gradient(self, images):
         gray = ((images + 0.5) * (255.0 / 2)).sum(dim=2)
@@ -165,11 +169,14 @@ class Patchifier(nn.Module):
         """image [3,H,W] uint8 -> fmap, gmap, imap, patches, index[, colours] (net.py:260-325)."""
         if sp_extractor is not None:
             raise NotImplementedError("SuperPoint keypoints are out of scope")
+        if (self.graphed and not gradient_bias and mask is None and disps is None and images.is_cuda and images.dim() == 3
+                and not torch.is_grad_enabled()):
+            return self._forward_graphed(images, patches_per_image, return_color)
         images = 2 * (images[None, None] / 255.0) - 0.5
         fmap = self.fnet(images) / 4.0
         imap = self.inet(images) / 4.0
         b, n, c, h, w = fmap.shape
-        P, dev = self.patch_size, images.device
+        dev = images.device
 
         if gradient_bias:
             g = self._image_gradient(images)
@@ -187,19 +194,73 @@ class Patchifier(nn.Module):
         else:
             x = torch.randint(1, w - 1, size=[n, patches_per_image], device=dev)
             y = torch.randint(1, h - 1, size=[n, patches_per_image], device=dev)
+        gmap, imap, patches, clr = self._gather(images, fmap, imap, x, y, disps, return_color)
+        index = torch.arange(n, device=dev).view(n, 1).repeat(1, patches_per_image).reshape(-1)
+        if return_color:
+            return fmap, gmap, imap, patches, index, clr
+        return fmap, gmap, imap, patches, index
 
+    def _gather(self, images, fmap, imap, x, y, disps, return_color):
+        """the four altcorr.patchify gathers at the chosen centres (net.py:301-315)."""
+        b, n, c, h, w = fmap.shape
+        P = self.patch_size
         coords = torch.stack([x, y], dim=-1).float()
         imap = altcorr.patchify(imap[0], coords, 0).view(b, -1, DIM, 1, 1)
         gmap = altcorr.patchify(fmap[0], coords, P // 2).view(b, -1, 128, P, P)
         clr = altcorr.patchify(images[0], 4 * (coords + 0.5), 0).view(b, -1, 3) if return_color else None
         if disps is None:
-            disps = torch.ones(b, n, h, w, device=dev)
+            disps = torch.ones(b, n, h, w, device=images.device)
         grid, _ = coords_grid_with_index(disps, device=fmap.device)
         patches = altcorr.patchify(grid[0], coords, P // 2).view(b, -1, 3, P, P)
-        index = torch.arange(n, device=dev).view(n, 1).repeat(1, patches_per_image).reshape(-1)
+        return gmap, imap, patches, clr
+
+    def _ingest(self, image, x, y, return_color):
+        """forward() after the centre draw: fixed shapes, no host syncs -- the
+        body of the captured graph."""
+        images = 2 * (image[None, None] / 255.0) - 0.5
+        fmap = self.fnet(images) / 4.0
+        imap = self.inet(images) / 4.0
+        return (fmap,) + self._gather(images, fmap, imap, x, y, None, return_color)
+
+    def _forward_graphed(self, image, M, return_color):
+        """forward() with the ~300 encoder / patchify launches replayed from
+        one HIP graph.  The patch centres are drawn eagerly with the same
+        randint calls, in the same order, as the eager path (the encoders draw
+        no random numbers), so the results are identical to forward()'s; the
+        graph reads them from static buffers.  Outputs are returned as clones:
+        the next replay overwrites the graph's own."""
+        H, W = image.shape[-2:]
+        h, w = ((H + 1) // 2 + 1) // 2, ((W + 1) // 2 + 1) // 2  # conv1 (s2) then layer2 (s2)
+        dev = image.device
+        x = torch.randint(1, w - 1, size=[1, M], device=dev)
+        y = torch.randint(1, h - 1, size=[1, M], device=dev)
+        amp = torch.is_autocast_enabled("cuda")
+        key = (tuple(image.shape), image.dtype, M, bool(return_color), amp, dev)
+        if self._graph_key != key:
+            self._capture(image, x, y, return_color, amp, key)
+        self._g_in[0].copy_(image)
+        self._g_in[1].copy_(x)
+        self._g_in[2].copy_(y)
+        self._graph.replay()
+        fmap, gmap, imap, patches, clr = (t.clone() if t is not None else None for t in self._g_out)
+        index = torch.zeros(M, dtype=torch.long, device=dev)
         if return_color:
             return fmap, gmap, imap, patches, index, clr
         return fmap, gmap, imap, patches, index
+
+    def _capture(self, image, x, y, return_color, amp, key):
+        self._graph = self._graph_key = None
+        static = (image.clone(), x.clone(), y.clone())
+        side = torch.cuda.Stream(device=image.device)
+        side.wait_stream(torch.cuda.current_stream(image.device))
+        with torch.cuda.stream(side), torch.autocast("cuda", enabled=amp, cache_enabled=False):
+            for _ in range(2):  # warm-up: MIOpen solver selection, allocator pools
+                self._ingest(*static, return_color)
+        torch.cuda.current_stream(image.device).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph), torch.autocast("cuda", enabled=amp, cache_enabled=False):
+            out = self._ingest(*static, return_color)
+        self._graph, self._graph_key, self._g_in, self._g_out = graph, key, static, out
 
 
 class VONet(nn.Module):
