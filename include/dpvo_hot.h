@@ -195,6 +195,15 @@ int dpvo_transform(const float* poses, const float* patches, int P, const float*
                    const int64_t* jj, const int64_t* kk, int64_t num_edges, int flags, float* coords, float* valid,
                    void* stream);
 
+/* DPVO.motionmag (dpvo.py:507-514) of both directions keyframe() compares
+ * (dpvo.py:609): out[0] = mean flow_mag (projective_ops.py:111-121, weight
+ * beta) over the edges with (ii, jj) == (i, j) and their P*P pixels,
+ * out[1] = the same for (j, i); NaN for a direction without edges.  out is a
+ * 2-float device buffer; no host synchronisation. */
+int dpvo_motion_mag(const float* poses, const float* patches, int P, const float* intrinsics, const int64_t* ii,
+                    const int64_t* jj, const int64_t* kk, int64_t num_edges, int64_t i, int64_t j, float beta,
+                    float* out, void* stream);
+
 /* projective_ops.point_cloud (projective_ops.py:106-108) of patches[0..m):
  * centre_only=1 -> out [m][3] = xyz/w of the centre pixel (what
  * DPVO.update stores in pg.points_, dpvo.py:747-749); else out [m][P][P][4]. */

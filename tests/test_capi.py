@@ -28,7 +28,7 @@ def test_header_declares_the_expected_surface():
     names = declared()
     for must in ["dpvo_corr_forward", "dpvo_corr_forward_pyramid", "dpvo_corr_backward", "dpvo_patchify_forward",
                  "dpvo_patchify_backward", "dpvo_ba_forward", "dpvo_ba_workspace_bytes", "dpvo_reproject",
-                 "dpvo_neighbors", "dpvo_lie_forward", "dpvo_lie_backward", "dpvo_transform", "dpvo_point_cloud"]:
+                 "dpvo_neighbors", "dpvo_lie_forward", "dpvo_lie_backward", "dpvo_transform", "dpvo_point_cloud", "dpvo_motion_mag"]:
         assert must in names
 
 

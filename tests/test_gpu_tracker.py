@@ -191,3 +191,38 @@ def test_graphed_ingest_matches_eager():
             assert a.shape == b.shape and a.dtype == b.dtype
             assert torch.equal(a, b)
     assert not torch.equal(graphed[0][3], graphed[1][3])  # fresh centres, not aliased outputs
+
+
+def test_motion_mag_matches_oracle(slam):
+    """DPVO.motionmag (dpvo.py:507-514) as one native launch for both
+    directions == the oracle's transform-based flow_mag (projective_ops.py:
+    111-121) averaged over the matching edges; NaN without edges."""
+    from dpvo import projective_ops as pops
+    from dpvo.lietorch import SE3
+    poses = slam.pg.poses_.cpu().numpy()
+    patches = slam.pg.patches_.view(-1, 3, 3, 3).cpu().numpy()
+    intr = slam.pg.intrinsics_.cpu().numpy()
+    ii, jj, kk = (t.cpu().numpy() for t in (slam.pg.ii, slam.pg.jj, slam.pg.kk))
+
+    def ref(i, j, beta=0.5):
+        s = (ii == i) & (jj == j)
+        if not s.any():
+            return float("nan")
+        c0 = oracle.transform(poses, patches, intr, ii[s], ii[s], kk[s])
+        c1 = oracle.transform(poses, patches, intr, ii[s], jj[s], kk[s])
+        c2 = oracle.transform(poses, patches, intr, ii[s], jj[s], kk[s], tonly=True)
+        f = beta * np.linalg.norm(c1 - c0, axis=-1) + (1 - beta) * np.linalg.norm(c2 - c0, axis=-1)
+        return float(f.mean())
+
+    n = slam.n
+    with torch.no_grad():
+        for i, j in ((n - 5, n - 3), (n - 2, n - 1), (n - 12, n - 1), (0, n - 1)):
+            got = pops.motion_mag_pair(SE3(slam.poses), slam.patches, slam.intrinsics, slam.pg.ii, slam.pg.jj,
+                                       slam.pg.kk, i, j).tolist()
+            for g, w in zip(got, (ref(i, j), ref(j, i))):
+                if np.isnan(w):
+                    assert np.isnan(g)
+                else:
+                    assert abs(g - w) <= 1e-4 * max(1.0, abs(w)), (i, j, g, w)
+        # the tracker's single-direction accessor agrees with the pair
+        assert abs(slam.motionmag(n - 5, n - 3) - ref(n - 5, n - 3)) <= 1e-4 * max(1.0, ref(n - 5, n - 3))

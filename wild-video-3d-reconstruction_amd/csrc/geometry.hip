@@ -81,6 +81,69 @@ __global__ __launch_bounds__(256) void point_cloud_kernel(const float* poses, co
     }
 }
 
+// transform_kernel's per-pixel projection (iproj -> act4 -> proj, Z >= 0.1)
+__device__ __forceinline__ void project_px(const G3& g, const float* ki, const float* kj, const float* pa,
+                                           int64_t PP, int64_t q, float& x, float& y)
+{
+    const float X0[4] = {(pa[q] - ki[2]) / ki[0], (pa[PP + q] - ki[3]) / ki[1], 1.0f, pa[2 * PP + q]};
+    float X1[4];
+    g.act4(X0, X1);
+    const float d = 1.0f / fmaxf(X1[2], 0.1f);
+    x = kj[0] * (d * X1[0]) + kj[2];
+    y = kj[1] * (d * X1[1]) + kj[3];
+}
+
+// DPVO.motionmag (dpvo.py:507-514) for the two directions keyframe() reads
+// (i -> j and j -> i, :609): mean over the matching edges and their P*P
+// pixels of flow_mag (projective_ops.py:111-121) = beta |x(Gij) - x(Gii)| +
+// (1 - beta) |x(t-only Gij) - x(Gii)|.  One workgroup scans the edge list
+// (no mask -> index -> gather round trip, no host sync for the match count),
+// per-thread partial sums are reduced in a fixed tree order (deterministic).
+// out[d] = NaN when direction d has no edge (torch's mean of an empty tensor).
+constexpr int MM_THREADS = 1024;
+__global__ __launch_bounds__(MM_THREADS) void motion_mag_kernel(const float* poses, const float* patches, int P,
+                                                               const float* intr, const int64_t* ii,
+                                                               const int64_t* jj, const int64_t* kk, int64_t E,
+                                                               int64_t fi, int64_t fj, float beta, float* out)
+{
+    __shared__ float s_sum[2][MM_THREADS];
+    __shared__ int s_cnt[2][MM_THREADS];
+    const int t = threadIdx.x;
+    const int64_t PP = (int64_t)P * P;
+    float sum[2] = {0.f, 0.f};
+    int cnt[2] = {0, 0};
+    for (int64_t e = t; e < E; e += MM_THREADS) {
+        const int64_t a = ii[e], b = jj[e];
+        const int dir = (a == fi && b == fj) ? 0 : (a == fj && b == fi) ? 1 : -1;
+        if (dir < 0) continue;
+        const G3 Pa = G3::load(poses + a * 7), Pb = G3::load(poses + b * 7);
+        const G3 g0 = Pa.mul(Pa.inv());
+        const G3 g1 = Pb.mul(Pa.inv());
+        G3 g2 = g1;
+        g2.so3.q.x = 0.f; g2.so3.q.y = 0.f; g2.so3.q.z = 0.f; g2.so3.q.w = 1.f;
+        const float *ka = intr + a * 4, *kb = intr + b * 4;
+        const float* pa = patches + kk[e] * 3 * PP;
+        for (int64_t q = 0; q < PP; q++) {
+            float x0, y0, x1, y1, x2, y2;
+            project_px(g0, ka, ka, pa, PP, q, x0, y0);
+            project_px(g1, ka, kb, pa, PP, q, x1, y1);
+            project_px(g2, ka, kb, pa, PP, q, x2, y2);
+            const float f1 = sqrtf((x1 - x0) * (x1 - x0) + (y1 - y0) * (y1 - y0));
+            const float f2 = sqrtf((x2 - x0) * (x2 - x0) + (y2 - y0) * (y2 - y0));
+            sum[dir] += beta * f1 + (1.0f - beta) * f2;
+        }
+        cnt[dir]++;
+    }
+    for (int d = 0; d < 2; d++) { s_sum[d][t] = sum[d]; s_cnt[d][t] = cnt[d]; }
+    __syncthreads();
+    for (int w = MM_THREADS / 2; w > 0; w >>= 1) {
+        if (t < w)
+            for (int d = 0; d < 2; d++) { s_sum[d][t] += s_sum[d][t + w]; s_cnt[d][t] += s_cnt[d][t + w]; }
+        __syncthreads();
+    }
+    if (t < 2) out[t] = s_cnt[t][0] ? s_sum[t][0] / (float)((int64_t)s_cnt[t][0] * PP) : __builtin_nanf("");
+}
+
 }  // namespace dpvo
 
 using namespace dpvo;
@@ -109,6 +172,19 @@ extern "C" int dpvo_point_cloud(const float* poses, const float* patches, int P,
     DPVO_CHECK_ARG(poses && patches && intrinsics && ix && out, "null operand");
     hipLaunchKernelGGL(point_cloud_kernel, dim3(grid_for(m, 256)), dim3(256), 0, as_stream(stream), poses, patches,
                        P, intrinsics, ix, m, centre_only, out);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_motion_mag(const float* poses, const float* patches, int P, const float* intrinsics,
+                               const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t num_edges, int64_t i,
+                               int64_t j, float beta, float* out, void* stream)
+{
+    DPVO_CHECK_ARG(P >= 1, "bad patch size");
+    DPVO_CHECK_ARG(num_edges >= 0, "negative edge count");
+    DPVO_CHECK_ARG(out && (num_edges == 0 || (poses && patches && intrinsics && ii && jj && kk)), "null operand");
+    hipLaunchKernelGGL(motion_mag_kernel, dim3(1), dim3(MM_THREADS), 0, as_stream(stream), poses, patches, P,
+                       intrinsics, ii, jj, kk, num_edges, i, j, beta, out);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

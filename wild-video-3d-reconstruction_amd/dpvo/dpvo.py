@@ -241,14 +241,13 @@ class DPVO:
         return torch.quantile(delta.norm(dim=-1).float(), 0.5)
 
     def motionmag(self, i, j):
-        return self._motionmag_dev(i, j).item()
+        return self._motionmag_dev(i, j)[0].item()
 
     def _motionmag_dev(self, i, j):
-        """mean flow of the (i -> j) edges (dpvo.py:507-514), left on the device."""
-        k = torch.nonzero((self.pg.ii == i) & (self.pg.jj == j)).squeeze(1)
-        flow = pops.flow_mag(SE3(self.poses), self.patches, self.intrinsics, self.pg.ii[k], self.pg.jj[k],
-                             self.pg.kk[k], beta=0.5)
-        return flow.mean()
+        """[mean flow of the (i -> j) edges, of the (j -> i) edges]
+        (dpvo.py:507-514), one native launch, left on the device."""
+        return pops.motion_mag_pair(SE3(self.poses), self.patches, self.intrinsics, self.pg.ii, self.pg.jj,
+                                    self.pg.kk, i, j, beta=0.5)
 
     def update(self):
         """One keyframe of the hot loop (dpvo.py:711-749)."""
@@ -278,7 +277,7 @@ class DPVO:
         k = self.n - self.cfg.KEYFRAME_INDEX
         i, j = k - 1, k + 1
         # one host read for both directions (the reference reads each, :609)
-        m = (self._motionmag_dev(i, j) + self._motionmag_dev(j, i)).item()
+        m = sum(self._motionmag_dev(i, j).tolist())
         if m / 2 < self.cfg.KEYFRAME_THRESH:
             t0, t1 = self.pg.tstamps_[k - 1:k + 1].tolist()
             dP = SE3(self.pg.poses_[k]) * SE3(self.pg.poses_[k - 1]).inv()

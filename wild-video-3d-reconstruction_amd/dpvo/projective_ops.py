@@ -66,6 +66,20 @@ def transform_fused(poses, patches, intrinsics, ii, jj, kk, depth=False, valid=F
     return (out, v) if valid else out
 
 
+def motion_mag_pair(poses, patches, intrinsics, ii, jj, kk, i, j, beta=0.5):
+    """[mean flow_mag over the (i -> j) edges, same for (j -> i)] as a 2-float
+    device tensor, one launch and no host sync (dpvo.py:507-514 + :609;
+    NaN for a direction without edges, as torch's mean of an empty tensor)."""
+    data = poses.data.contiguous()
+    patches, intrinsics = patches.contiguous(), intrinsics.contiguous()
+    ii, jj, kk = H.idx64(ii), H.idx64(jj), H.idx64(kk)
+    out = torch.empty(2, dtype=torch.float32, device=data.device)
+    H.check(H.lib().dpvo_motion_mag(H.ptr(data), H.ptr(patches), patches.shape[-1], H.ptr(intrinsics), H.ptr(ii),
+                                    H.ptr(jj), H.ptr(kk), ii.numel(), int(i), int(j), float(beta), H.ptr(out),
+                                    H.stream_of(data)))
+    return out
+
+
 def transform(poses, patches, intrinsics, ii, jj, kk, depth=False, valid=False, jacobian=False, tonly=False):
     """Reproject patch kk from frame ii into frame jj (poses are world->camera)."""
     if not jacobian and _fusable(poses, patches, intrinsics):
