@@ -28,6 +28,9 @@
  */
 #include <math.h>
 #include <stdint.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdlib.h>
 #include <string.h>
 
@@ -127,14 +130,23 @@ int oracle_corr_forward(int mode, const void* fmap1, const int64_t* s1sz, const 
     const int R = radius, D = 2 * radius + 2, Do = D - 1;
     const int64_t B = csz[0], M = csz[1], H = csz[3], W = csz[4];
     const int64_t C = s1sz[2], N1 = s1sz[1], N2 = s2sz[1], H2 = s2sz[3], W2 = s2sz[4];
+    int status = 0;
+    /* edges are independent: OpenMP over (b, m) when built with -fopenmp
+     * (each edge is computed by one thread in the same order either way) */
+#pragma omp parallel
+    {
     double* raw = (double*)malloc(sizeof(double) * D * D);
     uint16_t* rawh = (uint16_t*)malloc(sizeof(uint16_t) * D * D);
-    if (!raw || !rawh) return -1;
-
-    for (int64_t b = 0; b < B; b++)
-    for (int64_t m = 0; m < M; m++)
+    if (!raw || !rawh) {
+#pragma omp atomic write
+        status = -1;
+    }
+#pragma omp for schedule(dynamic, 4)
+    for (int64_t bm = 0; bm < B * M; bm++)
     for (int64_t i0 = 0; i0 < H; i0++)
     for (int64_t j0 = 0; j0 < W; j0++) {
+        const int64_t b = bm / M, m = bm % M;
+        if (!raw || !rawh) continue;
         const int64_t ix = (int32_t)ii[m], jx = (int32_t)jj[m];
         const int valid_idx = ix >= 0 && ix < N1 && jx >= 0 && jx < N2;
         const float x = coords[b * cst[0] + m * cst[1] + 0 * cst[2] + i0 * cst[3] + j0 * cst[4]];
@@ -214,7 +226,27 @@ int oracle_corr_forward(int mode, const void* fmap1, const int64_t* s1sz, const 
     }
     free(raw);
     free(rawh);
-    return 0;
+    }
+    return status;
+}
+
+/* OpenMP threads of the parallel oracle loops (1 = the scalar port) */
+void oracle_set_threads(int n)
+{
+#ifdef _OPENMP
+    omp_set_num_threads(n > 0 ? n : 1);
+#else
+    (void)n;
+#endif
+}
+
+int oracle_max_threads(void)
+{
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
 }
 
 /* ------------------------------------------------------------------ */

@@ -38,6 +38,12 @@ def lib():
     return _lib
 
 
+def set_threads(n):
+    """OpenMP threads of the oracle's parallel loops (the altcorr edge loop);
+    1 = the scalar port."""
+    lib().oracle_set_threads(ctypes.c_int(int(n)))
+
+
 def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
