@@ -32,14 +32,25 @@ C, P, LEVELS = 128, 3, 2
 CORR_BYTES_PER_EDGE = 2 * C * (P * P + 10 * 10 + 9 * 9) + 2 * 2 * 49 * P * P + 4 * 2 * P * P + 8 * 2
 
 
+# BASELINE.json configs that fit one GPU: preset, overrides, buffer, BA iterations
+CONFIGS = {
+    "C3": dict(preset="dpvo_2k", overrides={}, buffer=2048, iterations=2,
+               name="C3 dpvo_2k.yaml"),
+    "C2": dict(preset="default", overrides={"PATCHES_PER_FRAME": 96}, buffer=512, iterations=8,
+               name="C2 default.yaml with M=96 (BASELINE.json)"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--buffer", type=int, default=2048)
-    ap.add_argument("--preset", default="dpvo_2k")
-    ap.add_argument("--iterations", type=int, default=2)
+    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS),
+                    help="C3 (the metric's workload, default) or C2 (512-KF buffer, M=96, 8 BA iterations)")
+    ap.add_argument("--buffer", type=int, default=None)
+    ap.add_argument("--iterations", type=int, default=None)
+    ap.add_argument("--e2e-frames", type=int, default=32, help="end-to-end frames timed after the bench (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-edges", type=int, default=1500)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "altcorr_traffic.json"))
@@ -148,12 +159,75 @@ def phase_breakdown(slam, reps=5):
     return {k: round(float(np.median(v)), 4) for k, v in acc.items()}
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _update_op_cpu_seconds(slam, rows, threads):
+    """The learned update operator (net.py:75-93) on the host: the module's
+    own layers in fp32 on torch's CPU backend with `threads` intra-op
+    threads, over a bounded sample of edge rows (the cost is linear in rows:
+    every layer is row-wise except the two SoftAggs, done here with
+    scatter_reduce over the sample's own groups); scaled to all edges by the
+    caller."""
+    import copy
+    upd = copy.deepcopy(slam.network.update).float().cpu().eval()
+    E = slam.pg.ii.numel()
+    idx = torch.linspace(0, E - 1, rows).long()
+    dev = slam.device
+    net = slam.pg.net[0, idx.to(dev)].float().cpu()
+    ctx = slam.imap[0, (slam.pg.kk[idx.to(dev)] % (slam.M * slam.pmem))].float().cpu()
+    corr = torch.randn(rows, 882)
+    kk = slam.pg.kk[idx.to(dev)].cpu()
+    ii, jj = slam.pg.ii[idx.to(dev)].cpu(), slam.pg.jj[idx.to(dev)].cpu()
+
+    def softagg(agg, x, key):
+        _, gid = torch.unique(key, return_inverse=True)
+        G = int(gid.max()) + 1
+        f, g = agg.f(x), agg.g(x)
+        gmax = torch.full((G, x.shape[1]), -float("inf")).scatter_reduce(0, gid[:, None].expand_as(g), g, "amax")
+        w = torch.exp(g - gmax[gid])
+        den = torch.zeros(G, x.shape[1]).index_add_(0, gid, w)
+        y = torch.zeros(G, x.shape[1]).index_add_(0, gid, f * w) / den
+        return agg.h(y)[gid]
+
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        with torch.no_grad():
+            t = time.perf_counter()
+            x = upd.norm(net + ctx + upd.corr(corr))
+            # neighbour rows (net[:, ix], net.py:82-85): a fixed permutation of the sample
+            x = x + upd.c1(x[torch.roll(torch.arange(rows), 1)])
+            x = x + upd.c2(x[torch.roll(torch.arange(rows), -1)])
+            x = x + softagg(upd.agg_kk, x, kk)
+            x = x + softagg(upd.agg_ij, x, ii * 12345 + jj)
+            x = upd.gru(x)
+            upd.d(x), upd.w(x)
+            return time.perf_counter() - t
+    finally:
+        torch.set_num_threads(prev)
+
+
 def cpu_baseline(slam, sample_edges, iterations):
-    """The CPU oracle (a C restatement of the reference's altcorr + fastba +
-    point-cloud arithmetic) timed on this host: altcorr on a bounded edge
-    sample (extrapolated linearly to all edges) with T = min(16, cpu_count)
-    OpenMP threads over edges (the box's CPU share per GPU) and with 1
-    thread, BA and the point cloud (single-threaded) on the full patch graph."""
+    """A whole keyframe of the hot path on this host's CPU, timed phase by
+    phase on bounded samples and scaled to the full workload:
+      * altcorr: the C oracle (a restatement of correlation_kernel.cu) on a
+        sample of edges, with T = min(16, cpu_count) OpenMP threads (the box's
+        CPU share per GPU) and with 1 thread;
+      * update operator: the module's own layers in fp32 torch-CPU (T threads),
+        on a sample of edge rows;
+      * fastba (the C oracle, 1 thread) and the point cloud (1 thread) on the
+        full patch graph.
+    Per-phase seconds and threads are reported; cores = the largest thread
+    count any phase used."""
     from oracle import oracle
     E = slam.pg.ii.numel()
     threads = max(1, min(16, os.cpu_count() or 1))
@@ -175,6 +249,9 @@ def cpu_baseline(slam, sample_edges, iterations):
     sample_t = min(E, sample_edges * threads)
     t_corr = corr_seconds(sample_t, threads)
     oracle.set_threads(1)
+    rows = min(E, 8192)
+    t_net = _update_op_cpu_seconds(slam, rows, threads) * E / rows
+    t_net1 = _update_op_cpu_seconds(slam, min(E, 2048), 1) * E / min(E, 2048)
     n = slam.n
     target = (slam.reproject()[..., 1, 1] + torch.randn(1, E, 2, device=slam.device)).cpu().numpy()
     weight = torch.rand(1, E, 2).numpy()
@@ -189,15 +266,63 @@ def cpu_baseline(slam, sample_edges, iterations):
     t = time.perf_counter()
     oracle.point_cloud_centre(poses, patches[:m], intr, slam.ix[:m].cpu().numpy())
     t_pc = time.perf_counter() - t
-    total, total1 = t_corr + t_ba + t_pc, t_corr1 + t_ba + t_pc
+    total = t_corr + t_net + t_ba + t_pc
+    total1 = t_corr1 + t_net1 + t_ba + t_pc
+    r = lambda x: round(x, 4)
     return {"value": round(1.0 / total, 6), "unit": "keyframes/s", "cores": threads, "kind": "port",
-            "sample": f"C oracle (tests' parity checker): altcorr on {sample_t} of {E} edges with {threads} OpenMP "
-                      f"threads (scaled x{E / sample_t:.1f}), fastba ({iterations} it) and point cloud on the full "
-                      f"graph single-threaded ({t_ba:.2f}s, {t_pc:.2f}s); update operator (network) excluded -- "
-                      f"it has no CPU restatement",
+            "cpu_model": _cpu_model(), "whole_keyframe": True,
+            "phases": {"altcorr": {"seconds": r(t_corr), "threads": threads,
+                                   "sample": f"C oracle on {sample_t} of {E} edges, scaled x{E / sample_t:.1f}"},
+                       "update_op": {"seconds": r(t_net), "threads": threads,
+                                     "sample": f"torch-CPU fp32 module layers on {rows} of {E} rows, scaled"},
+                       "fastba": {"seconds": r(t_ba), "threads": 1, "sample": f"C oracle, full graph, {iterations} it"},
+                       "point_cloud": {"seconds": r(t_pc), "threads": 1, "sample": f"C oracle, {m} patches"}},
+            "sample": f"altcorr and update operator on edge samples with {threads} threads (scaled to E={E}); "
+                      f"fastba ({iterations} it) and point cloud single-threaded on the full graph",
             "seconds_per_keyframe": round(total, 3),
             "single_thread": {"value": round(1.0 / total1, 6), "cores": 1, "seconds_per_keyframe": round(total1, 3),
-                              "sample": f"altcorr on {sample_edges} of {E} edges, 1 thread"}}
+                              "sample": f"altcorr on {sample_edges} edges, update operator on 2048 rows, 1 thread"}}
+
+
+def end_to_end(cfgd, buffer, iterations, frames, warmup=8, device="cuda"):
+    """North-star end-to-end frames/s: DPVO.__call__ per synthetic 512x384
+    frame (ingest CNNs + patchify + edges + update + keyframe) from the
+    injected steady state.  KEYFRAME_THRESH is set to the median motion
+    magnitude seen over the warm-up frames, so keyframe() both keeps and
+    drops frames in the timed stream (random weights give no natural scale);
+    the keep / drop counts are reported."""
+    from dpvo.synthetic import image_stream, steady_state_tracker
+    total = frames + warmup
+    slam = steady_state_tracker(cfgd["preset"], buffer=buffer, n=buffer - 8 - total, seed=0, iterations=iterations,
+                                device=device, **cfgd["overrides"])
+    intr = torch.tensor([320.0, 320.0, 320.0, 240.0], device=slam.device)
+    imgs = [img for _, img in image_stream(total, device=slam.device)]
+    mags, kept = [], [0, 0]
+    inner = slam.keyframe
+
+    def keyframe():
+        k = slam.n - slam.cfg.KEYFRAME_INDEX
+        if len(mags) < warmup:
+            mags.append(sum(slam._motionmag_dev(k - 1, k + 1).tolist()) / 2)
+        n0 = slam.n
+        inner()
+        kept[int(slam.n == n0)] += 1
+    slam.keyframe = keyframe
+    t_first = slam.n
+    with torch.no_grad():
+        for k, img in enumerate(imgs):
+            if k == warmup:
+                slam.cfg.KEYFRAME_THRESH = float(np.median(mags))
+                kept[:] = [0, 0]
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            slam(t_first + k, img, None, None, intr)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    return {"metric": "end-to-end frames/s (DPVO.__call__: ingest CNNs + patchify + update + keyframe)",
+            "value": round(frames / dt, 2), "unit": "frames/s", "ms_per_frame": round(dt / frames * 1e3, 3),
+            "frames": frames, "warmup": warmup, "keyframes_kept": kept[1], "keyframes_dropped": kept[0],
+            "keyframe_thresh": round(slam.cfg.KEYFRAME_THRESH, 4)}
 
 
 def main():
@@ -208,8 +333,11 @@ def main():
     from dpvo.synthetic import steady_state_tracker
 
     cuda_ba.CHECK_CHOLESKY = True
-    slam = steady_state_tracker(args.preset, buffer=args.buffer, seed=rank, iterations=args.iterations,
-                                device=f"cuda:{local}")
+    cfgd = CONFIGS[args.config]
+    args.buffer = args.buffer or cfgd["buffer"]
+    args.iterations = args.iterations or cfgd["iterations"]
+    slam = steady_state_tracker(cfgd["preset"], buffer=args.buffer, seed=rank, iterations=args.iterations,
+                                device=f"cuda:{local}", **cfgd["overrides"])
     E = slam.pg.ii.numel()
     probe = CorrProbe()
     probe.wrap(slam)
@@ -253,7 +381,7 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f16+f32",
             "data": "synthetic (seeded steady-state patch graph, random-init VONet weights)",
-            "config": {"workload": f"C3 dpvo_2k.yaml: M={slam.M}, {args.buffer}-KF buffer, n={slam.n} keyframes, "
+            "config": {"workload": f"{cfgd['name']}: M={slam.M}, {args.buffer}-KF buffer, n={slam.n} keyframes, "
                                    f"E={E} edges, 512x384, {slam.cfg.BA_ITERATIONS} BA iterations",
                        "patches_per_frame": slam.M, "buffer": args.buffer, "n_keyframes": slam.n, "edges": E,
                        "ba_iterations": slam.cfg.BA_ITERATIONS, "image": "512x384",
@@ -263,11 +391,16 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "bytes_per_edge": CORR_BYTES_PER_EDGE, "avg_launch_ms": round(corr_ms, 5)},
             "breakdown_ms": breakdown,
+            "fastba_us_per_iteration": round(breakdown["fastba"] * 1e3 / slam.cfg.BA_ITERATIONS, 2),
         }
         if gather_ms is not None:
             line["gather_ms"] = gather_ms
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(slam, args.cpu_sample_edges, slam.cfg.BA_ITERATIONS)
+        if world == 1 and args.e2e_frames > 0:
+            del slam
+            torch.cuda.empty_cache()
+            line["end_to_end"] = end_to_end(cfgd, args.buffer, args.iterations, args.e2e_frames, device=f"cuda:{local}")
         print(json.dumps(line), flush=True)
 
     if world > 1:

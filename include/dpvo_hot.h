@@ -238,7 +238,9 @@ int dpvo_softagg_forward(int dtype, const void* f, int64_t ldf, const void* s, i
  * the groups, without a host round trip.  gid[e] = rank of key[e] among the
  * distinct keys (ascending, = torch.unique's inverse); group g's edges are
  * perm[offs[g] .. offs[g+1]) in ascending edge order; *groups (device int64)
- * = number of distinct keys.  Keys must lie in [0, 2^key_bits), key_bits <= 32.
+ * = number of distinct keys.  Keys must lie in [0, 2^key_bits) when
+ * key_bits <= 32 (a 32-bit radix sort over key_bits bits); key_bits in 33..64
+ * sorts the full 64-bit key (any int64; gid order is then unsigned order).
  * offs has n+1 entries, perm n. */
 size_t dpvo_group_by_workspace_bytes(int64_t n);
 int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_t* gid, int* offs, int* perm, int64_t* groups,

@@ -35,6 +35,9 @@ def lib():
     if _lib is None:
         build()
         _lib = ctypes.CDLL(_LIB_PATH)
+        # one thread unless a caller asks for more (bench.cpu_baseline): test
+        # processes share the box with the GPU run and need no thread team
+        _lib.oracle_set_threads(ctypes.c_int(int(os.environ.get("DPVO_ORACLE_THREADS", "1"))))
     return _lib
 
 

@@ -4,6 +4,7 @@ plyfile (absent), so the checks restate the formats they write: the TUM line
 layout including the reference's quaternion-component order, COLMAP's text
 model (poses inverted to world->camera), and an ASCII PLY round trip."""
 import numpy as np
+import pytest
 
 from dpvo import io
 
@@ -44,8 +45,11 @@ def test_colmap_model_inverts_poses(tmp_path):
     pts = np.random.default_rng(2).normal(size=(4, 3))
     clr = np.random.default_rng(3).random((4, 3))
     traj = io.PoseTrajectory3D.from_dpvo(poses, np.arange(3))
-    io.save_output_for_COLMAP(tmp_path / "m", np.arange(3), traj, pts, clr, 80.0, 81.0, 64.0, 48.0, H=384, W=512)
+    # the reference's positional call (dpvo_demo.py:205): nerf_studio_format sits before the intrinsics
+    io.save_output_for_COLMAP(tmp_path / "m", np.arange(3), traj, pts, clr, False, 80.0, 81.0, 64.0, 48.0, 384, 512)
     assert (tmp_path / "m" / "cameras.txt").read_text() == "1 PINHOLE 512 384 80.0 81.0 64.0 48.0"
+    with pytest.raises(NotImplementedError):
+        io.save_output_for_COLMAP(tmp_path / "n", np.arange(3), traj, pts, clr, True, 80.0, 81.0, 64.0, 48.0)
     lines = [line for line in (tmp_path / "m" / "images.txt").read_text().split("\n") if line]
     assert len(lines) == 3
     for line, p in zip(lines, poses):

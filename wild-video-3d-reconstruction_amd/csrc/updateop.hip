@@ -212,16 +212,21 @@ int gather_dispatch_out(const TI* x, int64_t ldx, int64_t rows, const int64_t* i
 // ---------------------------------------------------------------------------
 // sync-free group-by (torch.unique(key, return_inverse=True) + CSR)
 // ---------------------------------------------------------------------------
+// keys as unsigned radix-sort keys: 32-bit when the caller's bound fits
+// (fewer radix passes), 64-bit otherwise (any int64 key; negative keys sort
+// after the non-negative ones but still group by equality)
+template <typename K>
 __global__ __launch_bounds__(256) void gb_keys_kernel(const int64_t* __restrict__ key, int64_t n,
-                                                      uint32_t* __restrict__ k32, int* __restrict__ idx)
+                                                      K* __restrict__ kout, int* __restrict__ idx)
 {
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-        k32[e] = (uint32_t)key[e];
+        kout[e] = (K)key[e];
         idx[e] = (int)e;
     }
 }
 
-__global__ __launch_bounds__(256) void gb_flags_kernel(const uint32_t* __restrict__ sk, int64_t n, int* __restrict__ flag)
+template <typename K>
+__global__ __launch_bounds__(256) void gb_flags_kernel(const K* __restrict__ sk, int64_t n, int* __restrict__ flag)
 {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         flag[i] = (i == 0 || sk[i] != sk[i - 1]) ? 1 : 0;
@@ -249,19 +254,21 @@ struct GbLayout {
 
 size_t gb_tmp_bytes(int64_t n)
 {
-    size_t a = 0, b = 0;
+    size_t a = 0, a64 = 0, b = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a, (uint32_t*)nullptr, (uint32_t*)nullptr, (int*)nullptr,
                                              (int*)nullptr, (int)n);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, a64, (uint64_t*)nullptr, (uint64_t*)nullptr, (int*)nullptr,
+                                             (int*)nullptr, (int)n);
     (void)hipcub::DeviceScan::InclusiveSum(nullptr, b, (int*)nullptr, (int*)nullptr, (int)n);
-    return a > b ? a : b;
+    return std::max(std::max(a, a64), b);
 }
 
 GbLayout gb_layout(int64_t n)
 {
     GbLayout L;
     int64_t o = 0;
-    L.k_in = o;  o += align256(4 * n);
-    L.k_out = o; o += align256(4 * n);
+    L.k_in = o;  o += align256(8 * n);
+    L.k_out = o; o += align256(8 * n);
     L.v_in = o;  o += align256(4 * n);
     L.flag = o;  o += align256(4 * n);
     L.incl = o;  o += align256(4 * n);
@@ -403,7 +410,7 @@ extern "C" int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_
                              int64_t* groups, void* workspace, size_t workspace_bytes, void* stream)
 {
     DPVO_CHECK_ARG(n >= 0 && n < (int64_t(1) << 31), "bad size");
-    DPVO_CHECK_ARG(key_bits >= 1 && key_bits <= 32, "key_bits must be 1..32");
+    DPVO_CHECK_ARG(key_bits >= 1 && key_bits <= 64, "key_bits must be 1..64");
     DPVO_CHECK_ARG(groups != nullptr, "groups output missing");
     hipStream_t st = as_stream(stream);
     if (n == 0) {
@@ -414,18 +421,24 @@ extern "C" int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_
     const GbLayout L = gb_layout(n);
     DPVO_CHECK_ARG(workspace != nullptr && workspace_bytes >= (size_t)L.total + 256, "workspace too small");
     char* ws = (char*)(((uintptr_t)workspace + 255) & ~uintptr_t(255));
-    uint32_t* k_in = (uint32_t*)(ws + L.k_in);
-    uint32_t* k_out = (uint32_t*)(ws + L.k_out);
     int* v_in = (int*)(ws + L.v_in);
     int* flag = (int*)(ws + L.flag);
     int* incl = (int*)(ws + L.incl);
     size_t tmp_bytes = (size_t)L.tmp_bytes;
     const unsigned g = grid_for(n, 256, 2048);
-    hipLaunchKernelGGL(gb_keys_kernel, dim3(g), dim3(256), 0, st, key, n, k_in, v_in);
-    DPVO_CHECK_LAUNCH();
-    DPVO_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(ws + L.tmp, tmp_bytes, k_in, k_out, v_in, perm, (int)n, 0,
-                                                      key_bits, st));
-    hipLaunchKernelGGL(gb_flags_kernel, dim3(g), dim3(256), 0, st, k_out, n, flag);
+    auto sort = [&](auto* k_in, auto* k_out) -> int {
+        using K = std::remove_pointer_t<decltype(k_in)>;
+        hipLaunchKernelGGL(gb_keys_kernel<K>, dim3(g), dim3(256), 0, st, key, n, k_in, v_in);
+        DPVO_CHECK_LAUNCH();
+        DPVO_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(ws + L.tmp, tmp_bytes, k_in, k_out, v_in, perm, (int)n, 0,
+                                                          key_bits, st));
+        hipLaunchKernelGGL(gb_flags_kernel<K>, dim3(g), dim3(256), 0, st, k_out, n, flag);
+        return 0;
+    };
+    if (key_bits <= 32)
+        sort((uint32_t*)(ws + L.k_in), (uint32_t*)(ws + L.k_out));
+    else
+        sort((uint64_t*)(ws + L.k_in), (uint64_t*)(ws + L.k_out));
     tmp_bytes = (size_t)L.tmp_bytes;
     DPVO_CHECK_HIP(hipcub::DeviceScan::InclusiveSum(ws + L.tmp, tmp_bytes, flag, incl, (int)n, st));
     hipLaunchKernelGGL(gb_finish_kernel, dim3(g), dim3(256), 0, st, flag, incl, perm, n, gid, offs, groups);

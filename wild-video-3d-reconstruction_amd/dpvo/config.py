@@ -66,6 +66,9 @@ PRESETS = {
     "dpvo_2k": dict(PATCHES_PER_FRAME=192, REMOVAL_WINDOW=22, OPTIMIZATION_WINDOW=10, PATCH_LIFETIME=13,
                     KEYFRAME_THRESH=65.0, MOTION_MODEL="DAMPED_LINEAR", MOTION_DAMPING=0.5, MIXED_PRECISION=True,
                     GRADIENT_BIAS=False),
+    "tum_default": dict(PATCHES_PER_FRAME=384, REMOVAL_WINDOW=22, OPTIMIZATION_WINDOW=10, PATCH_LIFETIME=13,
+                        KEYFRAME_THRESH=30.0, MOTION_MODEL="DAMPED_LINEAR", MOTION_DAMPING=0.5,
+                        MIXED_PRECISION=True, GRADIENT_BIAS=False),
     "fast": dict(PATCHES_PER_FRAME=48, REMOVAL_WINDOW=16, OPTIMIZATION_WINDOW=7, PATCH_LIFETIME=11,
                  KEYFRAME_THRESH=15.0, MOTION_MODEL="DAMPED_LINEAR", MOTION_DAMPING=0.5, MIXED_PRECISION=True,
                  GRADIENT_BIAS=False),

@@ -40,6 +40,10 @@ class DPVO:
                  device="cuda"):
         if viz or rerun:
             raise NotImplementedError("visualisation is out of scope for the MI355X hot-path build")
+        if getattr(cfg, "loop_enabled", False):
+            # the reference builds a retrieval + DISK/LightGlue + Sim(3) PGO loop
+            # closer here (dpvo.py:101-102); it needs remote weights and is out of scope
+            raise NotImplementedError("cfg.loop_enabled: loop closure is out of scope for the MI355X hot-path build")
         self.cfg = cfg
         self.device = torch.device(device)
         self.load_weights(network)
@@ -249,8 +253,10 @@ class DPVO:
         return pops.motion_mag_pair(SE3(self.poses), self.patches, self.intrinsics, self.pg.ii, self.pg.jj,
                                     self.pg.kk, i, j, beta=0.5)
 
-    def update(self):
-        """One keyframe of the hot loop (dpvo.py:711-749)."""
+    def update(self, t0=None):
+        """One keyframe of the hot loop (dpvo.py:711-749).  t0: optional lower
+        bound of the optimised pose window (the reference's max(t0_, t0 or 1),
+        :730-731)."""
         with Timer("other", enabled=self.enable_timing):
             coords = self.reproject()
             with torch.autocast("cuda", enabled=True):
@@ -258,14 +264,15 @@ class DPVO:
                 # ctx = imap[:, kk % (M pmem)] (dpvo.py:718), gathered by the consumer
                 ctx_idx = self.pg.kk % (self.M * self.pmem)
                 self.pg.net, (delta, weight, _) = self.network.update(self.pg.net, self.imap, corr, None, self.pg.ii,
-                                                                      self.pg.jj, self.pg.kk, inp_idx=ctx_idx)
+                                                                      self.pg.jj, self.pg.kk, inp_idx=ctx_idx,
+                                                                      index_bounds=(self.N * self.M, self.N))
             weight = weight.float()
             target = coords[..., self.P // 2, self.P // 2] + delta.float()
         self.pg.target = target
         self.pg.weight = weight
         with Timer("BA", enabled=self.enable_timing):
-            t0 = self.n - self.cfg.OPTIMIZATION_WINDOW if self.is_initialized else 1
-            t0 = max(t0, 1)
+            t0_ = self.n - self.cfg.OPTIMIZATION_WINDOW if self.is_initialized else 1
+            t0 = max(t0_, t0 or 1)
             fastba.BA(self.poses, self.patches, self.intrinsics, target, weight, self._lmbda, self.pg.ii, self.pg.jj,
                       self.pg.kk, t0, self.n, getattr(self.cfg, "BA_ITERATIONS", 2))
             m = self.pg.m

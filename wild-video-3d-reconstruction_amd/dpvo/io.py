@@ -98,15 +98,21 @@ def _quat_wxyz(R):
     return q if q[0] >= 0 else -q
 
 
-def save_output_for_COLMAP(name, tstamp, traj, points, colors, fx, fy, cx, cy, H=480, W=640, image_names=None):
-    """COLMAP text model (plot_utils.py:57-95): cameras.txt (one PINHOLE
-    camera), images.txt (the inverted poses, world->camera, as IMAGE_ID QW QX
-    QY QZ TX TY TZ 1 NAME plus an empty line) and points3D.txt (ID X Y Z R G B
-    0.0 and an empty track).  traj: a PoseTrajectory3D (dpvo_demo.py:205
-    passes the from_dpvo one) or a (poses, tstamps) tuple (make_traj's
-    reading).  colors in [0, 1].  The nerfstudio / `colmap model_converter`
-    branch (:97-113) shells out to external tools and is not reproduced;
-    image_names replaces the images/ directory listing (:66-77)."""
+def save_output_for_COLMAP(name, tstamp, traj, points, colors, nerf_studio_format, fx, fy, cx, cy, H=480, W=640, *,
+                           image_names=None):
+    """COLMAP text model (plot_utils.py:58-95), same positional signature:
+    cameras.txt (one PINHOLE camera), images.txt (the inverted poses,
+    world->camera, as IMAGE_ID QW QX QY QZ TX TY TZ 1 NAME plus an empty line)
+    and points3D.txt (ID X Y Z R G B 0.0 and an empty track).  traj: a
+    PoseTrajectory3D (dpvo_demo.py:205 passes the from_dpvo one) or a (poses,
+    tstamps) tuple (make_traj's reading).  colors in [0, 1].  The
+    nerf_studio_format branch (:96-113) shells out to `colmap
+    model_converter` and nerfstudio, which are not part of this build: True
+    raises NotImplementedError.  image_names (keyword) replaces the images/
+    directory listing (:66-77)."""
+    if nerf_studio_format:
+        raise NotImplementedError("nerf_studio_format shells out to colmap / nerfstudio (plot_utils.py:96-113); "
+                                  "not part of the MI355X build")
     d = Path(name)
     d.mkdir(parents=True, exist_ok=True)
     traj = make_traj(traj)

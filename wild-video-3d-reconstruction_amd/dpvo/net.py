@@ -68,7 +68,7 @@ class Update(nn.Module):
                 torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16 and
                 self.FUSED)
 
-    def _forward_fused(self, net, inp, corr, ii, jj, kk, inp_idx=None):
+    def _forward_fused(self, net, inp, corr, ii, jj, kk, inp_idx=None, index_bounds=None):
         """The same dataflow as the reference under autocast, in 19 full-row
         fused GEMMs (csrc/rowgemm.hip; 5 Linear->ReLU->Linear pairs chained,
         14 launches) + 2 SoftAggs: every Linear is an fp16
@@ -92,14 +92,20 @@ class Update(nn.Module):
                                 ln=pk["norm"], want32=True)
         # the kk group-by (SoftAgg below) also yields the temporal neighbours:
         # fastba.neighbors(kk, jj) without a second sort
-        kk_groups = U.group_by(kk, key_bits=32)
+        # radix-sort key widths: from the caller's index bounds (the tracker
+        # knows its buffer: kk < N M, ii, jj < N), else full 64-bit keys
+        kk_bits, ij_bits = 64, 64
+        if index_bounds is not None:
+            kk_bits = U.key_bits_for(index_bounds[0])
+            ij_bits = U.key_bits_for(index_bounds[1] * 12345 + 12345)
+        kk_groups = U.group_by(kk, key_bits=kk_bits)
         ix, jx = U.neighbors_csr(jj, kk_groups[1], kk_groups[2], kk_groups[3], E)
         for (la, lb), nb in ((pk["c1"], ix), (pk["c2"], jx)):
             n32, n16, _ = U.rowchain(n16, *la, *lb, flags1=U.RELU, a_idx=nb, flags=U.RES, res32=n32, want32=True)
         ln0, gr1, ln1, gr2 = pk["gru"]
         for (pf, pg_, ph), key, ln in ((pk["agg_kk"], None, None), (pk["agg_ij"], ii * 12345 + jj, ln0)):
             # unique(key) + CSR on the device (no host sync); G stays on the device
-            gid, offs, perm, G = kk_groups if key is None else U.group_by(key, key_bits=32)
+            gid, offs, perm, G = kk_groups if key is None else U.group_by(key, key_bits=ij_bits)
             _, f16, _ = U.rowgemm(n16, *pf)
             _, g16, _ = U.rowgemm(n16, *pg_)
             y = U.softagg_csr(f16, g16, offs, perm, G, E)
@@ -117,13 +123,15 @@ class Update(nn.Module):
                                          gate16=g16, ln=ln1, want32=True)
         return n32[None], (heads[None, :, :2], heads[None, :, 2:], None)
 
-    def forward(self, net, inp, corr, flow, ii, jj, kk, inp_idx=None):
+    def forward(self, net, inp, corr, flow, ii, jj, kk, inp_idx=None, index_bounds=None):
         """edge hidden state -> (new state, (delta, weight, None)) (net.py:75-93).
 
-        inp_idx (optional, not in the reference): inp is then the un-gathered
-        context ring and the rows are inp[:, inp_idx]."""
+        Optional, not in the reference: inp_idx -- inp is then the un-gathered
+        context ring and the rows are inp[:, inp_idx]; index_bounds =
+        (num_patches, num_frames) -- kk < num_patches and ii, jj < num_frames,
+        which narrows the fused path's radix sorts."""
         if self._fusable(net, inp, corr) and (inp_idx is None or inp.is_contiguous()):
-            return self._forward_fused(net, inp, corr, ii, jj, kk, inp_idx)
+            return self._forward_fused(net, inp, corr, ii, jj, kk, inp_idx, index_bounds)
         if inp_idx is not None:
             inp = inp[:, inp_idx]
         net = self.norm(net + inp + self.corr(corr))
@@ -235,7 +243,12 @@ class Patchifier(nn.Module):
         x = torch.randint(1, w - 1, size=[1, M], device=dev)
         y = torch.randint(1, h - 1, size=[1, M], device=dev)
         amp = torch.is_autocast_enabled("cuda")
-        key = (tuple(image.shape), image.dtype, M, bool(return_color), amp, dev)
+        # the captured kernels hold raw parameter / buffer addresses and the
+        # autocast dtype: any re-placement (.to(), .half(), load_state_dict
+        # with assign=True) or a different autocast dtype re-captures
+        tensors = tuple(t.data_ptr() for t in self.parameters()) + tuple(t.data_ptr() for t in self.buffers())
+        key = (tuple(image.shape), image.dtype, M, bool(return_color), amp,
+               torch.get_autocast_dtype("cuda") if amp else None, dev, tensors)
         if self._graph_key != key:
             self._capture(image, x, y, return_color, amp, key)
         self._g_in[0].copy_(image)
@@ -253,12 +266,13 @@ class Patchifier(nn.Module):
         static = (image.clone(), x.clone(), y.clone())
         side = torch.cuda.Stream(device=image.device)
         side.wait_stream(torch.cuda.current_stream(image.device))
-        with torch.cuda.stream(side), torch.autocast("cuda", enabled=amp, cache_enabled=False):
+        dt = key[5] or torch.float16
+        with torch.cuda.stream(side), torch.autocast("cuda", dtype=dt, enabled=amp, cache_enabled=False):
             for _ in range(2):  # warm-up: MIOpen solver selection, allocator pools
                 self._ingest(*static, return_color)
         torch.cuda.current_stream(image.device).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph), torch.autocast("cuda", enabled=amp, cache_enabled=False):
+        with torch.cuda.graph(graph), torch.autocast("cuda", dtype=dt, enabled=amp, cache_enabled=False):
             out = self._ingest(*static, return_color)
         self._graph, self._graph_key, self._g_in, self._g_out = graph, key, static, out
 

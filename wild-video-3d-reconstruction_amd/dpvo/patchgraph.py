@@ -12,6 +12,7 @@ import torch
 
 from . import projective_ops as pops
 from .lietorch import SE3
+from .utils import matrix_to_quaternion
 
 
 class PatchGraph:
@@ -76,14 +77,39 @@ class PatchGraph:
         pops.point_cloud_centre(SE3(self.poses), self.patches[:, :self.m], self.intrinsics, self.ix[:self.m],
                                 out=self.points_[:self.m])
 
-    def set_prior_depth(self, idx, depth):
-        """initialise frame idx's patch depth from a metric depth map (patchgraph.py:97-110)."""
-        if depth is None:
-            return
+    def _prior_patch(self, idx, depth):
+        """frame idx's patches with the inverse of the median metric depth
+        under each patch's 3x3 (full-resolution) sample points."""
         patch = self.patches_[idx]
         xs = torch.clamp(patch[:, 0].long() * self.RES, 0, depth.shape[1] - 1)
         ys = torch.clamp(patch[:, 1].long() * self.RES, 0, depth.shape[0] - 1)
         med = torch.median(depth[ys, xs].view(patch.shape[0], -1), dim=1).values
         patch[:, 2] = 1 / med.view(-1, 1, 1)
+        return patch
+
+    def set_prior_depth(self, idx, depth):
+        """initialise frame idx's patch depth from a metric depth map (patchgraph.py:97-110)."""
+        if depth is None:
+            return
+        patch = self._prior_patch(idx, depth)
         self.patches_est_[idx] = patch
         self.patches_[idx] = patch
+
+    def init_from_prior(self, depths, poses, indices, images=None):
+        """known depths and camera poses for the frames in `indices`
+        (patchgraph.py:112-140): depths, a list of full-resolution metric
+        depth maps [H, W]; poses [N, 4, 4] camera->world matrices, stored
+        inverted (world->camera) as [t, qx, qy, qz, qw].  As in the reference
+        the depth is written through the patches_[idx] view (so patches_ and
+        patches_est_ both get it)."""
+        depths = torch.stack(list(depths), dim=0)
+        dpvo_poses = create_se3_from_mat(torch.as_tensor(poses, device=depths.device, dtype=torch.float)).inv()
+        for idx in indices:
+            self.patches_est_[idx] = self._prior_patch(idx, depths[idx])
+            self.poses_[idx] = dpvo_poses[idx].data
+
+
+def create_se3_from_mat(mats):
+    """[N, 4, 4] -> SE3 with data [t, qx, qy, qz, qw] (patchgraph.py:142-148)."""
+    q = matrix_to_quaternion(mats[:, :3, :3])[:, [1, 2, 3, 0]]
+    return SE3(torch.cat([mats[:, :3, 3], q], dim=1))

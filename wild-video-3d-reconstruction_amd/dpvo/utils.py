@@ -70,3 +70,27 @@ def set_depth(patches, depth):
 
 def flatmeshgrid(*args, **kwargs):
     return (x.reshape(-1) for x in torch.meshgrid(*args, **kwargs))
+
+
+def matrix_to_quaternion(matrix):
+    """rotation matrices [..., 3, 3] -> unit quaternions [..., 4] as (w, x, y,
+    z) with w >= 0 (reference utils.py:118-167).  Of the four algebraically
+    equal candidates (each divides by one of 4w^2, 4x^2, 4y^2, 4z^2) the one
+    with the largest divisor is kept, as the reference does."""
+    if matrix.shape[-2:] != (3, 3):
+        raise ValueError(f"Invalid rotation matrix shape {tuple(matrix.shape)}.")
+    m = matrix.reshape(matrix.shape[:-2] + (9,))
+    m00, m01, m02, m10, m11, m12, m20, m21, m22 = m.unbind(-1)
+    four_sq = torch.stack([1 + m00 + m11 + m22, 1 + m00 - m11 - m22,
+                           1 - m00 + m11 - m22, 1 - m00 - m11 + m22], -1)
+    r = torch.sqrt(four_sq.clamp(min=0))  # 2|w|, 2|x|, 2|y|, 2|z|
+    # candidate c scaled by r_c: rows (w, x, y, z) * r_c
+    cand = torch.stack([
+        torch.stack([r[..., 0] ** 2, m21 - m12, m02 - m20, m10 - m01], -1),
+        torch.stack([m21 - m12, r[..., 1] ** 2, m10 + m01, m02 + m20], -1),
+        torch.stack([m02 - m20, m10 + m01, r[..., 2] ** 2, m12 + m21], -1),
+        torch.stack([m10 - m01, m20 + m02, m21 + m12, r[..., 3] ** 2], -1)], -2)
+    cand = cand / (2.0 * r.clamp(min=0.1))[..., None]
+    best = r.argmax(-1)
+    q = torch.gather(cand, -2, best[..., None, None].expand(best.shape + (1, 4))).squeeze(-2)
+    return torch.where(q[..., :1] < 0, -q, q)

@@ -35,10 +35,19 @@ def softagg(f, s, group, groups, eps=1e-12):
     return y
 
 
-def group_by(key, key_bits=32):
+def key_bits_for(bound):
+    """radix-sort key width for keys known to lie in [0, bound)."""
+    return max(1, (int(bound) - 1).bit_length())
+
+
+def group_by(key, key_bits=64):
     """torch.unique(key, return_inverse=True) without a host sync, plus the
     groups' CSR: -> (gid int64 [E], offs int32 [E+1], perm int32 [E],
-    groups int64 [1] on the device).  Keys must lie in [0, 2**key_bits)."""
+    groups int64 [1] on the device).  key_bits <= 32 promises keys in
+    [0, 2**key_bits) (fewer radix passes: pass key_bits_for(bound) when the
+    caller knows a bound); the default sorts full 64-bit keys."""
+    if not 1 <= int(key_bits) <= 64:
+        raise RuntimeError("group_by: key_bits must be 1..64")
     H.on_gpu(key)
     key = H.idx64(key)
     n = key.numel()
