@@ -131,28 +131,32 @@ def phase_breakdown(slam, reps=5):
     from dpvo import projective_ops as pops
     from dpvo.lietorch import SE3
     ev = lambda: torch.cuda.Event(enable_timing=True)
-    acc = {k: [] for k in ("reproject", "altcorr", "update_op", "fastba", "point_cloud")}
+    import update_ops
+    acc = {k: [] for k in ("reproject", "group_by", "altcorr", "update_op", "fastba", "point_cloud")}
     for _ in range(reps):
-        e = [ev() for _ in range(6)]
+        e = [ev() for _ in range(7)]
         e[0].record()
         coords = slam.reproject()
         e[1].record()
+        kk_groups = update_ops.group_by(slam.pg.kk, key_bits=update_ops.key_bits_for(slam.N * slam.M))
+        e[2].record()
         with torch.autocast("cuda", enabled=True):
             corr = slam.corr(coords)
-            e[2].record()
+            e[3].record()
             ctx_idx = slam.pg.kk % (slam.M * slam.pmem)
             net, (delta, weight, _) = slam.network.update(slam.pg.net, slam.imap, corr, None, slam.pg.ii, slam.pg.jj,
-                                                          slam.pg.kk, inp_idx=ctx_idx)
+                                                          slam.pg.kk, inp_idx=ctx_idx,
+                                                          index_bounds=(slam.N * slam.M, slam.N), kk_groups=kk_groups)
         target = coords[..., 1, 1] + delta.float()
-        e[3].record()
+        e[4].record()
         fastba.BA(slam.poses, slam.patches, slam.intrinsics, target, weight.float(), slam._lmbda, slam.pg.ii,
                   slam.pg.jj, slam.pg.kk, max(slam.n - slam.cfg.OPTIMIZATION_WINDOW, 1), slam.n,
-                  slam.cfg.BA_ITERATIONS)
-        e[4].record()
+                  slam.cfg.BA_ITERATIONS, csr=kk_groups[1:])
+        e[5].record()
         m = slam.pg.m
         pops.point_cloud_centre(SE3(slam.poses), slam.patches[:, :m], slam.intrinsics, slam.ix[:m],
                                 out=slam.pg.points_[:m])
-        e[5].record()
+        e[6].record()
         torch.cuda.synchronize()
         for k, (a, b) in zip(acc, zip(e[:-1], e[1:])):
             acc[k].append(a.elapsed_time(b))

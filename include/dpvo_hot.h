@@ -127,20 +127,35 @@ int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches, int P, co
                     const int64_t* jj, const int64_t* kk, int64_t num_edges, int t0, int t1, int iterations,
                     void* workspace, size_t workspace_bytes, int* status, void* stream);
 
-/* Same, with a solver choice.  Windows of up to 64 optimised poses (DPVO's
- * sliding window of 10) use the dense path: dense B / E, one-wave Cholesky,
- * fully asynchronous.  Larger windows -- the global BA of dpvo.py:436-505,
- * t0 = 1, t1 = n -- or DPVO_BA_SPARSE use the sparse path: per-edge Schur
- * entries instead of the dense E (6N x Mu), S accumulated into 64 x 64 tiles
- * of its band, tiled band Cholesky.  Up to 32767 poses.  The sparse path
- * reads the pose-graph bandwidth back to the host once per call (one stream
- * synchronisation); its status is the failing leading-minor order as above. */
-enum { DPVO_BA_AUTO = 0, DPVO_BA_SPARSE = 1 };
+/* Same, with a solver choice.  Windows of up to 12 optimised poses (DPVO's
+ * sliding window of 10) use the deterministic per-patch path: one wave per
+ * unique patch reduces its edges' C, u, E row and pose-block terms without
+ * atomics, per-wave partials of S = B - E Q E^T are summed in a fixed order,
+ * one workgroup factors S (fp32 Cholesky) -- bitwise repeatable, fully
+ * asynchronous.  Windows of 13..64 poses (or DPVO_BA_ATOMIC) use the dense
+ * atomic path: dense B / E, one-wave Cholesky.  Larger windows -- the global
+ * BA of dpvo.py:436-505, t0 = 1, t1 = n -- or DPVO_BA_SPARSE use the sparse
+ * path: per-edge Schur entries instead of the dense E (6N x Mu), S
+ * accumulated into 64 x 64 tiles of its band, tiled band Cholesky.  Up to
+ * 32767 poses.  The sparse path reads the pose-graph bandwidth back to the
+ * host once per call (one stream synchronisation); its status is the failing
+ * leading-minor order as above. */
+enum { DPVO_BA_AUTO = 0, DPVO_BA_SPARSE = 1, DPVO_BA_ATOMIC = 2 };
 size_t dpvo_ba_workspace_bytes_ex(int64_t num_edges, int64_t num_patches, int num_opt_poses, int flags);
 int dpvo_ba_forward_ex(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
                        const float* target, const float* weight, const float* lmbda, const int64_t* ii,
                        const int64_t* jj, const int64_t* kk, int64_t num_edges, int t0, int t1, int iterations,
                        int flags, void* workspace, size_t workspace_bytes, int* status, void* stream);
+
+/* dpvo_ba_forward_ex with the caller's kk group-by (dpvo_group_by(kk): offs
+ * [E+1], perm [E], groups [1], device): the deterministic path's patch CSR.
+ * DPVO.update already groups kk for the update operator (SoftAgg over kk,
+ * the temporal neighbours), so BA reuses it; NULLs build it here. */
+int dpvo_ba_forward_csr(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
+                        const float* target, const float* weight, const float* lmbda, const int64_t* ii,
+                        const int64_t* jj, const int64_t* kk, int64_t num_edges, int t0, int t1, int iterations,
+                        int flags, const int* csr_offs, const int* csr_perm, const int64_t* csr_groups,
+                        void* workspace, size_t workspace_bytes, int* status, void* stream);
 
 /* cuda_ba.reproject (ba_cuda.cu:368-418,543-575): coords [E][2][P][P]. */
 int dpvo_reproject(const float* poses, const float* patches, int P, const float* intrinsics, const int64_t* ii,

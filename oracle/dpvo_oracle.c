@@ -15,7 +15,7 @@
  *   oracle_ba_forward       dpvo/fastba/ba_cuda.cu:18-211 (device math),
  *                           :214-365 (Hessian), :422-540 (driver)
  *   oracle_reproject        dpvo/fastba/ba_cuda.cu:368-418
- *   oracle_lie_*            dpvo/lietorch/include/so3.h, se3.h (SO3/SE3)
+ *   oracle_lie_*            dpvo/lietorch/include/so3.h, se3.h, rxso3.h, sim3.h
  *   oracle_transform        dpvo/projective_ops.py:19-68
  *   oracle_point_cloud      dpvo/projective_ops.py:106-108
  *   oracle_neighbors        dpvo/fastba/ba.cpp:113-158
@@ -812,13 +812,238 @@ static void se3_log(se3 g, double* xi)
     xi[3] = phi[0]; xi[4] = phi[1]; xi[5] = phi[2];
 }
 
+
+/* ------------------------------------------------------------------ */
+/* RxSO3 [qx qy qz qw s] and Sim3 [t q s] in double (rxso3.h, sim3.h)   */
+/* ------------------------------------------------------------------ */
+typedef struct { quat q; double s; } rxso3;
+typedef struct { rxso3 r; double t[3]; } sim3;
+
+static rxso3 rx_load(const double* d) { rxso3 g; g.q = q_load(d); g.s = d[4]; return g; }
+static void rx_store(rxso3 g, double* d) { d[0] = g.q.x; d[1] = g.q.y; d[2] = g.q.z; d[3] = g.q.w; d[4] = g.s; }
+static rxso3 rx_inv(rxso3 g) { rxso3 h; h.q = q_norm(q_conj(g.q)); h.s = 1.0 / g.s; return h; }
+static rxso3 rx_mul(rxso3 a, rxso3 b) { rxso3 c; c.q = q_norm(q_mul(a.q, b.q)); c.s = a.s * b.s; return c; }
+static void rx_act(rxso3 g, const double* p, double* o) /* s (R p) */
+{
+    q_act(g.q, p, o);
+    o[0] *= g.s; o[1] *= g.s; o[2] *= g.s;
+}
+static void rx_log(rxso3 g, double* ps) { so3_log(g.q, ps); ps[3] = log(g.s); }
+static rxso3 rx_exp(const double* ps) { rxso3 g; g.q = so3_exp(ps); g.s = exp(ps[3]); return g; }
+static void rx_calcW(const double* ps, double* W) /* rxso3.h calcW, row-major 3x3 */
+{
+    double Ph[9], Ph2[9];
+    hat3(ps, Ph);
+    mm3(Ph, Ph, Ph2);
+    const double sigma = ps[3], theta = sqrt(ps[0] * ps[0] + ps[1] * ps[1] + ps[2] * ps[2]), sc = exp(sigma);
+    double A, B, C;
+    if (fabs(sigma) < LIE_EPS) {
+        C = 1.0;
+        if (fabs(theta) < LIE_EPS) { A = 0.5; B = 1.0 / 6.0; }
+        else { A = (1.0 - cos(theta)) / (theta * theta); B = (theta - sin(theta)) / (theta * theta * theta); }
+    } else {
+        C = (sc - 1.0) / sigma;
+        if (fabs(theta) < LIE_EPS) {
+            const double s2 = sigma * sigma;
+            A = ((sigma - 1.0) * sc + 1.0) / s2;
+            B = (sc * 0.5 * s2 + sc - 1.0 - sigma * sc) / (s2 * sigma);
+        } else {
+            const double t2 = theta * theta, a = sc * sin(theta), b = sc * cos(theta), c = t2 + sigma * sigma;
+            A = (a * sigma + (1.0 - b) * theta) / (theta * c);
+            B = (C - ((b - 1.0) * sigma + a * theta) / c) / t2;
+        }
+    }
+    for (int i = 0; i < 9; i++) W[i] = A * Ph[i] + B * Ph2[i] + (i % 4 == 0 ? C : 0.0);
+}
+static void inv3d(const double* A, double* B) /* adjugate / determinant */
+{
+    const double c00 = A[4] * A[8] - A[5] * A[7], c01 = A[5] * A[6] - A[3] * A[8], c02 = A[3] * A[7] - A[4] * A[6];
+    const double det = A[0] * c00 + A[1] * c01 + A[2] * c02, id = 1.0 / det;
+    B[0] = c00 * id; B[1] = (A[2] * A[7] - A[1] * A[8]) * id; B[2] = (A[1] * A[5] - A[2] * A[4]) * id;
+    B[3] = c01 * id; B[4] = (A[0] * A[8] - A[2] * A[6]) * id; B[5] = (A[2] * A[3] - A[0] * A[5]) * id;
+    B[6] = c02 * id; B[7] = (A[1] * A[6] - A[0] * A[7]) * id; B[8] = (A[0] * A[4] - A[1] * A[3]) * id;
+}
+static sim3 sim3_load(const double* d) { sim3 g; g.t[0] = d[0]; g.t[1] = d[1]; g.t[2] = d[2]; g.r = rx_load(d + 3); return g; }
+static void sim3_store(sim3 g, double* d) { d[0] = g.t[0]; d[1] = g.t[1]; d[2] = g.t[2]; rx_store(g.r, d + 3); }
+static void sim3_log(sim3 g, double* xi) /* [W^-1 t, phi, sigma] */
+{
+    double W[9], Wi[9];
+    rx_log(g.r, xi + 3);
+    rx_calcW(xi + 3, W);
+    inv3d(W, Wi);
+    for (int i = 0; i < 3; i++) xi[i] = Wi[i * 3] * g.t[0] + Wi[i * 3 + 1] * g.t[1] + Wi[i * 3 + 2] * g.t[2];
+}
+static void sim3_adj_matrix(sim3 g, double* Ad) /* sim3.h Adj, row-major 7x7 */
+{
+    double R[9], tx[9], tR[9];
+    q_mat(g.r.q, R);
+    hat3(g.t, tx);
+    mm3(tx, R, tR);
+    memset(Ad, 0, sizeof(double) * 49);
+    for (int i = 0; i < 7; i++) Ad[i * 7 + i] = 1;
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) {
+            Ad[i * 7 + j] = g.r.s * R[i * 3 + j];
+            Ad[i * 7 + 3 + j] = tR[i * 3 + j];
+            Ad[(3 + i) * 7 + 3 + j] = R[i * 3 + j];
+        }
+        Ad[i * 7 + 6] = -g.t[i];
+    }
+}
+static void sim3_ad(const double* a, double* A) /* sim3.h adj */
+{
+    double Ta[9], Ph[9];
+    hat3(a, Ta);
+    hat3(a + 3, Ph);
+    memset(A, 0, sizeof(double) * 49);
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) {
+            A[i * 7 + j] = Ph[i * 3 + j] + (i == j ? a[6] : 0.0);
+            A[i * 7 + 3 + j] = Ta[i * 3 + j];
+            A[(3 + i) * 7 + 3 + j] = Ph[i * 3 + j];
+        }
+        A[i * 7 + 6] = -a[i];
+    }
+}
+static void mm7(const double* A, const double* B, double* C)
+{
+    double T[49];
+    for (int i = 0; i < 7; i++)
+        for (int j = 0; j < 7; j++) {
+            double s = 0;
+            for (int k = 0; k < 7; k++) s += A[i * 7 + k] * B[k * 7 + j];
+            T[i * 7 + j] = s;
+        }
+    memcpy(C, T, sizeof T);
+}
+static void sim3_left_jacobian_inverse(const double* xi, double* J) /* I - X/2 + X^2/12 - X^4/720 */
+{
+    double X[49], X2[49], X4[49];
+    sim3_ad(xi, X);
+    mm7(X, X, X2);
+    mm7(X2, X2, X4);
+    for (int i = 0; i < 49; i++) J[i] = (i % 8 == 0 ? 1.0 : 0.0) - 0.5 * X[i] + X2[i] / 12.0 - X4[i] / 720.0;
+}
+
+static int lie_forward_scaled(int op, int group, const double* X, const double* Y, double* out, int64_t n)
+{
+    for (int64_t i = 0; i < n; i++) {
+        if (group == G_RXSO3) {
+            const double* x = X + i * 5;
+            switch (op) {
+            case OP_EXP: rx_store(rx_exp(X + i * 4), out + i * 5); break;
+            case OP_LOG: rx_log(rx_load(x), out + i * 4); break;
+            case OP_INV: rx_store(rx_inv(rx_load(x)), out + i * 5); break;
+            case OP_MUL: rx_store(rx_mul(rx_load(x), rx_load(Y + i * 5)), out + i * 5); break;
+            case OP_ADJ: case OP_ADJT: { /* Adj = diag(R, 1) */
+                double R[9]; q_mat(rx_load(x).q, R);
+                const double* a = Y + i * 4; double* o = out + i * 4;
+                for (int r = 0; r < 3; r++) o[r] = op == OP_ADJ ? R[r * 3] * a[0] + R[r * 3 + 1] * a[1] + R[r * 3 + 2] * a[2]
+                                                           : R[r] * a[0] + R[3 + r] * a[1] + R[6 + r] * a[2];
+                o[3] = a[3];
+                break;
+            }
+            case OP_ACT: rx_act(rx_load(x), Y + i * 3, out + i * 3); break;
+            case OP_ACT4: rx_act(rx_load(x), Y + i * 4, out + i * 4); out[i * 4 + 3] = Y[i * 4 + 3]; break;
+            case OP_MATRIX: {
+                rxso3 g = rx_load(x); double R[9]; q_mat(g.q, R); double* o = out + i * 16;
+                memset(o, 0, sizeof(double) * 16);
+                for (int r = 0; r < 3; r++) for (int cc = 0; cc < 3; cc++) o[r * 4 + cc] = g.s * R[r * 3 + cc];
+                o[15] = 1; break;
+            }
+            case OP_PROJECTOR: { /* rxso3.h orthogonal_projector, 5x5 */
+                rxso3 g = rx_load(x); double* o = out + i * 25; memset(o, 0, sizeof(double) * 25);
+                const double v[3] = {-g.q.x, -g.q.y, -g.q.z}; double H[9]; hat3(v, H);
+                for (int r = 0; r < 3; r++) for (int cc = 0; cc < 3; cc++) o[r * 5 + cc] = 0.5 * ((r == cc ? g.q.w : 0) + H[r * 3 + cc]);
+                for (int cc = 0; cc < 3; cc++) o[3 * 5 + cc] = 0.5 * v[cc];
+                o[4 * 5 + 3] = g.s;
+                break;
+            }
+            case OP_JINV: { /* diag(so3 Jl^-1, 1) at Log(X) */
+                double ps[4], J[9]; rx_log(rx_load(x), ps); so3_left_jacobian_inverse(ps, J);
+                const double* a = Y + i * 4; double* o = out + i * 4;
+                for (int r = 0; r < 3; r++) o[r] = J[r * 3] * a[0] + J[r * 3 + 1] * a[1] + J[r * 3 + 2] * a[2];
+                o[3] = a[3];
+                break;
+            }
+            default: return -1;
+            }
+        } else {
+            const double* x = X + i * 8;
+            switch (op) {
+            case OP_EXP: {
+                const double* xi = X + i * 7; sim3 g; double W[9];
+                g.r = rx_exp(xi + 3); rx_calcW(xi + 3, W);
+                for (int r = 0; r < 3; r++) g.t[r] = W[r * 3] * xi[0] + W[r * 3 + 1] * xi[1] + W[r * 3 + 2] * xi[2];
+                sim3_store(g, out + i * 8); break;
+            }
+            case OP_LOG: sim3_log(sim3_load(x), out + i * 7); break;
+            case OP_INV: {
+                sim3 g = sim3_load(x), h; double tt[3]; h.r = rx_inv(g.r); rx_act(h.r, g.t, tt);
+                h.t[0] = -tt[0]; h.t[1] = -tt[1]; h.t[2] = -tt[2];
+                sim3_store(h, out + i * 8); break;
+            }
+            case OP_MUL: {
+                sim3 a = sim3_load(x), b = sim3_load(Y + i * 8), c; double tt[3];
+                c.r = rx_mul(a.r, b.r); rx_act(a.r, b.t, tt);
+                c.t[0] = a.t[0] + tt[0]; c.t[1] = a.t[1] + tt[1]; c.t[2] = a.t[2] + tt[2];
+                sim3_store(c, out + i * 8); break;
+            }
+            case OP_ADJ: case OP_ADJT: {
+                double Ad[49]; sim3_adj_matrix(sim3_load(x), Ad);
+                const double* a = Y + i * 7; double* o = out + i * 7;
+                for (int r = 0; r < 7; r++) {
+                    double sum = 0; for (int cc = 0; cc < 7; cc++) sum += (op == OP_ADJ ? Ad[r * 7 + cc] : Ad[cc * 7 + r]) * a[cc];
+                    o[r] = sum;
+                }
+                break;
+            }
+            case OP_ACT: { sim3 g = sim3_load(x); double* o = out + i * 3; rx_act(g.r, Y + i * 3, o); o[0] += g.t[0]; o[1] += g.t[1]; o[2] += g.t[2]; break; }
+            case OP_ACT4: {
+                sim3 g = sim3_load(x); const double* p = Y + i * 4; double* o = out + i * 4; rx_act(g.r, p, o);
+                o[0] += p[3] * g.t[0]; o[1] += p[3] * g.t[1]; o[2] += p[3] * g.t[2]; o[3] = p[3]; break;
+            }
+            case OP_MATRIX: {
+                sim3 g = sim3_load(x); double R[9]; q_mat(g.r.q, R); double* o = out + i * 16; memset(o, 0, sizeof(double) * 16);
+                for (int r = 0; r < 3; r++) { for (int cc = 0; cc < 3; cc++) o[r * 4 + cc] = g.r.s * R[r * 3 + cc]; o[r * 4 + 3] = g.t[r]; }
+                o[15] = 1; break;
+            }
+            case OP_PROJECTOR: { /* sim3.h orthogonal_projector, 8x8 */
+                sim3 g = sim3_load(x); double* o = out + i * 64; memset(o, 0, sizeof(double) * 64);
+                const double mt[3] = {-g.t[0], -g.t[1], -g.t[2]}; double H[9]; hat3(mt, H);
+                for (int r = 0; r < 3; r++) {
+                    o[r * 8 + r] = 1;
+                    for (int cc = 0; cc < 3; cc++) o[r * 8 + 3 + cc] = H[r * 3 + cc];
+                    o[r * 8 + 6] = g.t[r];
+                }
+                const double v[3] = {-g.r.q.x, -g.r.q.y, -g.r.q.z}; double Hq[9]; hat3(v, Hq);
+                for (int r = 0; r < 3; r++) for (int cc = 0; cc < 3; cc++) o[(3 + r) * 8 + 3 + cc] = 0.5 * ((r == cc ? g.r.q.w : 0) + Hq[r * 3 + cc]);
+                for (int cc = 0; cc < 3; cc++) o[6 * 8 + 3 + cc] = 0.5 * v[cc];
+                o[7 * 8 + 6] = g.r.s;
+                break;
+            }
+            case OP_JINV: {
+                double xi[7], J[49]; sim3_log(sim3_load(x), xi); sim3_left_jacobian_inverse(xi, J);
+                const double* a = Y + i * 7; double* o = out + i * 7;
+                for (int r = 0; r < 7; r++) { double sum = 0; for (int cc = 0; cc < 7; cc++) sum += J[r * 7 + cc] * a[cc]; o[r] = sum; }
+                break;
+            }
+            default: return -1;
+            }
+        }
+    }
+    return 0;
+}
+
 /*
  * Forward group operators on flat [n][dim] double arrays (lietorch.cpp:18-283
- * semantics; inputs already broadcast).  SO3 and SE3 only.
+ * semantics; inputs already broadcast).  RxSO3 / Sim3 go to
+ * lie_forward_scaled (rxso3.h / sim3.h).
  * Returns 0, or -1 for an unsupported (group, op).
  */
 int oracle_lie_forward(int op, int group, const double* X, const double* Y, double* out, int64_t n)
 {
+    if (group == G_RXSO3 || group == G_SIM3) return lie_forward_scaled(op, group, X, Y, out, n);
     if (group != G_SO3 && group != G_SE3) return -1;
     for (int64_t i = 0; i < n; i++) {
         if (group == G_SO3) {

@@ -162,14 +162,20 @@ def neighbors(ii, jj):
 
 
 # ----------------------------------------------------------------------------
-# lietorch (SO3 / SE3) and projective ops, in double
+# lietorch (SO3 / RxSO3 / SE3 / Sim3) and projective ops, in double
 # ----------------------------------------------------------------------------
+DIMS = {SO3: (3, 4), RXSO3: (4, 5), SE3: (6, 7), SIM3: (7, 8)}  # group -> (K, N)
 _OUT_DIM = {
     (SO3, "exp"): 4, (SO3, "log"): 3, (SO3, "inv"): 4, (SO3, "mul"): 4, (SO3, "adj"): 3, (SO3, "adjT"): 3,
     (SO3, "act"): 3, (SO3, "act4"): 4, (SO3, "matrix"): 16, (SO3, "projector"): 16, (SO3, "Jinv"): 3,
     (SE3, "exp"): 7, (SE3, "log"): 6, (SE3, "inv"): 7, (SE3, "mul"): 7, (SE3, "adj"): 6, (SE3, "adjT"): 6,
     (SE3, "act"): 3, (SE3, "act4"): 4, (SE3, "matrix"): 16, (SE3, "projector"): 49, (SE3, "Jinv"): 6,
 }
+for _g in (RXSO3, SIM3):
+    _K, _N = DIMS[_g]
+    _OUT_DIM.update({(_g, "exp"): _N, (_g, "log"): _K, (_g, "inv"): _N, (_g, "mul"): _N, (_g, "adj"): _K,
+                     (_g, "adjT"): _K, (_g, "act"): 3, (_g, "act4"): 4, (_g, "matrix"): 16, (_g, "projector"): _N * _N,
+                     (_g, "Jinv"): _K})
 
 
 def lie_forward(op, group, X, Y=None):
@@ -185,7 +191,7 @@ def lie_forward(op, group, X, Y=None):
     if op == "matrix":
         out = out.reshape(n, 4, 4)
     elif op == "projector":
-        d = 4 if group == SO3 else 7
+        d = DIMS[group][1]
         out = out.reshape(n, d, d)
     return out
 

@@ -11,7 +11,7 @@ What pins what
   ``dpvo/projective_ops.py``, ``dpvo/ba.py``) executed as imported code.  The
   reference's native modules cannot be built here (no nvcc, no Eigen; see
   SURVEY.md 8c), so ``lietorch_backends`` is served by the CPU oracle's
-  restatement of ``lietorch/include/{so3,se3}.h``, which is first checked by
+  restatement of ``lietorch/include/{so3,rxso3,se3,sim3}.h``, which is first checked by
   the reference's own property tests (``dpvo/lietorch/run_tests.py``
   test_exp_log / test_inv / test_adj / test_act, executed below).
   ``torch_scatter.scatter_sum`` (torch-scatter 2.1.2, absent) is restated as
@@ -117,7 +117,7 @@ def lietorch_fixtures(lie):
     sys.modules["gradcheck"].get_analytical_jacobian = None
     rt = importlib.import_module("run_tests")
     torch.manual_seed(0)
-    for G in [lie.SO3, lie.SE3]:
+    for G in [lie.SO3, lie.RxSO3, lie.SE3, lie.Sim3]:
         rt.test_exp_log(G, device="cpu")
         rt.test_inv(G, device="cpu")
         rt.test_adj(G, device="cpu")
@@ -126,7 +126,7 @@ def lietorch_fixtures(lie):
     # vectors through the reference Python surface (broadcasting + views)
     g = torch.Generator().manual_seed(1)
     out = {}
-    for name, G in [("SE3", lie.SE3), ("SO3", lie.SO3)]:
+    for name, G in [("SE3", lie.SE3), ("SO3", lie.SO3), ("RxSO3", lie.RxSO3), ("Sim3", lie.Sim3)]:
         D = G.manifold_dim
         a = 0.7 * torch.randn(5, 4, D, generator=g, dtype=torch.float64)
         b = 0.7 * torch.randn(5, 4, D, generator=g, dtype=torch.float64)
@@ -352,10 +352,17 @@ def neighbors_fixtures():
 
 
 if __name__ == "__main__":
+    # python make_golden.py [part ...]: parts lietorch, pops, ba, altcorr, neighbors (default: all)
     torch.set_num_threads(8)
+    parts = set(sys.argv[1:]) or {"lietorch", "pops", "ba", "altcorr", "neighbors"}
     pops, ba, lie = import_reference()
-    lietorch_fixtures(lie)
-    pops_fixtures(pops, lie)
-    ba_fixtures(ba, lie)
-    altcorr_fixtures()
-    neighbors_fixtures()
+    if "lietorch" in parts:
+        lietorch_fixtures(lie)
+    if "pops" in parts:
+        pops_fixtures(pops, lie)
+    if "ba" in parts:
+        ba_fixtures(ba, lie)
+    if "altcorr" in parts:
+        altcorr_fixtures()
+    if "neighbors" in parts:
+        neighbors_fixtures()

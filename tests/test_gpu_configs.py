@@ -140,6 +140,10 @@ def test_fused_update_operator_drift_on_outputs():
     and recorded in DESIGN.md; bars are the north star's 1e-3 relative."""
     from dpvo.net import Update
     a, b = _twin_trackers(7)
+    assert a.pg.net.dtype == torch.float32  # steady state: the fused path's input
+    calls = []
+    inner = Update._forward_fused
+    Update._forward_fused = lambda self, *x, **k: calls.append(1) or inner(self, *x, **k)
     # the network outputs first (same inputs)
     with torch.no_grad():
         outs = []
@@ -164,6 +168,8 @@ def test_fused_update_operator_drift_on_outputs():
             b.update()
     finally:
         Update.FUSED = True
+        Update._forward_fused = inner
+    assert len(calls) == 2  # the network call and a.update(); not b.update()
     torch.cuda.synchronize()
     t0, t1 = a.n - a.cfg.OPTIMIZATION_WINDOW, a.n
     pa, pb = a.pg.poses_[t0:t1].cpu().numpy(), b.pg.poses_[t0:t1].cpu().numpy()

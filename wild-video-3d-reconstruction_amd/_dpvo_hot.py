@@ -43,6 +43,8 @@ _SIGNATURES = {
     "dpvo_ba_workspace_bytes_ex": (_sz, [_i64, _i64, _ip, _ip]),
     "dpvo_ba_forward_ex": (_ip, [_vp, _vp, _i64, _ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _ip, _ip, _ip, _ip,
                                  _vp, _sz, _vp, _vp]),
+    "dpvo_ba_forward_csr": (_ip, [_vp, _vp, _i64, _ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _ip, _ip, _ip, _ip,
+                                  _vp, _vp, _vp, _vp, _sz, _vp, _vp]),
     "dpvo_reproject": (_ip, [_vp, _vp, _ip, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
     "dpvo_solve_system_assemble": (_ip, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _fp, _fp, _vp, _vp, _vp, _vp]),
     "dpvo_neighbors_workspace_bytes": (_sz, [_i64]),

@@ -1539,22 +1539,594 @@ static size_t nb_sort_temp_bytes(int64_t E)
     return bytes;
 }
 
+// ---------------------------------------------------------------------------
+// Deterministic dense path: DPVO's sliding window (N <= 12 optimised poses).
+//
+// One wave per unique patch (the groups of the kk group-by CSR, members in
+// ascending edge order), lanes = the patch's edges:
+//   * C, u and the patch's E row are wave sums of its edges -- no atomics;
+//   * the pose-block terms go into a per-wave LDS partial of H = B - E Q E^T
+//     (upper triangle) and g = v - E Q u: the shared-frame (i, i) block by wave
+//     sums, each edge's own (j, j) / (i, j) blocks by one ds_add per value
+//     (the edges of one patch have distinct target frames, so a ds_add never
+//     sees two lanes on one address; otherwise the patch runs lane by lane),
+//     and the patch's Schur term -Q e e^T over the poses it touches;
+//   * the next iteration's launch first applies this one's depth update
+//     dZ = Q (u - e . dX) to its patches (ba_cuda.cu:191-211, :523).
+// Per-wave partials are summed in a fixed order (workgroup, then a reduce
+// kernel), so every run gives the same bits.  The 6N x 6N (N <= 12) system
+// is factored by one workgroup, one barrier per column, the augmented row g
+// carried along (forward substitution for free), then one wave back-
+// substitutes and the poses are retracted.
+// ---------------------------------------------------------------------------
+constexpr int BD_NMAX = 12;
+constexpr int BD_N6MAX = 6 * BD_NMAX;     // 72
+constexpr int BD_WAVES = 4;
+constexpr int BD_GRID = 256;
+constexpr int BD_OWN = 11;                // augmented lower-triangle entries per solve thread (2700 / 256)
+
+struct BdLayout {
+    size_t hdr, gid, offs, perm, groups, gbws, gbws_bytes, Em, Cg, ug, Hpart, H, dX, total;
+    int64_t mu_max;
+    int n6, nup, ent;
+};
+
+static BdLayout bd_layout(int64_t E, int64_t num_patches, int N)
+{
+    BdLayout L{};
+    L.n6 = 6 * N;
+    L.nup = L.n6 * (L.n6 + 1) / 2;
+    L.ent = L.nup + L.n6;
+    L.mu_max = std::max<int64_t>(1, std::min(E, num_patches));
+    const size_t e = (size_t)std::max<int64_t>(E, 1);
+    size_t off = 0;
+    auto take = [&](size_t bytes) { size_t o = off; off += align256(bytes); return o; };
+    L.hdr = take(HDR_WORDS * 4);
+    L.gid = take(e * 8);
+    L.offs = take((e + 1) * 4);
+    L.perm = take(e * 4);
+    L.groups = take(8);
+    L.gbws_bytes = dpvo_group_by_workspace_bytes((int64_t)e);
+    L.gbws = take(L.gbws_bytes);
+    L.Em = take((size_t)L.mu_max * std::max(L.n6, 1) * 4);
+    L.Cg = take((size_t)L.mu_max * 4);
+    L.ug = take((size_t)L.mu_max * 4);
+    L.Hpart = take((size_t)BD_GRID * std::max(L.ent, 1) * 4);
+    L.H = take((size_t)std::max(L.ent, 1) * 4);
+    L.dX = take((size_t)std::max(L.n6, 1) * 4);
+    L.total = off;
+    return L;
+}
+
+struct BdParams {
+    float* poses;
+    float* patches;
+    const float* intrinsics;
+    const float* target;
+    const float* weight;
+    const float* lmbda;
+    const int64_t* ii;
+    const int64_t* jj;
+    const int64_t* kk;
+    int64_t num_patches, mu_max;
+    int P, t0, N, n6, nup, ent;
+    const int* offs;       // kk group-by CSR
+    const int* perm;
+    const int64_t* groups;
+    int* status;
+    float *Em, *Cg, *ug, *Hpart, *H, *dX;
+};
+
+// row-major upper triangle of the n6 x n6 system, a <= b
+__device__ __forceinline__ int tri_up(int a, int b, int n6) { return a * (2 * n6 - a + 1) / 2 + (b - a); }
+
+// all-lane sum kept in VGPRs (no readlanes: 33 sums in flight would not fit
+// in SGPRs); (r0 + r1) + (r2 + r3) of the four DPP-row sums, the same bits in
+// every lane since a + b == b + a
+__device__ __forceinline__ float wave64_allsum(float s)
+{
+    s = row16_sum(s);
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    return s;
+}
+
+__device__ __forceinline__ unsigned wave_or(unsigned v)
+{
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v |= __shfl_xor(v, o);
+    return v;
+}
+
+// per-edge Jacobians of one residual pair (ba_cuda.cu:254-290, 326-330)
+struct BdEdge {
+    float Ji[2][6], Jj[2][6], Jz[2], w[2], r[2];
+    int ix, jx;
+    bool iv, jv, self;
+};
+
+__device__ __forceinline__ void bd_edge(const BdParams& p, int64_t e, float px, float py, float dk, float fx, float fy,
+                                        float cx, float cy, BdEdge& o)
+{
+    const int64_t i_abs = p.ii[e], j_abs = p.jj[e];
+    const float* Pi = p.poses + i_abs * 7;
+    const float* Pj = p.poses + j_abs * 7;
+    const float ti[3] = {Pi[0], Pi[1], Pi[2]}, tj[3] = {Pj[0], Pj[1], Pj[2]};
+    const float qi[4] = {Pi[3], Pi[4], Pi[5], Pi[6]}, qj[4] = {Pj[3], Pj[4], Pj[5], Pj[6]};
+    float Xi[4], Xj[4], tij[3], qij[4];
+    Xi[0] = (px - cx) / fx;
+    Xi[1] = (py - cy) / fy;
+    Xi[2] = 1.0f;
+    Xi[3] = dk;
+    relSE3(ti, qi, tj, qj, tij, qij);
+    actSE3(tij, qij, Xi, Xj);
+    const float X = Xj[0], Y = Xj[1], Z = Xj[2], W = Xj[3];
+    const float d = (Z >= 0.2f) ? 1.0f / Z : 0.0f;
+    const float d2 = d * d;
+    const float x1 = fx * (X / Z) + cx, y1 = fy * (Y / Z) + cy;
+    const float rx = p.target[e * 2 + 0] - x1, ry = p.target[e * 2 + 1] - y1;
+    const bool in_bounds = (sqrtf(rx * rx + ry * ry) < 128.f) && (Z > 0.2f) && (x1 > -64.f) && (y1 > -64.f) &&
+                           (x1 < 2.f * cx + 64.f) && (y1 < 2.f * cy + 64.f);
+    const float mask = in_bounds ? 1.0f : 0.0f;
+    o.w[0] = mask * p.weight[e * 2 + 0];
+    o.w[1] = mask * p.weight[e * 2 + 1];
+    o.r[0] = rx;
+    o.r[1] = ry;
+    o.Jz[0] = fx * (tij[0] * d - tij[2] * (X * d2));
+    o.Jz[1] = fy * (tij[1] * d - tij[2] * (Y * d2));
+    const float a[6] = {fx * W * d, 0.f, fx * -X * W * d2, fx * -X * Y * d2, fx * (1.f + X * X * d2), fx * -Y * d};
+    const float b[6] = {0.f, fy * W * d, fy * -Y * W * d2, fy * (-1.f - Y * Y * d2), fy * (X * Y * d2), fy * X * d};
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        o.Jj[0][t] = a[t];
+        o.Jj[1][t] = b[t];
+    }
+    adjSE3(tij, qij, o.Jj[0], o.Ji[0]);
+    adjSE3(tij, qij, o.Jj[1], o.Ji[1]);
+    o.ix = (int)(i_abs - p.t0);
+    o.jx = (int)(j_abs - p.t0);
+    o.iv = o.ix >= 0 && o.ix < p.N;
+    o.jv = o.jx >= 0 && o.jx < p.N;
+    o.self = o.iv && o.jv && o.ix == o.jx;
+}
+
+// the terms of one edge on the patch's own frame i (a self edge folds its
+// j terms in, ba_cuda.cu:294-322): (i, i) upper block, v_i, E_i
+__device__ __forceinline__ void bd_iterms(const BdEdge& o, float bii[21], float vi[6], float Ei[6])
+{
+    int u = 0;
+#pragma unroll
+    for (int a = 0; a < 6; a++)
+#pragma unroll
+        for (int b = a; b < 6; b++, u++) {
+            float s = 0.f;
+#pragma unroll
+            for (int row = 0; row < 2; row++) {
+                if (o.self)
+                    s += o.w[row] * (o.Ji[row][a] * o.Ji[row][b] + o.Jj[row][a] * o.Jj[row][b] -
+                                     o.Ji[row][a] * o.Jj[row][b] - o.Jj[row][a] * o.Ji[row][b]);
+                else
+                    s += o.w[row] * o.Ji[row][a] * o.Ji[row][b];
+            }
+            bii[u] = o.iv ? s : 0.f;
+        }
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        float v = -o.w[0] * o.r[0] * o.Ji[0][t] - o.w[1] * o.r[1] * o.Ji[1][t];
+        float e = -o.w[0] * o.Jz[0] * o.Ji[0][t] - o.w[1] * o.Jz[1] * o.Ji[1][t];
+        if (o.self) {
+            v += o.w[0] * o.r[0] * o.Jj[0][t] + o.w[1] * o.r[1] * o.Jj[1][t];
+            e += o.w[0] * o.Jz[0] * o.Jj[0][t] + o.w[1] * o.Jz[1] * o.Jj[1][t];
+        }
+        vi[t] = o.iv ? v : 0.f;
+        Ei[t] = o.iv ? e : 0.f;
+    }
+}
+
+// the edge's own target-frame terms, added to the wave's partial and E row
+__device__ __forceinline__ void bd_jterms_add(const BdEdge& o, float* part, float* ev, int n6, int nup)
+{
+    if (!o.jv || o.self) return;
+    const int j6 = 6 * o.jx;
+#pragma unroll
+    for (int a = 0; a < 6; a++) {
+#pragma unroll
+        for (int b = a; b < 6; b++)
+            atomicAdd(&part[tri_up(j6 + a, j6 + b, n6)], o.w[0] * o.Jj[0][a] * o.Jj[0][b] + o.w[1] * o.Jj[1][a] * o.Jj[1][b]);
+        atomicAdd(&part[nup + j6 + a], o.w[0] * o.r[0] * o.Jj[0][a] + o.w[1] * o.r[1] * o.Jj[1][a]);
+        atomicAdd(&ev[j6 + a], o.w[0] * o.Jz[0] * o.Jj[0][a] + o.w[1] * o.Jz[1] * o.Jj[1][a]);
+    }
+    if (o.iv) {
+        const int i6 = 6 * o.ix;
+        const bool up = o.ix < o.jx;
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+            for (int b = 0; b < 6; b++) {
+                const float s = up ? -(o.w[0] * o.Ji[0][a] * o.Jj[0][b] + o.w[1] * o.Ji[1][a] * o.Jj[1][b])
+                                   : -(o.w[0] * o.Jj[0][a] * o.Ji[0][b] + o.w[1] * o.Jj[1][a] * o.Ji[1][b]);
+                atomicAdd(&part[up ? tri_up(i6 + a, j6 + b, n6) : tri_up(j6 + a, i6 + b, n6)], s);
+            }
+    }
+}
+
+template <bool APPLY, bool HESS>
+__global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
+{
+    extern __shared__ __attribute__((aligned(16))) float sm[];
+    if (*(volatile int*)p.status != 0) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int n6 = p.n6, nup = p.nup, ent = p.ent, N = p.N;
+    const bool pose_terms = HESS && N > 0;
+    float* part = sm + wave * ent;
+    float* ev = sm + BD_WAVES * ent + wave * BD_N6MAX;
+    if (pose_terms)
+        for (int i = threadIdx.x; i < BD_WAVES * ent; i += blockDim.x) sm[i] = 0.f;
+    __syncthreads();
+    const int64_t G = min(*p.groups, p.mu_max);
+    const float lm = p.lmbda[0];
+    const float fx = p.intrinsics[0], fy = p.intrinsics[1], cx = p.intrinsics[2], cy = p.intrinsics[3];
+    const int64_t PP = (int64_t)p.P * p.P, centre = (p.P / 2) * p.P + p.P / 2;
+    const float dx0 = (APPLY && lane < n6) ? p.dX[lane] : 0.f;
+    const float dx1 = (APPLY && lane + 64 < n6) ? p.dX[lane + 64] : 0.f;
+
+    for (int64_t g = (int64_t)blockIdx.x * BD_WAVES + wave; g < G; g += (int64_t)gridDim.x * BD_WAVES) {
+        const int start = p.offs[g], cnt = p.offs[g + 1] - start;
+        const int64_t k = p.kk[p.perm[start]];
+        if (k < 0 || k >= p.num_patches) {
+            if (lane == 0) atomicExch(p.status, -1);  // patch index out of range
+            continue;
+        }
+        float* pd = p.patches + (k * 3 + 2) * PP;
+        float dk;
+        if (APPLY) {
+            // this patch's depth update from the previous iteration's solve
+            const float Q = 1.0f / (p.Cg[g] + lm);
+            float s = 0.f;
+            if (N > 0) {
+                const float* Er = p.Em + g * n6;
+                s = wave64_sum((lane < n6 ? Er[lane] * dx0 : 0.f) + (lane + 64 < n6 ? Er[lane + 64] * dx1 : 0.f));
+            }
+            float d = pd[0] + Q * (p.ug[g] - s);
+            d = (d > 20.f) ? 1.0f : d;
+            d = fmaxf(d, 1e-4f);
+            if (lane < PP) pd[lane] = d;
+            dk = d;
+        } else {
+            dk = pd[centre];
+        }
+        if (!HESS) continue;
+        const float px = p.patches[(k * 3 + 0) * PP + centre], py = p.patches[(k * 3 + 1) * PP + centre];
+
+        if (pose_terms) {
+            if (lane < n6) ev[lane] = 0.f;
+            if (lane + 64 < n6) ev[lane + 64] = 0.f;
+        }
+        float Ck = 0.f, uk = 0.f;
+        unsigned touched = 0;  // window poses this patch's E row touches
+        wave_lds_fence();
+        for (int c0 = 0; c0 < cnt; c0 += 64) {
+            const bool on = lane < cnt - c0;
+            const int64_t e = on ? p.perm[start + c0 + lane] : p.perm[start];
+            BdEdge o;
+            bd_edge(p, e, px, py, dk, fx, fy, cx, cy, o);
+            if (!on) { o.w[0] = o.w[1] = 0.f; o.iv = o.jv = o.self = false; }
+            float cl = 0.f, ul = 0.f;
+#pragma unroll
+            for (int row = 0; row < 2; row++) {
+                cl += o.w[row] * o.Jz[row] * o.Jz[row];
+                ul += o.w[row] * o.r[row] * o.Jz[row];
+            }
+            Ck += wave64_sum(cl);
+            uk += wave64_sum(ul);
+            if (!pose_terms) continue;
+            touched |= wave_or((o.iv ? 1u << o.ix : 0u) | (o.jv ? 1u << o.jx : 0u));
+            // one pass when every edge of the patch has the same frame i (DPVO:
+            // the patch's own frame) and distinct target frames; otherwise one
+            // lane per pass, in edge order
+            const uint64_t ivm0 = __ballot(o.iv);
+            const int ix0 = __shfl(o.ix, ivm0 ? __ffsll((unsigned long long)ivm0) - 1 : 0);
+            bool mixed = __ballot(o.iv && o.ix != ix0) != 0;
+            const bool jt = o.jv && !o.self;
+            for (int q = 0; q < N && !mixed; q++)
+                mixed = __popcll(__ballot(jt && o.jx == q)) > 1;
+            const int passes = mixed ? 64 : 1;
+            for (int ps = 0; ps < passes; ps++) {
+                const bool act = !mixed || lane == ps;
+                const uint64_t ivm = __ballot(act && o.iv);
+                if (ivm) {
+                    // the shared-frame terms: wave sums, entry t added by lane t
+                    const int i6 = 6 * __shfl(o.ix, __ffsll((unsigned long long)ivm) - 1);
+                    float bii[21], vi[6], Ei[6];
+                    bd_iterms(o, bii, vi, Ei);
+                    float val = 0.f;
+                    int u = 0;
+#pragma unroll
+                    for (int a = 0; a < 6; a++)
+#pragma unroll
+                        for (int b = a; b < 6; b++, u++) {
+                            const float sum = wave64_allsum(act ? bii[u] : 0.f);
+                            if (lane == u) val = sum;
+                        }
+#pragma unroll
+                    for (int t = 0; t < 6; t++) {
+                        const float sv = wave64_allsum(act ? vi[t] : 0.f);
+                        const float se = wave64_allsum(act ? Ei[t] : 0.f);
+                        if (lane == 21 + t) val = sv;
+                        if (lane == 27 + t) val = se;
+                    }
+                    int addr = -1;
+                    float* base = part;
+                    if (lane < 21) {
+                        int a = 0, r = lane;
+                        while (r >= 6 - a) { r -= 6 - a; a++; }
+                        addr = tri_up(i6 + a, i6 + a + r, n6);
+                    } else if (lane < 27) {
+                        addr = nup + i6 + lane - 21;
+                    } else if (lane < 33) {
+                        addr = i6 + lane - 27;
+                        base = ev;
+                    }
+                    if (addr >= 0) atomicAdd(&base[addr], val);
+                }
+                if (act) bd_jterms_add(o, part, ev, n6, nup);
+                wave_lds_fence();
+            }
+        }
+        if (!pose_terms) {
+            if (lane == 0) { p.Cg[g] = Ck; p.ug[g] = uk; }
+            continue;
+        }
+        wave_lds_fence();
+        // the patch's E row, C, u (the next launch's depth update reads them)
+        const float e0 = lane < n6 ? ev[lane] : 0.f, e1 = lane + 64 < n6 ? ev[lane + 64] : 0.f;
+        float* Er = p.Em + g * n6;
+        if (lane < n6) Er[lane] = e0;
+        if (lane + 64 < n6) Er[lane + 64] = e1;
+        if (lane == 0) { p.Cg[g] = Ck; p.ug[g] = uk; }
+        // Schur term: H -= Q e e^T (upper), g -= Q u e, over the touched poses
+        const float Q = 1.0f / (Ck + lm);
+        const float qu = Q * uk;
+        for (unsigned tm = touched; tm; tm &= tm - 1) {
+            const int pa = __ffs(tm) - 1;
+#pragma unroll
+            for (int t = 0; t < 6; t++) {
+                const int a = 6 * pa + t;
+                const float qa = Q * ev[a];
+                if (lane >= a && lane < n6) atomicAdd(&part[tri_up(a, lane, n6)], -qa * e0);
+                if (lane + 64 >= a && lane + 64 < n6) atomicAdd(&part[tri_up(a, lane + 64, n6)], -qa * e1);
+                if (lane == 0) part[nup + a] -= qu * ev[a];
+            }
+        }
+        wave_lds_fence();
+    }
+    if (!pose_terms) return;
+    // the workgroup's partial: its waves' partials summed in wave order
+    __syncthreads();
+    float* dst = p.Hpart + (int64_t)blockIdx.x * ent;
+    for (int i = threadIdx.x; i < ent; i += blockDim.x) {
+        float s = sm[i];
+#pragma unroll
+        for (int w = 1; w < BD_WAVES; w++) s += sm[w * ent + i];
+        dst[i] = s;
+    }
+}
+
+// H = sum of the patch kernel's workgroup partials, fixed order
+__global__ __launch_bounds__(1024) void bd_reduce_kernel(BdParams p, int nparts)
+{
+    __shared__ float red[16][64];
+    if (*(volatile int*)p.status != 0) return;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + lane;
+    float s = 0.f;
+    if (i < p.ent) {
+#pragma unroll 4
+        for (int b = wave; b < nparts; b += 16) s += p.Hpart[(int64_t)b * p.ent + i];
+    }
+    red[wave][lane] = s;
+    __syncthreads();
+    if (wave == 0 && i < p.ent) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < 16; w++) t += red[w][lane];
+        p.H[i] = t;
+    }
+}
+
+// damping S += diag(1e-4 S + 1) (ba_cuda.cu:517-518), fp32 Cholesky of the
+// augmented [S; g^T] (one barrier per column), back substitution, retraction
+__global__ __launch_bounds__(256) void bd_solve_kernel(BdParams p)
+{
+    __shared__ float colbuf[2][BD_N6MAX + 1];
+    __shared__ float Lm[(BD_N6MAX + 1) * BD_N6MAX];
+    __shared__ float xs[BD_N6MAX];
+    if (*(volatile int*)p.status != 0) return;
+    const int n = p.n6, tid = threadIdx.x;
+    const int ntri = n * (n + 1) / 2, ne = ntri + n;
+    float a[BD_OWN];
+    int rr[BD_OWN], cc[BD_OWN];
+#pragma unroll
+    for (int s = 0; s < BD_OWN; s++) {
+        const int t = tid + 256 * s;
+        int r = -1, c = -1;
+        float v = 0.f;
+        if (t < ntri) {
+            r = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
+            while (r * (r + 1) / 2 > t) r--;
+            while ((r + 1) * (r + 2) / 2 <= t) r++;
+            c = t - r * (r + 1) / 2;
+            v = p.H[tri_up(c, r, n)];
+            if (r == c) v += 1e-4f * v + 1.0f;
+        } else if (t < ne) {
+            r = n;
+            c = t - ntri;
+            v = p.H[p.nup + c];
+        }
+        rr[s] = r;
+        cc[s] = c;
+        a[s] = v;
+        if (c == 0) colbuf[0][r] = v;
+    }
+    // clamped copies of the owned (row, column) pairs: the column reads below
+    // are issued together, unconditionally, and waited for once per column
+    int rq[BD_OWN], cq[BD_OWN];
+#pragma unroll
+    for (int s = 0; s < BD_OWN; s++) {
+        rq[s] = rr[s] < 0 ? 0 : rr[s];
+        cq[s] = cc[s] < 0 ? 0 : cc[s];
+    }
+    int fail = 0;
+    for (int j = 0; j < n; j++) {
+        __syncthreads();
+        const float* cur = colbuf[j & 1];
+        float* nxt = colbuf[(j + 1) & 1];
+        float vr[BD_OWN], vc[BD_OWN];
+#pragma unroll
+        for (int s = 0; s < BD_OWN; s++) {
+            vr[s] = cur[rq[s]];
+            vc[s] = cur[cq[s]];
+        }
+        const float d = cur[j];
+        if (!(d > 0.f)) {
+            fail = j + 1;
+            break;
+        }
+        const float invd = 1.0f / d, invl = 1.0f / sqrtf(d);
+#pragma unroll
+        for (int s = 0; s < BD_OWN; s++) {
+            const int c = cc[s];
+            const float na = a[s] - vr[s] * vc[s] * invd;
+            if (c == j) Lm[rq[s] * n + j] = a[s] * invl;
+            a[s] = c > j ? na : a[s];
+            if (c == j + 1) nxt[rq[s]] = a[s];
+        }
+    }
+    if (fail) {
+        if (tid == 0) atomicExch(p.status, fail);
+        return;
+    }
+    __syncthreads();
+    // L^T x = z, z = row n of the augmented factor; lane c holds x_c / z_c
+    if (tid < 64) {
+        float z0 = tid < n ? Lm[n * n + tid] : 0.f, z1 = tid + 64 < n ? Lm[n * n + tid + 64] : 0.f;
+        for (int j = n - 1; j >= 0; j--) {
+            const float zj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(j < 64 ? z0 : z1), j & 63));
+            const float xj = zj / Lm[j * n + j];
+            if (tid < j) z0 -= Lm[j * n + tid] * xj;
+            if (tid + 64 < j) z1 -= Lm[j * n + tid + 64] * xj;
+            if (tid == (j & 63)) {
+                if (j < 64) z0 = xj;
+                else z1 = xj;
+            }
+        }
+        if (tid < n) xs[tid] = z0;
+        if (tid + 64 < n) xs[tid + 64] = z1;
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) p.dX[i] = xs[i];
+    if (tid < p.N) {
+        float* P = p.poses + (int64_t)(p.t0 + tid) * 7;
+        const float t0v[3] = {P[0], P[1], P[2]}, q0v[4] = {P[3], P[4], P[5], P[6]};
+        float xi[6], t1v[3], q1v[4];
+        for (int k = 0; k < 6; k++) xi[k] = xs[6 * tid + k];
+        retrSE3(xi, t0v, q0v, t1v, q1v);
+        P[0] = t1v[0]; P[1] = t1v[1]; P[2] = t1v[2];
+        P[3] = q1v[0]; P[4] = q1v[1]; P[5] = q1v[2]; P[6] = q1v[3];
+    }
+}
+
+static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, const int* csr_offs,
+                          const int* csr_perm, const int64_t* csr_groups, int iterations, hipStream_t s)
+{
+    if (csr_offs && csr_perm && csr_groups) {
+        p.offs = csr_offs;
+        p.perm = csr_perm;
+        p.groups = csr_groups;
+    } else {
+        int bits = 1;
+        while (bits < 64 && (int64_t(1) << bits) < p.num_patches) bits++;
+        if (dpvo_group_by(p.kk, E, bits, (int64_t*)(ws + L.gid), (int*)(ws + L.offs), (int*)(ws + L.perm),
+                          (int64_t*)(ws + L.groups), ws + L.gbws, L.gbws_bytes, s) != 0)
+            return -2;
+        p.offs = (const int*)(ws + L.offs);
+        p.perm = (const int*)(ws + L.perm);
+        p.groups = (const int64_t*)(ws + L.groups);
+    }
+    p.Em = (float*)(ws + L.Em);
+    p.Cg = (float*)(ws + L.Cg);
+    p.ug = (float*)(ws + L.ug);
+    p.Hpart = (float*)(ws + L.Hpart);
+    p.H = (float*)(ws + L.H);
+    p.dX = (float*)(ws + L.dX);
+    const size_t lds = (size_t)(BD_WAVES * (p.N > 0 ? L.ent : 0) + BD_WAVES * BD_N6MAX) * 4;
+    const unsigned gR = (unsigned)((L.ent + 63) / 64);
+    for (int it = 0; it < iterations; it++) {
+        if (it == 0)
+            hipLaunchKernelGGL((bd_patch_kernel<false, true>), dim3(BD_GRID), dim3(64 * BD_WAVES), lds, s, p);
+        else
+            hipLaunchKernelGGL((bd_patch_kernel<true, true>), dim3(BD_GRID), dim3(64 * BD_WAVES), lds, s, p);
+        if (p.N > 0) {
+            hipLaunchKernelGGL(bd_reduce_kernel, dim3(gR), dim3(1024), 0, s, p, BD_GRID);
+            hipLaunchKernelGGL(bd_solve_kernel, dim3(1), dim3(256), 0, s, p);
+        }
+        DPVO_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL((bd_patch_kernel<true, false>), dim3(BD_GRID), dim3(64 * BD_WAVES), 0, s, p);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
 }  // namespace dpvo
 
 using namespace dpvo;
 
 static bool ba_sparse(int N, int flags) { return N > 0 && ((flags & DPVO_BA_SPARSE) || N > BA_SOLVE_NMAX); }
+static bool ba_det(int N, int flags) { return !ba_sparse(N, flags) && N <= BD_NMAX && !(flags & DPVO_BA_ATOMIC); }
 
 extern "C" size_t dpvo_ba_workspace_bytes_ex(int64_t num_edges, int64_t num_patches, int num_opt_poses, int flags)
 {
     const int N = num_opt_poses < 0 ? 0 : num_opt_poses;
     if (ba_sparse(N, flags)) return bs_layout(num_edges, num_patches, N).total;
+    if (ba_det(N, flags)) return bd_layout(num_edges, num_patches, N).total;
     return ba_layout(num_edges, num_patches, N).total;
 }
 
 extern "C" size_t dpvo_ba_workspace_bytes(int64_t num_edges, int64_t num_patches, int num_opt_poses)
 {
     return dpvo_ba_workspace_bytes_ex(num_edges, num_patches, num_opt_poses, 0);
+}
+
+extern "C" int dpvo_ba_forward_csr(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
+                                   const float* target, const float* weight, const float* lmbda, const int64_t* ii,
+                                   const int64_t* jj, const int64_t* kk, int64_t num_edges, int t0, int t1,
+                                   int iterations, int flags, const int* csr_offs, const int* csr_perm,
+                                   const int64_t* csr_groups, void* workspace, size_t workspace_bytes, int* status,
+                                   void* stream)
+{
+    const int N = t1 - t0;
+    DPVO_CHECK_ARG(N >= 0, "t1 must be >= t0");
+    DPVO_CHECK_ARG(N <= BS_NMAX, "more than 32767 optimised poses");
+    DPVO_CHECK_ARG(P >= 1 && num_patches >= 0 && iterations >= 0, "bad sizes");
+    hipStream_t s = as_stream(stream);
+    char* ws = (char*)workspace;
+    if (ba_det(N, flags)) {
+        const BdLayout L = bd_layout(num_edges, num_patches, N);
+        DPVO_CHECK_ARG(workspace && workspace_bytes >= L.total, "workspace too small");
+        DPVO_CHECK_ARG(P * P <= 64, "patch size above 8");
+        DPVO_CHECK_ARG(num_edges < 0x7fffffff, "too many edges");
+        BdParams p{};
+        p.poses = poses; p.patches = patches; p.intrinsics = intrinsics; p.target = target; p.weight = weight;
+        p.lmbda = lmbda; p.ii = ii; p.jj = jj; p.kk = kk; p.num_patches = num_patches; p.mu_max = L.mu_max;
+        p.P = P; p.t0 = t0; p.N = N; p.n6 = L.n6; p.nup = L.nup; p.ent = L.ent;
+        p.status = status ? status : (int*)(ws + L.hdr) + HDR_STATUS;
+        DPVO_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int), s));
+        if (num_edges == 0 || iterations == 0) return 0;
+        return ba_forward_det(p, ws, L, num_edges, csr_offs, csr_perm, csr_groups, iterations, s);
+    }
+    return dpvo_ba_forward_ex(poses, patches, num_patches, P, intrinsics, target, weight, lmbda, ii, jj, kk,
+                              num_edges, t0, t1, iterations, flags | DPVO_BA_ATOMIC, workspace, workspace_bytes, status,
+                              stream);
 }
 
 extern "C" int dpvo_ba_forward_ex(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
@@ -1567,6 +2139,10 @@ extern "C" int dpvo_ba_forward_ex(float* poses, float* patches, int64_t num_patc
     DPVO_CHECK_ARG(N >= 0, "t1 must be >= t0");
     DPVO_CHECK_ARG(N <= BS_NMAX, "more than 32767 optimised poses");
     DPVO_CHECK_ARG(P >= 1 && num_patches >= 0 && iterations >= 0, "bad sizes");
+    if (ba_det(N, flags))
+        return dpvo_ba_forward_csr(poses, patches, num_patches, P, intrinsics, target, weight, lmbda, ii, jj, kk,
+                                   num_edges, t0, t1, iterations, flags, nullptr, nullptr, nullptr, workspace,
+                                   workspace_bytes, status, stream);
     hipStream_t s = as_stream(stream);
     char* ws = (char*)workspace;
     BaParams p{};

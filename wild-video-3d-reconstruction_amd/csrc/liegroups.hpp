@@ -1,10 +1,11 @@
-// liegroups.hpp -- SO3 / SE3 on the device, no Eigen.
+// liegroups.hpp -- SO3 / RxSO3 / SE3 / Sim3 on the device, no Eigen.
 //
 // Restates the group algebra of the reference's lietorch headers
-// (dpvo/lietorch/include/so3.h, se3.h) with explicit small-matrix code:
-// element data [qx,qy,qz,qw] (SO3) and [tx,ty,tz,qx,qy,qz,qw] (SE3); the
-// quaternion is normalised on every load exactly as SO3(const Scalar*) does
-// (so3.h:47-49); EPS = 1e-6 small-angle branches (common.h:7).
+// (dpvo/lietorch/include/so3.h, rxso3.h, se3.h, sim3.h) with explicit
+// small-matrix code: element data [qx,qy,qz,qw] (SO3), [qx,qy,qz,qw,s]
+// (RxSO3), [tx,ty,tz,qx,qy,qz,qw] (SE3) and [tx,ty,tz,qx,qy,qz,qw,s] (Sim3);
+// the quaternion is normalised on every load exactly as SO3(const Scalar*)
+// does (so3.h:47-49); EPS = 1e-6 small-angle branches (common.h:7).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -348,6 +349,332 @@ struct SE3 {
         for (int i = 0; i < 3; i++)
             for (int j = 0; j < 3; j++) { J[i][j] = i == j ? p[3] : (T)0; J[i][j + 3] = H[i][j]; }
         for (int j = 0; j < 6; j++) J[3][j] = 0;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// small dense helpers for the 4x4 / 7x7 tangent-space matrices
+template <typename T, int K>
+__device__ __forceinline__ void mmk(const T A[K][K], const T B[K][K], T C[K][K])
+{
+    T R[K][K];
+    for (int i = 0; i < K; i++)
+        for (int j = 0; j < K; j++) {
+            T s = 0;
+            for (int k = 0; k < K; k++) s += A[i][k] * B[k][j];
+            R[i][j] = s;
+        }
+    for (int i = 0; i < K; i++)
+        for (int j = 0; j < K; j++) C[i][j] = R[i][j];
+}
+template <typename T>
+__device__ __forceinline__ void inv3(const T A[3][3], T B[3][3])  // cofactors / determinant (Eigen's 3x3 inverse)
+{
+    const T c00 = A[1][1] * A[2][2] - A[1][2] * A[2][1];
+    const T c01 = A[1][2] * A[2][0] - A[1][0] * A[2][2];
+    const T c02 = A[1][0] * A[2][1] - A[1][1] * A[2][0];
+    const T det = A[0][0] * c00 + A[0][1] * c01 + A[0][2] * c02;
+    const T id = (T)1 / det;
+    B[0][0] = c00 * id; B[0][1] = (A[0][2] * A[2][1] - A[0][1] * A[2][2]) * id; B[0][2] = (A[0][1] * A[1][2] - A[0][2] * A[1][1]) * id;
+    B[1][0] = c01 * id; B[1][1] = (A[0][0] * A[2][2] - A[0][2] * A[2][0]) * id; B[1][2] = (A[0][2] * A[1][0] - A[0][0] * A[1][2]) * id;
+    B[2][0] = c02 * id; B[2][1] = (A[0][1] * A[2][0] - A[0][0] * A[2][1]) * id; B[2][2] = (A[0][0] * A[1][1] - A[0][1] * A[1][0]) * id;
+}
+
+// ---------------------------------------------------------------------------
+// RxSO3: rotation and positive scale, data [qx,qy,qz,qw,s] (rxso3.h)
+template <typename T>
+struct RxSO3 {
+    static constexpr int K = 4, N = 5;
+    SO3<T> so3;
+    T s;
+
+    __device__ static RxSO3 load(const T* d) { RxSO3 g; g.so3 = SO3<T>::load(d); g.s = d[4]; return g; }
+    __device__ void store(T* d) const { so3.store(d); d[4] = s; }
+    __device__ RxSO3 inv() const { RxSO3 g; g.so3 = so3.inv(); g.s = (T)1 / s; return g; }
+    __device__ RxSO3 mul(const RxSO3& o) const { RxSO3 g; g.so3 = so3.mul(o.so3); g.s = s * o.s; return g; }
+    __device__ void act(const T* p, T* o) const
+    {
+        so3.act(p, o);
+        o[0] *= s; o[1] *= s; o[2] *= s;
+    }
+    __device__ void act4(const T* p, T* o) const { act(p, o); o[3] = p[3]; }
+    __device__ void Adj(T A[4][4]) const  // rotation block, scale untouched
+    {
+        T R[3][3];
+        qmat(so3.q, R);
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 4; j++) A[i][j] = (i < 3 && j < 3) ? R[i][j] : (T)(i == j);
+    }
+    __device__ void matrix4(T M[4][4]) const
+    {
+        T R[3][3];
+        qmat(so3.q, R);
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 4; j++) M[i][j] = (i < 3 && j < 3) ? s * R[i][j] : (T)(i == j);
+    }
+    __device__ void projector(T* P) const  // rxso3.h orthogonal_projector, 5x5 row-major
+    {
+        T Pq[16];
+        so3.projector(Pq);
+        for (int i = 0; i < 25; i++) P[i] = 0;
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 3; j++) P[i * 5 + j] = Pq[i * 4 + j];
+        P[4 * 5 + 3] = s;
+    }
+    __device__ void Log(T* ps) const
+    {
+        so3.Log(ps);
+        ps[3] = log(s);
+    }
+    __device__ static RxSO3 Exp(const T* ps)
+    {
+        RxSO3 g;
+        g.so3 = SO3<T>::Exp(ps);
+        g.s = exp(ps[3]);
+        return g;
+    }
+    // W(phi, sigma): the translation part of Sim3's exp (rxso3.h calcW)
+    __device__ static void calcW(const T* ps, T W[3][3])
+    {
+        T Ph[3][3], Ph2[3][3];
+        hat(ps, Ph);
+        mm3(Ph, Ph, Ph2);
+        const T sigma = ps[3], theta = sqrt(ps[0] * ps[0] + ps[1] * ps[1] + ps[2] * ps[2]), sc = exp(sigma);
+        const T eps = lie_eps<T>(), one = 1, half = (T)0.5;
+        T A, B, C;
+        if (fabs(sigma) < eps) {
+            C = one;
+            if (fabs(theta) < eps) {
+                A = half;
+                B = (T)(1. / 6.);
+            } else {
+                const T t2 = theta * theta;
+                A = (one - cos(theta)) / t2;
+                B = (theta - sin(theta)) / (t2 * theta);
+            }
+        } else {
+            C = (sc - one) / sigma;
+            if (fabs(theta) < eps) {
+                const T s2 = sigma * sigma;
+                A = ((sigma - one) * sc + one) / s2;
+                B = (sc * half * s2 + sc - one - sigma * sc) / (s2 * sigma);
+            } else {
+                const T t2 = theta * theta, a = sc * sin(theta), b = sc * cos(theta), c = t2 + sigma * sigma;
+                A = (a * sigma + (one - b) * theta) / (theta * c);
+                B = (C - ((b - one) * sigma + a * theta) / c) * one / t2;
+            }
+        }
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) W[i][j] = A * Ph[i][j] + B * Ph2[i][j] + (i == j ? C : (T)0);
+    }
+    __device__ static void left_jacobian(const T* ps, T J[4][4])
+    {
+        T Js[3][3];
+        SO3<T>::left_jacobian(ps, Js);
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 4; j++) J[i][j] = (i < 3 && j < 3) ? Js[i][j] : (T)(i == j);
+    }
+    __device__ static void left_jacobian_inverse(const T* ps, T J[4][4])
+    {
+        T Js[3][3];
+        SO3<T>::left_jacobian_inverse(ps, Js);
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 4; j++) J[i][j] = (i < 3 && j < 3) ? Js[i][j] : (T)(i == j);
+    }
+    __device__ static void ad(const T* a, T A[4][4])
+    {
+        T H[3][3];
+        hat(a, H);
+        for (int i = 0; i < 4; i++)
+            for (int j = 0; j < 4; j++) A[i][j] = (i < 3 && j < 3) ? H[i][j] : (T)0;
+    }
+    __device__ static void act_jacobian(const T* p, T J[3][4])
+    {
+        const T m[3] = {-p[0], -p[1], -p[2]};
+        T H[3][3];
+        hat(m, H);
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) J[i][j] = H[i][j];
+            J[i][3] = p[i];
+        }
+    }
+    __device__ static void act4_jacobian(const T* p, T J[4][4])
+    {
+        const T m[3] = {-p[0], -p[1], -p[2]};
+        T H[3][3];
+        hat(m, H);
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) J[i][j] = H[i][j];
+            J[i][3] = p[i];
+        }
+        for (int j = 0; j < 4; j++) J[3][j] = 0;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Sim3: similarity, data [tx,ty,tz,qx,qy,qz,qw,s] (sim3.h)
+template <typename T>
+struct Sim3 {
+    static constexpr int K = 7, N = 8;
+    RxSO3<T> r;
+    T t[3];
+
+    __device__ static Sim3 load(const T* d)
+    {
+        Sim3 g;
+        g.t[0] = d[0]; g.t[1] = d[1]; g.t[2] = d[2];
+        g.r = RxSO3<T>::load(d + 3);
+        return g;
+    }
+    __device__ void store(T* d) const { d[0] = t[0]; d[1] = t[1]; d[2] = t[2]; r.store(d + 3); }
+    __device__ Sim3 inv() const
+    {
+        Sim3 g;
+        g.r = r.inv();
+        T tt[3];
+        g.r.act(t, tt);
+        g.t[0] = -tt[0]; g.t[1] = -tt[1]; g.t[2] = -tt[2];
+        return g;
+    }
+    __device__ Sim3 mul(const Sim3& o) const
+    {
+        Sim3 g;
+        g.r = r.mul(o.r);
+        T tt[3];
+        r.act(o.t, tt);
+        g.t[0] = t[0] + tt[0]; g.t[1] = t[1] + tt[1]; g.t[2] = t[2] + tt[2];
+        return g;
+    }
+    __device__ void act(const T* p, T* o) const
+    {
+        r.act(p, o);
+        o[0] += t[0]; o[1] += t[1]; o[2] += t[2];
+    }
+    __device__ void act4(const T* p, T* o) const
+    {
+        T q[3];
+        r.act(p, q);
+        o[0] = q[0] + p[3] * t[0];
+        o[1] = q[1] + p[3] * t[1];
+        o[2] = q[2] + p[3] * t[2];
+        o[3] = p[3];
+    }
+    __device__ void matrix4(T M[4][4]) const
+    {
+        r.matrix4(M);
+        M[0][3] = t[0]; M[1][3] = t[1]; M[2][3] = t[2];
+    }
+    __device__ void Adj(T A[7][7]) const  // sim3.h Adj
+    {
+        T R[3][3], tx[3][3], tR[3][3];
+        qmat(r.so3.q, R);
+        hat(t, tx);
+        mm3(tx, R, tR);
+        for (int i = 0; i < 7; i++)
+            for (int j = 0; j < 7; j++) A[i][j] = (T)(i == j);
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) {
+                A[i][j] = r.s * R[i][j];
+                A[i][j + 3] = tR[i][j];
+                A[i + 3][j + 3] = R[i][j];
+            }
+            A[i][6] = -t[i];
+        }
+    }
+    __device__ void projector(T* P) const  // sim3.h orthogonal_projector, 8x8 row-major
+    {
+        for (int i = 0; i < 64; i++) P[i] = 0;
+        const T mt[3] = {-t[0], -t[1], -t[2]};
+        T H[3][3];
+        hat(mt, H);
+        for (int i = 0; i < 3; i++) {
+            P[i * 8 + i] = 1;
+            for (int j = 0; j < 3; j++) P[i * 8 + 3 + j] = H[i][j];
+            P[i * 8 + 6] = t[i];
+        }
+        T Pr[25];
+        r.projector(Pr);
+        for (int i = 0; i < 5; i++)
+            for (int j = 0; j < 5; j++) P[(3 + i) * 8 + 3 + j] = Pr[i * 5 + j];
+    }
+    __device__ void Log(T* xi) const  // [W^-1 t, phi, sigma]
+    {
+        r.Log(xi + 3);
+        T W[3][3], Wi[3][3];
+        RxSO3<T>::calcW(xi + 3, W);
+        inv3(W, Wi);
+        for (int i = 0; i < 3; i++) xi[i] = Wi[i][0] * t[0] + Wi[i][1] * t[1] + Wi[i][2] * t[2];
+    }
+    __device__ static Sim3 Exp(const T* xi)
+    {
+        Sim3 g;
+        g.r = RxSO3<T>::Exp(xi + 3);
+        T W[3][3];
+        RxSO3<T>::calcW(xi + 3, W);
+        for (int i = 0; i < 3; i++) g.t[i] = W[i][0] * xi[0] + W[i][1] * xi[1] + W[i][2] * xi[2];
+        return g;
+    }
+    __device__ static void ad(const T* a, T A[7][7])  // sim3.h adj
+    {
+        T Ta[3][3], Ph[3][3];
+        hat(a, Ta);
+        hat(a + 3, Ph);
+        for (int i = 0; i < 7; i++)
+            for (int j = 0; j < 7; j++) A[i][j] = 0;
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) {
+                A[i][j] = Ph[i][j] + (i == j ? a[6] : (T)0);
+                A[i][j + 3] = Ta[i][j];
+                A[i + 3][j + 3] = Ph[i][j];
+            }
+            A[i][6] = -a[i];
+        }
+    }
+    // sim3.h left_jacobian: I + X/2 + X^2/6 + X^3/24 + X^4/120 (its 1/720 X^5
+    // term sits after the statement's semicolon in the reference: not applied)
+    __device__ static void left_jacobian(const T* xi, T J[7][7])
+    {
+        T X[7][7], X2[7][7], X3[7][7], X4[7][7];
+        ad(xi, X);
+        mmk<T, 7>(X, X, X2);
+        mmk<T, 7>(X, X2, X3);
+        mmk<T, 7>(X2, X2, X4);
+        for (int i = 0; i < 7; i++)
+            for (int j = 0; j < 7; j++)
+                J[i][j] = (T)(i == j) + (T)(1.0 / 2.0) * X[i][j] + (T)(1.0 / 6.0) * X2[i][j] +
+                          (T)(1.0 / 24.0) * X3[i][j] + (T)(1.0 / 120.0) * X4[i][j];
+    }
+    __device__ static void left_jacobian_inverse(const T* xi, T J[7][7])
+    {
+        T X[7][7], X2[7][7], X4[7][7];
+        ad(xi, X);
+        mmk<T, 7>(X, X, X2);
+        mmk<T, 7>(X2, X2, X4);
+        for (int i = 0; i < 7; i++)
+            for (int j = 0; j < 7; j++)
+                J[i][j] = (T)(i == j) - (T)(1.0 / 2.0) * X[i][j] + (T)(1.0 / 12.0) * X2[i][j] -
+                          (T)(1.0 / 720.0) * X4[i][j];
+    }
+    __device__ static void act_jacobian(const T* p, T J[3][7])
+    {
+        const T m[3] = {-p[0], -p[1], -p[2]};
+        T H[3][3];
+        hat(m, H);
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) { J[i][j] = (T)(i == j); J[i][j + 3] = H[i][j]; }
+            J[i][6] = p[i];
+        }
+    }
+    __device__ static void act4_jacobian(const T* p, T J[4][7])
+    {
+        const T m[3] = {-p[0], -p[1], -p[2]};
+        T H[3][3];
+        hat(m, H);
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) { J[i][j] = i == j ? p[3] : (T)0; J[i][j + 3] = H[i][j]; }
+            J[i][6] = p[i];
+        }
+        for (int j = 0; j < 7; j++) J[3][j] = 0;
     }
 };
 

@@ -1,4 +1,4 @@
-// lietorch.hip -- SO3 / SE3 group operators for gfx950.
+// lietorch.hip -- SO3 / RxSO3 / SE3 / Sim3 group operators for gfx950.
 //
 // Replaces the GPU half of the reference's lietorch_backends extension
 // (dpvo/lietorch/src/lietorch.cpp:286-316, lietorch_gpu.cu:21-601): one
@@ -195,15 +195,19 @@ int lie_dispatch_bwd(int op, int dtype, const void* g, const void* X, const void
 extern "C" int dpvo_lie_forward(int op, int group, int dtype, const void* X, const void* Y, void* out, int64_t n,
                                 void* stream)
 {
-    DPVO_CHECK_ARG(group == 1 || group == 3, "only SO3 (1) and SE3 (3) are built for MI355X; RxSO3/Sim3 are not");
+    DPVO_CHECK_ARG(group >= 1 && group <= 4, "group id must be 1 (SO3), 2 (RxSO3), 3 (SE3) or 4 (Sim3)");
     DPVO_CHECK_ARG(dtype == DPVO_F32 || dtype == DPVO_F64, "lietorch ops take float32 or float64");
     DPVO_CHECK_ARG(op >= DPVO_LIE_EXP && op <= DPVO_LIE_JINV, "unknown operator");
     if (n == 0) return 0;
     const bool binary = op == DPVO_LIE_MUL || op == DPVO_LIE_ADJ || op == DPVO_LIE_ADJT || op == DPVO_LIE_ACT ||
                         op == DPVO_LIE_ACT4 || op == DPVO_LIE_JINV;
     DPVO_CHECK_ARG(X && out && (!binary || Y), "null operand");
-    if (group == 1) lie_dispatch_fwd<lie::SO3>(op, dtype, X, Y, out, n, as_stream(stream));
-    else lie_dispatch_fwd<lie::SE3>(op, dtype, X, Y, out, n, as_stream(stream));
+    switch (group) {
+    case 1: lie_dispatch_fwd<lie::SO3>(op, dtype, X, Y, out, n, as_stream(stream)); break;
+    case 2: lie_dispatch_fwd<lie::RxSO3>(op, dtype, X, Y, out, n, as_stream(stream)); break;
+    case 3: lie_dispatch_fwd<lie::SE3>(op, dtype, X, Y, out, n, as_stream(stream)); break;
+    default: lie_dispatch_fwd<lie::Sim3>(op, dtype, X, Y, out, n, as_stream(stream)); break;
+    }
     DPVO_CHECK_LAUNCH();
     return 0;
 }
@@ -211,12 +215,16 @@ extern "C" int dpvo_lie_forward(int op, int group, int dtype, const void* X, con
 extern "C" int dpvo_lie_backward(int op, int group, int dtype, const void* grad, const void* X, const void* Y,
                                  void* dX, void* dY, int64_t n, void* stream)
 {
-    DPVO_CHECK_ARG(group == 1 || group == 3, "only SO3 (1) and SE3 (3) are built for MI355X; RxSO3/Sim3 are not");
+    DPVO_CHECK_ARG(group >= 1 && group <= 4, "group id must be 1 (SO3), 2 (RxSO3), 3 (SE3) or 4 (Sim3)");
     DPVO_CHECK_ARG(dtype == DPVO_F32 || dtype == DPVO_F64, "lietorch ops take float32 or float64");
     DPVO_CHECK_ARG(op >= DPVO_LIE_EXP && op <= DPVO_LIE_ACT4, "operator has no backward");
     if (n == 0) return 0;
-    if (group == 1) lie_dispatch_bwd<lie::SO3>(op, dtype, grad, X, Y, dX, dY, n, as_stream(stream));
-    else lie_dispatch_bwd<lie::SE3>(op, dtype, grad, X, Y, dX, dY, n, as_stream(stream));
+    switch (group) {
+    case 1: lie_dispatch_bwd<lie::SO3>(op, dtype, grad, X, Y, dX, dY, n, as_stream(stream)); break;
+    case 2: lie_dispatch_bwd<lie::RxSO3>(op, dtype, grad, X, Y, dX, dY, n, as_stream(stream)); break;
+    case 3: lie_dispatch_bwd<lie::SE3>(op, dtype, grad, X, Y, dX, dY, n, as_stream(stream)); break;
+    default: lie_dispatch_bwd<lie::Sim3>(op, dtype, grad, X, Y, dX, dY, n, as_stream(stream)); break;
+    }
     DPVO_CHECK_LAUNCH();
     return 0;
 }

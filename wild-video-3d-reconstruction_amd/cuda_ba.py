@@ -10,6 +10,13 @@ ba_cuda.cu:521 raises); it costs one device->host read of a status word per
 call.  Set it to False for fully asynchronous / graph-captured use; the
 status is then left in ``last_status`` (a device tensor).
 
+Windows of up to 12 optimised poses (DPVO's sliding window) take the
+deterministic per-patch path: no float atomics, bitwise repeatable.  It
+groups the edges by kk on the device, or reuses a caller's grouping
+(``csr=(offs, perm, groups)`` from update_ops.group_by(kk), which
+DPVO.update already computes for the update operator).  ``DETERMINISTIC =
+False`` selects the atomic dense path instead (A/B tests).
+
 Windows of more than 64 optimised poses (the global BA of dpvo.py:436-505)
 take the sparse path automatically: per-edge Schur entries and a tiled band
 Cholesky instead of the dense E / S (see include/dpvo_hot.h).  ``SPARSE =
@@ -21,11 +28,14 @@ import _dpvo_hot as H
 
 CHECK_CHOLESKY = True
 SPARSE = False
+DETERMINISTIC = True
 last_status = None
 
 
-def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, iterations):
-    """ba.cpp:31-43 -> ba_cuda.cu:422-540.  Updates poses and patches in place; returns []."""
+def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, iterations, csr=None):
+    """ba.cpp:31-43 -> ba_cuda.cu:422-540.  Updates poses and patches in place; returns [].
+    csr (optional, not in the reference): (offs int32 [E+1], perm int32 [E],
+    groups int64 [1]) of update_ops.group_by(kk) for these edges."""
     global last_status
     H.on_gpu(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk)
     for name, t in (("poses", poses), ("patches", patches), ("intrinsics", intrinsics), ("target", target),
@@ -40,14 +50,21 @@ def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t
     lmbda = lmbda.to(device=poses.device, dtype=torch.float32).contiguous()
     E = ii.numel()
     N = int(t1) - int(t0)
-    flags = 1 if SPARSE else 0
+    flags = (1 if SPARSE else 0) | (0 if DETERMINISTIC else 2)
     nbytes = H.lib().dpvo_ba_workspace_bytes_ex(E, num_patches, max(N, 0), flags)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=poses.device)
     status = torch.zeros(1, dtype=torch.int32, device=poses.device)
-    H.check(H.lib().dpvo_ba_forward_ex(
+    offs = perm = groups = None
+    if csr is not None:
+        offs, perm, groups = csr
+        H.on_gpu(offs, perm, groups)
+        if (offs.dtype != torch.int32 or perm.dtype != torch.int32 or groups.dtype != torch.int64 or
+                offs.numel() < E + 1 or perm.numel() < E):
+            raise RuntimeError("csr must be update_ops.group_by(kk)'s (offs int32 [E+1], perm int32 [E], groups int64)")
+    H.check(H.lib().dpvo_ba_forward_csr(
         H.ptr(poses), H.ptr(patches), num_patches, P, H.ptr(intrinsics), H.ptr(target), H.ptr(weight), H.ptr(lmbda),
-        H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(t0), int(t1), int(iterations), flags, H.ptr(ws), nbytes,
-        H.ptr(status), H.stream_of(poses)))
+        H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(t0), int(t1), int(iterations), flags, H.ptr(offs), H.ptr(perm),
+        H.ptr(groups), H.ptr(ws), nbytes, H.ptr(status), H.stream_of(poses)))
     last_status = status
     if CHECK_CHOLESKY:
         s = int(status.item())

@@ -17,6 +17,7 @@ import torch
 import torch.nn.functional as F
 
 import cuda_corr
+import update_ops
 
 from . import altcorr, fastba
 from . import projective_ops as pops
@@ -259,13 +260,18 @@ class DPVO:
         :730-731)."""
         with Timer("other", enabled=self.enable_timing):
             coords = self.reproject()
+            # the edges grouped by patch once, on the device: the update
+            # operator's SoftAgg over kk and temporal neighbours, and BA's
+            # per-patch reduction all read this CSR
+            kk_groups = update_ops.group_by(self.pg.kk, key_bits=update_ops.key_bits_for(self.N * self.M))
             with torch.autocast("cuda", enabled=True):
                 corr = self.corr(coords)
                 # ctx = imap[:, kk % (M pmem)] (dpvo.py:718), gathered by the consumer
                 ctx_idx = self.pg.kk % (self.M * self.pmem)
                 self.pg.net, (delta, weight, _) = self.network.update(self.pg.net, self.imap, corr, None, self.pg.ii,
                                                                       self.pg.jj, self.pg.kk, inp_idx=ctx_idx,
-                                                                      index_bounds=(self.N * self.M, self.N))
+                                                                      index_bounds=(self.N * self.M, self.N),
+                                                                      kk_groups=kk_groups)
             weight = weight.float()
             target = coords[..., self.P // 2, self.P // 2] + delta.float()
         self.pg.target = target
@@ -274,7 +280,7 @@ class DPVO:
             t0_ = self.n - self.cfg.OPTIMIZATION_WINDOW if self.is_initialized else 1
             t0 = max(t0_, t0 or 1)
             fastba.BA(self.poses, self.patches, self.intrinsics, target, weight, self._lmbda, self.pg.ii, self.pg.jj,
-                      self.pg.kk, t0, self.n, getattr(self.cfg, "BA_ITERATIONS", 2))
+                      self.pg.kk, t0, self.n, getattr(self.cfg, "BA_ITERATIONS", 2), csr=kk_groups[1:])
             m = self.pg.m
             pops.point_cloud_centre(SE3(self.poses), self.patches[:, :m], self.intrinsics, self.ix[:m],
                                     out=self.pg.points_[:m])

@@ -6,7 +6,10 @@ neighbors = cuda_ba.neighbors   # device-resident (the reference round-trips to 
 reproject = cuda_ba.reproject
 
 
-def BA(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, iterations=2):
+def BA(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, iterations=2, csr=None):
     """Gauss-Newton over poses [t0, t1) and the inverse depth of every patch
-    referenced by kk; `poses` and `patches` are updated in place."""
-    return cuda_ba.forward(poses.data, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, iterations)
+    referenced by kk; `poses` and `patches` are updated in place.  csr
+    (optional): the caller's update_ops.group_by(kk) CSR, reused instead of
+    grouping the edges again."""
+    return cuda_ba.forward(poses.data, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, iterations,
+                           csr=csr)

@@ -68,7 +68,7 @@ class Update(nn.Module):
                 torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16 and
                 self.FUSED)
 
-    def _forward_fused(self, net, inp, corr, ii, jj, kk, inp_idx=None, index_bounds=None):
+    def _forward_fused(self, net, inp, corr, ii, jj, kk, inp_idx=None, index_bounds=None, kk_groups=None):
         """The same dataflow as the reference under autocast, in 19 full-row
         fused GEMMs (csrc/rowgemm.hip; 5 Linear->ReLU->Linear pairs chained,
         14 launches) + 2 SoftAggs: every Linear is an fp16
@@ -98,7 +98,8 @@ class Update(nn.Module):
         if index_bounds is not None:
             kk_bits = U.key_bits_for(index_bounds[0])
             ij_bits = U.key_bits_for(index_bounds[1] * 12345 + 12345)
-        kk_groups = U.group_by(kk, key_bits=kk_bits)
+        if kk_groups is None:
+            kk_groups = U.group_by(kk, key_bits=kk_bits)
         ix, jx = U.neighbors_csr(jj, kk_groups[1], kk_groups[2], kk_groups[3], E)
         for (la, lb), nb in ((pk["c1"], ix), (pk["c2"], jx)):
             n32, n16, _ = U.rowchain(n16, *la, *lb, flags1=U.RELU, a_idx=nb, flags=U.RES, res32=n32, want32=True)
@@ -123,15 +124,16 @@ class Update(nn.Module):
                                          gate16=g16, ln=ln1, want32=True)
         return n32[None], (heads[None, :, :2], heads[None, :, 2:], None)
 
-    def forward(self, net, inp, corr, flow, ii, jj, kk, inp_idx=None, index_bounds=None):
+    def forward(self, net, inp, corr, flow, ii, jj, kk, inp_idx=None, index_bounds=None, kk_groups=None):
         """edge hidden state -> (new state, (delta, weight, None)) (net.py:75-93).
 
         Optional, not in the reference: inp_idx -- inp is then the un-gathered
         context ring and the rows are inp[:, inp_idx]; index_bounds =
         (num_patches, num_frames) -- kk < num_patches and ii, jj < num_frames,
-        which narrows the fused path's radix sorts."""
+        which narrows the fused path's radix sorts; kk_groups =
+        update_ops.group_by(kk), when the caller already has it."""
         if self._fusable(net, inp, corr) and (inp_idx is None or inp.is_contiguous()):
-            return self._forward_fused(net, inp, corr, ii, jj, kk, inp_idx, index_bounds)
+            return self._forward_fused(net, inp, corr, ii, jj, kk, inp_idx, index_bounds, kk_groups)
         if inp_idx is not None:
             inp = inp[:, inp_idx]
         net = self.norm(net + inp + self.corr(corr))

@@ -89,7 +89,9 @@ def steady_state_tracker(preset="dpvo_2k", buffer=2048, n=None, seed=0, ht=384, 
     # edges and hidden state
     ii, jj, kk = steady_state_edges(n, M, cfg.PATCH_LIFETIME, cfg.REMOVAL_WINDOW, dev)
     slam.pg.ii, slam.pg.jj, slam.pg.kk = ii, jj, kk
-    slam.pg.net = (0.1 * torch.randn(1, len(ii), slam.DIM, generator=g3, device=dev)).to(slam.kwargs["dtype"])
+    # fp32: after its first update() the reference's edge state is the fp32
+    # LayerNorm output (autocast), and appended fp16 zeros promote to it
+    slam.pg.net = 0.1 * torch.randn(1, len(ii), slam.DIM, generator=g3, device=dev)
     slam.pg.weight = torch.zeros(1, len(ii), 2, device=dev)
     slam.pg.target = torch.zeros(1, len(ii), 2, device=dev)
     slam.pg.n, slam.pg.m = n, n * M

@@ -2,7 +2,8 @@
 
 Same 19 functions, argument order (group_id first) and output shapes as
 dpvo/lietorch/src/lietorch.cpp:286-316 (imported by
-dpvo/lietorch/group_ops.py:1).  group_id: 1 = SO3, 3 = SE3 (dispatch.h:16-31).
+dpvo/lietorch/group_ops.py:1).  group_id: 1 = SO3, 2 = RxSO3, 3 = SE3,
+4 = Sim3 (dispatch.h:16-31).
 Inputs must be contiguous (lietorch.cpp:7 CHECK_CONTIGUOUS) float32/float64
 GPU tensors; the math runs in libdpvo_hot.so (csrc/lietorch.hip).
 """
@@ -11,7 +12,7 @@ import torch
 import _dpvo_hot as H
 
 EXP, LOG, INV, MUL, ADJ, ADJT, ACT, ACT4, MATRIX, PROJECTOR, JINV = range(11)
-_DIMS = {1: (3, 4), 3: (6, 7)}  # group -> (K manifold dim, N embedding dim)
+_DIMS = {1: (3, 4), 2: (4, 5), 3: (6, 7), 4: (7, 8)}  # group -> (K manifold dim, N embedding dim)
 
 
 def _contig(name, t):
@@ -21,7 +22,7 @@ def _contig(name, t):
 
 def _dims(group_id):
     if group_id not in _DIMS:
-        raise RuntimeError(f"group {group_id} (RxSO3=2 / Sim3=4) is not built for MI355X; SO3=1 and SE3=3 are")
+        raise RuntimeError(f"unknown group id {group_id}: 1 = SO3, 2 = RxSO3, 3 = SE3, 4 = Sim3")
     return _DIMS[group_id]
 
 
