@@ -86,6 +86,23 @@ int dpvo_corr_forward_pyramid_ld(int dtype, const void* gmap, const int64_t* gma
 size_t dpvo_corr_table_bytes(const int64_t* gmap_size);
 int dpvo_corr_pack(const void* gmap, const int64_t* gmap_size, const int64_t* gmap_stride, void* table, void* stream);
 
+/* DPVO.corr (dpvo.py:326-333) on the matrix cores: both pyramid levels, the
+ * same 882-wide stacked rows as dpvo_corr_forward_pyramid_ld with radius 3
+ * and 3x3 patches, but the 128-channel dot products accumulate in fp32
+ * (v_mfma_f32_16x16x32_f16) and the bilinear epilogue runs in fp32, rounded
+ * once to fp16 -- more accurate than the reference's fp16 accumulation, not
+ * bit-identical to it (dpvo_corr_forward_pyramid_ld is).  table: the gmap
+ * ring transposed to [N1][9][128] by dpvo_corr_pack_mfma (gmap [1][N1][128][3][3]);
+ * fmaps: 2 levels, [1][N2][128][H][W] channel-last; coords [1][E][2][3][3];
+ * corr rows edge_stride halves apart (0: 882). */
+size_t dpvo_corr_pack_mfma_bytes(const int64_t* gmap_size);
+int dpvo_corr_pack_mfma(const void* gmap, const int64_t* gmap_size, const int64_t* gmap_stride, void* table,
+                        void* stream);
+int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, const void* const* fmaps,
+                           const int64_t* fmap_sizes, const int64_t* fmap_strides, const float* level_scale,
+                           const float* coords, const int64_t* coords_size, const int64_t* coords_stride,
+                           const int64_t* ii, const int64_t* jj, void* corr, int64_t edge_stride, void* stream);
+
 /* cuda_corr.backward (correlation_kernel.cu:236-286): grad is the returned
  * (permuted) view's gradient given as contiguous [B][E][2r+1 (x)][2r+1 (y)][P][P]
  * float; gmap_grad / fmap_grad (contiguous, dtype, zero-filled by caller)

@@ -1941,6 +1941,7 @@ __global__ __launch_bounds__(256) void bd_solve_kernel(BdParams p)
     __shared__ float colbuf[2][BD_N6MAX + 1];
     __shared__ float Lm[(BD_N6MAX + 1) * BD_N6MAX];
     __shared__ float xs[BD_N6MAX];
+    __shared__ float dinv[BD_N6MAX];
     if (*(volatile int*)p.status != 0) return;
     const int n = p.n6, tid = threadIdx.x;
     const int ntri = n * (n + 1) / 2, ne = ntri + n;
@@ -1993,6 +1994,7 @@ __global__ __launch_bounds__(256) void bd_solve_kernel(BdParams p)
             break;
         }
         const float invd = 1.0f / d, invl = 1.0f / sqrtf(d);
+        if (tid == 0) dinv[j] = invl;
 #pragma unroll
         for (int s = 0; s < BD_OWN; s++) {
             const int c = cc[s];
@@ -2012,7 +2014,7 @@ __global__ __launch_bounds__(256) void bd_solve_kernel(BdParams p)
         float z0 = tid < n ? Lm[n * n + tid] : 0.f, z1 = tid + 64 < n ? Lm[n * n + tid + 64] : 0.f;
         for (int j = n - 1; j >= 0; j--) {
             const float zj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(j < 64 ? z0 : z1), j & 63));
-            const float xj = zj / Lm[j * n + j];
+            const float xj = zj * dinv[j];
             if (tid < j) z0 -= Lm[j * n + tid] * xj;
             if (tid + 64 < j) z1 -= Lm[j * n + tid + 64] * xj;
             if (tid == (j & 63)) {

@@ -74,6 +74,46 @@ def forward_pyramid(fmap1, pyramid, coords, ii, jj, radius, scales, out=None, ta
     return out
 
 
+def pack_mfma(fmap1, out=None):
+    """The gmap ring [1, N1, 128, 3, 3] transposed to [N1, 9, 128] for the
+    matrix-core correlation (dpvo_corr_pack_mfma); re-pack when it changes."""
+    H.on_gpu(fmap1)
+    if fmap1.dtype != torch.float16 or fmap1.dim() != 5 or fmap1.shape[0] != 1 or tuple(fmap1.shape[2:]) != (128, 3, 3):
+        raise RuntimeError("pack_mfma: fmap1 must be an fp16 [1, N1, 128, 3, 3] tensor")
+    n = fmap1.shape[1] * 9 * 128
+    if out is None or out.numel() < n:
+        out = torch.empty(n, dtype=torch.float16, device=fmap1.device)
+    H.check(H.lib().dpvo_corr_pack_mfma(H.ptr(fmap1), H.sizes(fmap1), H.strides(fmap1), H.ptr(out),
+                                        H.stream_of(fmap1)))
+    return out
+
+
+def forward_pyramid_mfma(table, num_patches, pyramid, coords, ii, jj, scales=(1, 4), out=None):
+    """DPVO.corr's two levels on the matrix cores (csrc/corrmfma.hip): the
+    stacked [1, E, 882] rows of forward_pyramid (radius 3, 3x3 patches), with
+    fp32 accumulation instead of the reference's fp16 chain (not bit-identical;
+    see include/dpvo_hot.h).  table = pack_mfma(gmap)."""
+    H.on_gpu(table, coords, ii, jj, *pyramid)
+    if len(pyramid) != 2 or any(f.dtype != torch.float16 for f in pyramid):
+        raise RuntimeError("forward_pyramid_mfma: two fp16 pyramid levels")
+    if coords.dtype != torch.float32 or coords.dim() != 5 or tuple(coords.shape[2:]) != (2, 3, 3):
+        raise RuntimeError("forward_pyramid_mfma: coords must be float32 [1, E, 2, 3, 3]")
+    E = coords.shape[1]
+    if out is None:
+        out = torch.empty((1, E, 882), dtype=torch.float16, device=coords.device)
+    elif out.shape != (1, E, 882) or out.dtype != torch.float16 or out.stride(2) != 1:
+        raise RuntimeError("forward_pyramid_mfma: out must be [1, E, 882] fp16 with unit feature stride")
+    ii, jj = H.idx64(ii), H.idx64(jj)
+    ptrs = (H._vp * 2)(*[f.data_ptr() for f in pyramid])
+    fs = H.i64arr([s for f in pyramid for s in f.shape])
+    fst = H.i64arr([s for f in pyramid for s in f.stride()])
+    sc = (H._fp * 2)(*[float(s) for s in scales])
+    H.check(H.lib().dpvo_corr_pyramid_mfma(
+        H.ptr(table), int(num_patches), ptrs, fs, fst, sc, H.ptr(coords), H.sizes(coords), H.strides(coords),
+        H.ptr(ii), H.ptr(jj), H.ptr(out), out.stride(1) if E > 0 else 0, H.stream_of(coords)))
+    return out
+
+
 def backward(fmap1, fmap2, coords, ii, jj, grad, radius):
     """correlation.cpp:37-45 / correlation_kernel.cu:236-286 -> [fmap1_grad, fmap2_grad]."""
     _check_corr_args(fmap1, fmap2, coords, ii, jj)

@@ -182,17 +182,25 @@ class DPVO:
             # Linear reads them as 16-byte aligned GEMM rows without a copy
             buf = self._corr_rows(E)
             out = buf[:E, :CORR_DIM].unsqueeze(0)
+            if not getattr(self.cfg, "EXACT_CORR", False) and getattr(self.cfg, "CHANNEL_LAST_FMAPS", True):
+                # matrix cores, fp32 accumulation (csrc/corrmfma.hip)
+                return altcorr.corr_pyramid_mfma(self._gmap_table(mfma=True), self.gmap.shape[1], self.pyramid,
+                                                 coords, ii1, jj1, out=out).view(1, E, -1)
             table = self._gmap_table()
         return altcorr.corr_pyramid(self.gmap, self.pyramid, coords, ii1, jj1, 3, (1, 4), out=out,
                                     table=table).view(1, E, -1)
 
-    def _gmap_table(self):
-        """The gmap ring packed for altcorr's scalar-operand path, re-packed only
-        when the ring changed (torch's in-place version counter: new keyframes)."""
-        key = (self.gmap_.data_ptr(), self.gmap_._version)
+    def _gmap_table(self, mfma=False):
+        """The gmap ring packed for altcorr (the exact kernel's scalar-operand
+        table, or the matrix-core kernel's [patch][pixel][channel] transpose),
+        re-packed only when the ring changed (torch's in-place version counter:
+        new keyframes)."""
+        key = (self.gmap_.data_ptr(), self.gmap_._version, mfma)
         if getattr(self, "_gtab_key", None) != key:
-            self._gtab = cuda_corr.pack(self.gmap, out=getattr(self, "_gtab", None))
-            self._gtab_key = key
+            pack = cuda_corr.pack_mfma if mfma else cuda_corr.pack
+            old = getattr(self, "_gtab", None)
+            self._gtab = pack(self.gmap, out=old if getattr(self, "_gtab_mfma", None) == mfma else None)
+            self._gtab_key, self._gtab_mfma = key, mfma
         return self._gtab
 
     def _corr_rows(self, E):
