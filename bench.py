@@ -51,6 +51,7 @@ def parse():
     ap.add_argument("--buffer", type=int, default=None)
     ap.add_argument("--iterations", type=int, default=None)
     ap.add_argument("--e2e-frames", type=int, default=32, help="end-to-end frames timed after the bench (0: skip)")
+    ap.add_argument("--exact-corr", action="store_true", help="the bit-exact fp16-chain altcorr instead of the MFMA one")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-edges", type=int, default=1500)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "altcorr_traffic.json"))
@@ -105,20 +106,23 @@ class CorrProbe:
         self.pairs = []
 
     def wrap(self, slam):
-        """Events bracket exactly the fused-altcorr launch (dpvo.altcorr.corr_pyramid,
-        called by DPVO.corr), on the current stream -- the stream it runs on."""
+        """Events bracket exactly the fused-altcorr launch (dpvo.altcorr.corr_pyramid
+        or corr_pyramid_mfma, called by DPVO.corr), on the current stream -- the
+        stream it runs on."""
         from dpvo import altcorr
-        inner = altcorr.corr_pyramid
 
-        def corr_pyramid(*a, **k):
-            s = torch.cuda.Event(enable_timing=True)
-            e = torch.cuda.Event(enable_timing=True)
-            s.record()
-            out = inner(*a, **k)
-            e.record()
-            self.pairs.append((s, e))
-            return out
-        altcorr.corr_pyramid = corr_pyramid
+        def timed(inner):
+            def f(*a, **k):
+                s = torch.cuda.Event(enable_timing=True)
+                e = torch.cuda.Event(enable_timing=True)
+                s.record()
+                out = inner(*a, **k)
+                e.record()
+                self.pairs.append((s, e))
+                return out
+            return f
+        altcorr.corr_pyramid = timed(altcorr.corr_pyramid)
+        altcorr.corr_pyramid_mfma = timed(altcorr.corr_pyramid_mfma)
 
     def mean_ms(self):
         ts = [s.elapsed_time(e) for s, e in self.pairs]
@@ -341,7 +345,7 @@ def main():
     args.buffer = args.buffer or cfgd["buffer"]
     args.iterations = args.iterations or cfgd["iterations"]
     slam = steady_state_tracker(cfgd["preset"], buffer=args.buffer, seed=rank, iterations=args.iterations,
-                                device=f"cuda:{local}", **cfgd["overrides"])
+                                device=f"cuda:{local}", EXACT_CORR=args.exact_corr, **cfgd["overrides"])
     E = slam.pg.ii.numel()
     probe = CorrProbe()
     probe.wrap(slam)
@@ -390,7 +394,8 @@ def main():
                        "patches_per_frame": slam.M, "buffer": args.buffer, "n_keyframes": slam.n, "edges": E,
                        "ba_iterations": slam.cfg.BA_ITERATIONS, "image": "512x384",
                        "parallelism": f"replicas{world}"},
-            "roofline": {"kernel": "corr_sfast_kernel<2,16> (fused 2-level altcorr)", "bound": "hbm",
+            "roofline": {"kernel": ("corr_sfast_kernel<2,16> (bit-exact fp16-chain altcorr)" if slam.cfg.EXACT_CORR
+                                    else "corr_mfma_kernel (2-level altcorr on the matrix cores)"), "bound": "hbm",
                          "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "bytes_per_edge": CORR_BYTES_PER_EDGE, "avg_launch_ms": round(corr_ms, 5)},

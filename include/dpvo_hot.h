@@ -94,14 +94,25 @@ int dpvo_corr_pack(const void* gmap, const int64_t* gmap_size, const int64_t* gm
  * bit-identical to it (dpvo_corr_forward_pyramid_ld is).  table: the gmap
  * ring transposed to [N1][9][128] by dpvo_corr_pack_mfma (gmap [1][N1][128][3][3]);
  * fmaps: 2 levels, [1][N2][128][H][W] channel-last; coords [1][E][2][3][3];
- * corr rows edge_stride halves apart (0: 882). */
+ * corr rows edge_stride halves apart (0: 882).  order (optional, NULL = edge
+ * order): a permutation of the edges from dpvo_edge_order(jj) -- edges that
+ * read one target frame then run back to back on one XCD, whose L2 holds
+ * that frame's map; the output does not depend on it. */
 size_t dpvo_corr_pack_mfma_bytes(const int64_t* gmap_size);
 int dpvo_corr_pack_mfma(const void* gmap, const int64_t* gmap_size, const int64_t* gmap_stride, void* table,
                         void* stream);
 int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, const void* const* fmaps,
                            const int64_t* fmap_sizes, const int64_t* fmap_strides, const float* level_scale,
                            const float* coords, const int64_t* coords_size, const int64_t* coords_stride,
-                           const int64_t* ii, const int64_t* jj, void* corr, int64_t edge_stride, void* stream);
+                           const int64_t* ii, const int64_t* jj, void* corr, int64_t edge_stride, const int* order,
+                           void* stream);
+
+/* A permutation of the E edges grouped by jj (values outside [0,
+ * num_buckets) last), by a counting sort; the order inside a group is
+ * unspecified.  Workspace: dpvo_edge_order_workspace_bytes(num_buckets). */
+size_t dpvo_edge_order_workspace_bytes(int num_buckets);
+int dpvo_edge_order(const int64_t* jj, int64_t num_edges, int num_buckets, int* order, void* workspace,
+                    size_t workspace_bytes, void* stream);
 
 /* cuda_corr.backward (correlation_kernel.cu:236-286): grad is the returned
  * (permuted) view's gradient given as contiguous [B][E][2r+1 (x)][2r+1 (y)][P][P]

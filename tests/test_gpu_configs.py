@@ -47,7 +47,9 @@ def _check_ba_and_points(slam, iters, seed=5, corr_sample=300):
         ref = oracle.transform(poses, patches, intr, ii, jj, kk)[0].transpose(0, 3, 1, 2)
         np.testing.assert_allclose(coords[0].cpu().numpy(), ref, rtol=1e-5, atol=5e-3)
 
+        slam.cfg.EXACT_CORR = True   # bit-exact fp16 chain here; the MFMA default is bounded below / in test_gpu_corr_mfma
         corr = slam.corr(coords)
+        slam.cfg.EXACT_CORR = False
         sel = np.linspace(0, len(ii) - 1, corr_sample).astype(np.int64)
         want = oracle.corr_pyramid(slam.gmap.cpu().numpy(), [slam.fmap1_.contiguous().cpu().numpy(),
                                                               slam.fmap2_.contiguous().cpu().numpy()],
@@ -264,3 +266,29 @@ def test_init_from_prior_poses_and_depths():
         np.testing.assert_allclose(got[i, :3], T[:3, 3], atol=1e-5)
         np.testing.assert_allclose(R, T[:3, :3], atol=1e-5)
         np.testing.assert_allclose(slam.pg.patches_est_[i, :, 2].cpu().numpy(), 1.0 / (2.0 + i), rtol=1e-6)
+
+
+def test_mfma_corr_drift_on_outputs():
+    """cfg.EXACT_CORR=False (matrix-core correlation, fp32 accumulation; the
+    default) vs True (the reference's fp16 chain, bit-exact) from the same
+    state: poses, inverse depths and points after one update().  Bars: the
+    north star's 1e-3 relative."""
+    a, b = _twin_trackers(11)
+    b.cfg.EXACT_CORR = True
+    with torch.no_grad():
+        a.update()
+        b.update()
+    torch.cuda.synchronize()
+    t0, t1 = a.n - a.cfg.OPTIMIZATION_WINDOW, a.n
+    pa, pb = a.pg.poses_[t0:t1].cpu().numpy(), b.pg.poses_[t0:t1].cpu().numpy()
+    kk = torch.unique(a.pg.kk)
+    da = a.pg.patches_.view(-1, 3, 3, 3)[kk, 2, 1, 1].cpu().numpy()
+    db = b.pg.patches_.view(-1, 3, 3, 3)[kk, 2, 1, 1].cpu().numpy()
+    m = a.pg.m
+    xa, xb = a.pg.points_[:m].cpu().numpy(), b.pg.points_[:m].cpu().numpy()
+    mx = lambda x, y: float(np.max(np.abs(x - y) / (np.abs(y) + 1e-3)))
+    drift = dict(poses=mx(pa, pb), depths=mx(da, db), points_norm=float(np.linalg.norm(xa - xb) / np.linalg.norm(xb)))
+    print("mfma-vs-exact corr drift:", {k: f"{v:.3g}" for k, v in drift.items()})
+    per_element(pa, pb, what="window poses (mfma vs exact corr)")
+    per_element(da, db, what="inverse depths (mfma vs exact corr)")
+    assert drift["points_norm"] < 1e-3

@@ -36,7 +36,9 @@ def test_update_pieces_match_oracle(slam):
         ref = oracle.transform(poses, patches, intr, ii, jj, kk)[0].transpose(0, 3, 1, 2)
         np.testing.assert_allclose(coords[0].cpu().numpy(), ref, rtol=1e-5, atol=5e-3)
 
+        slam.cfg.EXACT_CORR = True   # the bit-exact fp16-chain kernel (the MFMA default: test_gpu_corr_mfma.py)
         corr = slam.corr(coords)
+        slam.cfg.EXACT_CORR = False
         sel = np.linspace(0, len(ii) - 1, 300).astype(np.int64)
         c_np = coords[0].cpu().numpy()[sel][None]
         want = oracle.corr_pyramid(slam.gmap.cpu().numpy(), [slam.fmap1_.contiguous().cpu().numpy(),

@@ -36,7 +36,9 @@ _SIGNATURES = {
     "dpvo_corr_pack": (_ip, [_vp, _vp, _vp, _vp, _vp]),
     "dpvo_corr_pack_mfma_bytes": (_sz, [_vp]),
     "dpvo_corr_pack_mfma": (_ip, [_vp, _vp, _vp, _vp, _vp]),
-    "dpvo_corr_pyramid_mfma": (_ip, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "dpvo_corr_pyramid_mfma": (_ip, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "dpvo_edge_order_workspace_bytes": (_sz, [_ip]),
+    "dpvo_edge_order": (_ip, [_vp, _i64, _ip, _vp, _vp, _sz, _vp]),
     "dpvo_corr_backward": (_ip, [_ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip, _vp, _vp, _vp]),
     "dpvo_patchify_forward": (_ip, [_ip, _vp, _vp, _vp, _vp, _i64, _ip, _vp, _vp]),
     "dpvo_patchify_backward": (_ip, [_ip, _vp, _vp, _i64, _ip, _vp, _vp, _vp]),

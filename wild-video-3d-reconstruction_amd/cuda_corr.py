@@ -88,11 +88,25 @@ def pack_mfma(fmap1, out=None):
     return out
 
 
-def forward_pyramid_mfma(table, num_patches, pyramid, coords, ii, jj, scales=(1, 4), out=None):
+def edge_order(jj, num_frames):
+    """int32 permutation of the edges grouped by target frame jj (in
+    [0, num_frames)): the L2-friendly visiting order of forward_pyramid_mfma."""
+    H.on_gpu(jj)
+    jj = H.idx64(jj)
+    order = torch.empty(max(jj.numel(), 1), dtype=torch.int32, device=jj.device)
+    nbytes = H.lib().dpvo_edge_order_workspace_bytes(int(num_frames))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=jj.device)
+    H.check(H.lib().dpvo_edge_order(H.ptr(jj), jj.numel(), int(num_frames), H.ptr(order), H.ptr(ws), nbytes,
+                                    H.stream_of(jj)))
+    return order[:jj.numel()]
+
+
+def forward_pyramid_mfma(table, num_patches, pyramid, coords, ii, jj, scales=(1, 4), out=None, order=None):
     """DPVO.corr's two levels on the matrix cores (csrc/corrmfma.hip): the
     stacked [1, E, 882] rows of forward_pyramid (radius 3, 3x3 patches), with
     fp32 accumulation instead of the reference's fp16 chain (not bit-identical;
-    see include/dpvo_hot.h).  table = pack_mfma(gmap)."""
+    see include/dpvo_hot.h).  table = pack_mfma(gmap); order (optional) =
+    edge_order(jj, frames): a visiting order only, the output is the same."""
     H.on_gpu(table, coords, ii, jj, *pyramid)
     if len(pyramid) != 2 or any(f.dtype != torch.float16 for f in pyramid):
         raise RuntimeError("forward_pyramid_mfma: two fp16 pyramid levels")
@@ -108,9 +122,13 @@ def forward_pyramid_mfma(table, num_patches, pyramid, coords, ii, jj, scales=(1,
     fs = H.i64arr([s for f in pyramid for s in f.shape])
     fst = H.i64arr([s for f in pyramid for s in f.stride()])
     sc = (H._fp * 2)(*[float(s) for s in scales])
+    if order is not None:
+        H.on_gpu(order)
+        if order.dtype != torch.int32 or order.numel() != E or not order.is_contiguous():
+            raise RuntimeError("forward_pyramid_mfma: order must be a contiguous int32 permutation of the E edges")
     H.check(H.lib().dpvo_corr_pyramid_mfma(
         H.ptr(table), int(num_patches), ptrs, fs, fst, sc, H.ptr(coords), H.sizes(coords), H.strides(coords),
-        H.ptr(ii), H.ptr(jj), H.ptr(out), out.stride(1) if E > 0 else 0, H.stream_of(coords)))
+        H.ptr(ii), H.ptr(jj), H.ptr(out), out.stride(1) if E > 0 else 0, H.ptr(order), H.stream_of(coords)))
     return out
 
 

@@ -62,8 +62,9 @@ def corr_pyramid(gmap, pyramid, coords, ii, jj, radius=3, levels=(1, 4), out=Non
     return cuda_corr.forward_pyramid(gmap, list(pyramid), coords, ii, jj, radius, list(levels), out=out, table=table)
 
 
-def corr_pyramid_mfma(table, num_patches, pyramid, coords, ii, jj, levels=(1, 4), out=None):
+def corr_pyramid_mfma(table, num_patches, pyramid, coords, ii, jj, levels=(1, 4), out=None, order=None):
     """corr_pyramid's two levels (radius 3, 3x3 patches) on the matrix cores:
     fp32 accumulation of the 128-channel products instead of the reference's
     fp16 chain (more accurate; not bit-identical).  table = cuda_corr.pack_mfma(gmap)."""
-    return cuda_corr.forward_pyramid_mfma(table, num_patches, list(pyramid), coords, ii, jj, list(levels), out=out)
+    return cuda_corr.forward_pyramid_mfma(table, num_patches, list(pyramid), coords, ii, jj, list(levels), out=out,
+                                          order=order)

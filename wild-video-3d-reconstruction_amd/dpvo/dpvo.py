@@ -184,8 +184,10 @@ class DPVO:
             out = buf[:E, :CORR_DIM].unsqueeze(0)
             if not getattr(self.cfg, "EXACT_CORR", False) and getattr(self.cfg, "CHANNEL_LAST_FMAPS", True):
                 # matrix cores, fp32 accumulation (csrc/corrmfma.hip)
+                # edges grouped by target frame: one frame's map per XCD L2 at a time
+                order = cuda_corr.edge_order(jj1, self.pmem)
                 return altcorr.corr_pyramid_mfma(self._gmap_table(mfma=True), self.gmap.shape[1], self.pyramid,
-                                                 coords, ii1, jj1, out=out).view(1, E, -1)
+                                                 coords, ii1, jj1, out=out, order=order).view(1, E, -1)
             table = self._gmap_table()
         return altcorr.corr_pyramid(self.gmap, self.pyramid, coords, ii1, jj1, 3, (1, 4), out=out,
                                     table=table).view(1, E, -1)
