@@ -247,6 +247,17 @@ int dpvo_motion_mag(const float* poses, const float* patches, int P, const float
                     const int64_t* jj, const int64_t* kk, int64_t num_edges, int64_t i, int64_t j, float beta,
                     float* out, void* stream);
 
+/* Keyframe distance matrix of the global BA's distance-based edges
+ * (replaces the O(n^2) loop of dpvo.py:383-429 -- two flow_mag calls and one
+ * .item() per frame pair): dist [n][n] (device), dist[a][b] = mean over frame
+ * a's patches [M a, M (a + 1)) and their P*P pixels of flow_mag(a -> b)
+ * (projective_ops.py:111-121, weight beta).  The reference's distance of the
+ * pair (i, j) is 0.5 (dist[i][j] + dist[j][i]).  M 6 P^2 floats must fit in
+ * LDS (dpvo_keyframe_flow_lds_bytes). */
+size_t dpvo_keyframe_flow_lds_bytes(int P, int64_t patches_per_frame);
+int dpvo_keyframe_flow(const float* poses, const float* patches, int P, const float* intrinsics, int64_t num_frames,
+                       int64_t patches_per_frame, float beta, float* dist, void* stream);
+
 /* projective_ops.point_cloud (projective_ops.py:106-108) of patches[0..m):
  * centre_only=1 -> out [m][3] = xyz/w of the centre pixel (what
  * DPVO.update stores in pg.points_, dpvo.py:747-749); else out [m][P][P][4]. */

@@ -14,7 +14,7 @@ import os
 import re
 import sys
 
-KERNEL = re.compile(r"corr_s?fast_kernel<2")
+KERNEL = re.compile(os.environ.get("KREGEX", r"corr_mfma_kernel|corr_s?fast_kernel<2"))
 
 
 def per_dispatch(d, counter):

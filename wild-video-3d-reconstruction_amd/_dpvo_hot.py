@@ -59,6 +59,8 @@ _SIGNATURES = {
     "dpvo_transform": (_ip, [_vp, _vp, _ip, _vp, _vp, _vp, _vp, _i64, _ip, _vp, _vp, _vp]),
     "dpvo_point_cloud": (_ip, [_vp, _vp, _ip, _vp, _vp, _i64, _ip, _vp, _vp]),
     "dpvo_motion_mag": (_ip, [_vp, _vp, _ip, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _fp, _vp, _vp]),
+    "dpvo_keyframe_flow_lds_bytes": (ctypes.c_size_t, [_ip, _i64]),
+    "dpvo_keyframe_flow": (_ip, [_vp, _vp, _ip, _vp, _i64, _i64, _fp, _vp, _vp]),
     "dpvo_softagg_workspace_bytes": (_sz, [_i64, _i64]),
     "dpvo_softagg_forward": (_ip, [_ip, _vp, _i64, _vp, _i64, _vp, _i64, _ip, _i64, _fp, _vp, _vp, _sz, _vp]),
     "dpvo_gather_rows": (_ip, [_ip, _vp, _i64, _i64, _vp, _i64, _ip, _ip, _vp, _vp]),

@@ -28,7 +28,10 @@ namespace dpvo {
 
 namespace cm {
 constexpr int R = 3, D = 8, DO = 7, NP = 9, C = 128, BOXMAX = 12, WAVES = 4;
-constexpr int RS = 148;   // raw row stride (>= 144 box slots; 4 rows apart land 16 banks apart)
+constexpr int RW = 20;            // LDS window row: 8 columns at 4..11, the rest catches out-of-window box columns
+constexpr int RQ = D * RW + 4;    // LDS window stride per patch pixel
+constexpr int RL = NP * RQ;       // per level
+constexpr unsigned OOB = 0x80000000u;   // a buffer offset past every descriptor's range: the load returns 0
 }  // namespace cm
 
 typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
@@ -43,19 +46,18 @@ struct CorrMfmaParams {
     const int64_t* jj;
     int E;
     const half_t* fmap[2];
-    int64_t f_s1[2], f_s3[2], f_s4[2];
+    int64_t f_s1[2];
     int N2[2], H2[2], W2[2];
+    int64_t rowb[2];          // row stride in bytes
+    int pixb[2];              // pixel stride in bytes
+    int rowext[2];            // bytes from a row's first pixel to the end of its last
+    int frameext[2];          // bytes from a frame's first pixel to the end of its last
     float scale[2];
     half_t* out;
     int64_t o_e;
     const int* order;   // optional edge visiting order (edges grouped by target frame), NULL = 0..E-1
 };
 
-struct CorrMfmaMeta {
-    float xs[2][cm::NP], ys[2][cm::NP];
-    int fy[2][cm::NP], fx[2][cm::NP];
-    int oy[2], ox[2], bw[2], bh[2], fast[2], ntiles[2];
-};
 
 __device__ __forceinline__ void cm_wave_fence()
 {
@@ -63,213 +65,305 @@ __device__ __forceinline__ void cm_wave_fence()
     __builtin_amdgcn_wave_barrier();
 }
 
-// blocks b, b + 8, ... share an XCD under round-robin dispatch: give each XCD a
-// contiguous run of edges (consecutive edges mostly share a target frame)
-__device__ __forceinline__ int cm_xcd_swizzle(int b, int nblk)
+// Edge slots per wave.  Workgroups are dispatched to the 8 XCDs round-robin
+// (block b on XCD b % 8), each with its own L2: give each XCD one contiguous
+// eighth of the (target-frame-grouped) edge sequence, walked by all of its
+// waves in step, so an XCD streams through a few target frames' maps instead
+// of every XCD touching every frame.
+struct CmRange { int slot, end, stride; };
+__device__ __forceinline__ CmRange cm_range(int E, int wave)
 {
-    const int main = nblk & ~7;
-    if (b >= main) return b;
-    return (b & 7) * (main >> 3) + (b >> 3);
+    const int nblk = gridDim.x, b = blockIdx.x;
+    CmRange r;
+    if (nblk >= 8 && (nblk & 7) == 0) {
+        const int x = b & 7, per = nblk >> 3;
+        const int lo = (int)((int64_t)E * x / 8);
+        r.end = (int)((int64_t)E * (x + 1) / 8);
+        r.slot = lo + (b >> 3) * cm::WAVES + wave;
+        r.stride = per * cm::WAVES;
+    } else {
+        r.slot = b * cm::WAVES + wave;
+        r.end = E;
+        r.stride = nblk * cm::WAVES;
+    }
+    return r;
 }
 
 // per-edge prologue operands, loaded one edge ahead
 struct CmEdgeIn {
     int e, ix, jx;
-    float cx[1], cy[1];   // lane < 9: patch pixel q's coordinates (x, y) -- level scaling applied later
+    float cx, cy;   // patch pixel (lane & 15)'s coordinates (x, y) when < 9 -- level scaling applied later
 };
 
-__device__ __forceinline__ CmEdgeIn cm_load_edge(const CorrMfmaParams& p, int slot, int lane)
+__device__ __forceinline__ CmEdgeIn cm_load_edge(const CorrMfmaParams& p, int slot, int q16)
 {
     CmEdgeIn in;
     in.e = p.order ? p.order[slot] : slot;
     in.ix = (int)p.ii[in.e];
     in.jx = (int)p.jj[in.e];
-    const int q = lane < cm::NP ? lane : 0;
+    const int q = q16 < cm::NP ? q16 : 0;
     const float* cb = p.coords + (int64_t)in.e * p.c_s[1] + (q / 3) * p.c_s[3] + (q % 3) * p.c_s[4];
-    in.cx[0] = cb[0];
-    in.cy[0] = cb[p.c_s[2]];
+    in.cx = cb[0];
+    in.cy = cb[p.c_s[2]];
     return in;
 }
 
-// One wave per edge, persistent over a grid-stride range of edge slots.  The
-// next edge's indices and coordinates are in flight while the current edge
-// runs; the box tiles of both levels are one flat sequence whose B fragments
-// are loaded three tiles ahead (a static register ring), so about 12 KB per
-// wave is in flight at any time.
+// Per edge and level: the pixels the nine 8x8 windows need.  When the nine
+// floors lie within 4 of each other ("fast") that is one box of at most 12x12
+// pixels, visited one box ROW per tile: the A operand is 16 consecutive
+// pixels of the row (lanes past the box width read nothing), so a lane's load
+// offset is the same for every row of the level and the row itself is the
+// buffer descriptor's base -- wave-uniform scalar work.  Otherwise each patch
+// pixel's own window is visited, two window rows (16 pixels) per tile.
+struct CmLevel {
+    const char* frame;    // this target frame's map (byte pointer), wave-uniform
+    int64_t rowb;         // row stride in bytes
+    int H, W, pixb, rowext, frameext;
+    int fast, oy, ntiles;
+    // per lane (fast): load offset of box column (lane & 15); window origin of
+    // patch pixel (lane & 15) inside the box; LDS slot base and row mask
+    unsigned voff;
+    int wy0, sbase;
+    int fy, fx;           // per lane: floors of patch pixel (lane & 15) (wide path)
+};
+
+// One wave per edge, persistent over a contiguous per-XCD range of edge
+// slots.  The next edge's indices and coordinates are in flight while the
+// current edge runs; the tiles of both levels are one flat sequence whose A
+// fragments are loaded four tiles ahead (a static register ring).  Products
+// land in a per-wave LDS window [level][patch pixel][8][RW] (fp32), from which
+// the bilinear epilogue writes 256-byte coalesced rows.
 __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParams p)
 {
     using namespace cm;
-    __shared__ float raw[WAVES][2][NP][RS];
-    __shared__ CorrMfmaMeta meta[WAVES];
+    __shared__ float raw[WAVES][2 * RL];
+    __shared__ float wts[WAVES][2][4][16];   // bilinear weights per level and patch pixel
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nwaves = gridDim.x * WAVES;
-    int slot = cm_xcd_swizzle(blockIdx.x, gridDim.x) * WAVES + wave;
-    if (slot >= p.E) return;   // the whole wave; nothing below synchronises across waves
-    CorrMfmaMeta& m = meta[wave];
-    float (*rw)[NP][RS] = raw[wave];
+    const CmRange rg = cm_range(p.E, wave);
+    int slot = rg.slot;
+    if (slot >= rg.end) return;   // the whole wave; nothing below synchronises across waves
+    float* rw = raw[wave];
     const int q16 = lane & 15, kc = lane >> 4;
-    const h8_t hz = (h8_t)(_Float16)0;
-    CmEdgeIn nin = cm_load_edge(p, slot, lane);
+    const bool qv = q16 < NP;
 
-    for (; slot < p.E; slot += nwaves) {
+    // epilogue: output t = lane + 64 i is (x offset, y offset, patch pixel) = ((t / 9) / 7, (t / 9) % 7, t % 9)
+    int eoff[7], eq[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        const int t = min(lane + 64 * i, DO * DO * NP - 1);
+        const int pos = t / NP, q = t - pos * NP;
+        const int bxo = pos / DO, ay = pos - bxo * DO;
+        eq[i] = q;
+        eoff[i] = q * RQ + ay * RW + bxo + 4;
+    }
+
+    CmEdgeIn nin = cm_load_edge(p, slot, q16);
+    for (; slot < rg.end; slot += rg.stride) {
         const CmEdgeIn in = nin;
-        if (slot + nwaves < p.E) nin = cm_load_edge(p, slot + nwaves, lane);
-        const int e = in.e, ix = in.ix, jx = in.jx;
+        if (slot + rg.stride < rg.end) nin = cm_load_edge(p, slot + rg.stride, q16);
+        const int e = __builtin_amdgcn_readfirstlane(in.e);
+        const int ix = __builtin_amdgcn_readfirstlane(in.ix);
+        const int jx = __builtin_amdgcn_readfirstlane(in.jx);
         const bool ix_ok = ix >= 0 && ix < p.N1;
 
-        // ---- coordinates, floors, and per level the box covering the nine windows
-        cm_wave_fence();   // the previous edge's epilogue has read meta / raw
-        if (lane < 2 * NP) {
-            const int lev = lane / NP, q = lane - lev * NP;
-            const float xr = __shfl(in.cx[0], q), yr = __shfl(in.cy[0], q);
-            const float x = xr / p.scale[lev], y = yr / p.scale[lev];
-            m.xs[lev][q] = x;
-            m.ys[lev][q] = y;
-            m.fy[lev][q] = floor_to_int_sat(y);
-            m.fx[lev][q] = floor_to_int_sat(x);
-        }
-        cm_wave_fence();
-        if (lane < 2) {
-            const int lev = lane;
-            int ymin = 0x7fffffff, ymax = (int)0x80000000u, xmin = 0x7fffffff, xmax = (int)0x80000000u;
-#pragma unroll
-            for (int q = 0; q < NP; q++) {
-                ymin = min(ymin, m.fy[lev][q]); ymax = max(ymax, m.fy[lev][q]);
-                xmin = min(xmin, m.fx[lev][q]); xmax = max(xmax, m.fx[lev][q]);
-            }
-            const bool fast = ((int64_t)ymax - ymin) <= BOXMAX - D && ((int64_t)xmax - xmin) <= BOXMAX - D;
-            m.fast[lev] = fast;
-            m.oy[lev] = wrap_add(ymin, -R);
-            m.ox[lev] = wrap_add(xmin, -R);
-            m.bh[lev] = fast ? ymax - ymin + D : D;
-            m.bw[lev] = fast ? xmax - xmin + D : D;
-            // wide spreads: one 8x8 window per patch pixel, 4 tiles each
-            m.ntiles[lev] = fast ? (m.bh[lev] * m.bw[lev] + 15) / 16 : NP * 4;
-        }
-        cm_wave_fence();
-
-        // ---- A fragments: patch pixel (lane & 15) x 8 channels of each 32-channel step
-        h8_t a[4];
+        // ---- B fragments: patch pixel (lane & 15) x 8 channels of each 32-channel step
+        h8_t bq[4];
         {
-            const bool ok = ix_ok && q16 < NP;
-            const half_t* ga = p.gt + ((int64_t)(ok ? ix : 0) * NP + (ok ? q16 : 0)) * C + 8 * kc;
-#pragma unroll
-            for (int ks = 0; ks < 4; ks++) a[ks] = ok ? *(const h8_t*)(ga + 32 * ks) : hz;
-        }
-
-        // ---- box tiles of both levels.  Per-level constants are selected, never
-        // indexed by the runtime level: an indexed kernel argument is a memory
-        // load whose vmcnt(0) wait would drain the prefetched tiles every step.
-        const int nt0 = m.ntiles[0], ntot = nt0 + m.ntiles[1];
-        struct Lev { const half_t* base; int64_t s3, s4; int H, W, fast, bw, bh, oy, ox; bool ok; };
-        Lev L0, L1;
-#pragma unroll
-        for (int l = 0; l < 2; l++) {
-            Lev& L = l ? L1 : L0;
-            const bool jok = jx >= 0 && jx < p.N2[l];
-            L.base = p.fmap[l] + (jok ? (int64_t)jx * p.f_s1[l] : 0) + 8 * kc;
-            L.s3 = p.f_s3[l];
-            L.s4 = p.f_s4[l];
-            L.H = p.H2[l];
-            L.W = p.W2[l];
-            L.fast = m.fast[l];
-            L.bw = m.bw[l];
-            L.bh = m.bh[l];
-            L.oy = m.oy[l];
-            L.ox = m.ox[l];
-            L.ok = jok && ix_ok;
-        }
-        struct Src { const h8_t* ptr; bool inb; int lev, n, qq; };
-        auto locate = [&](int t) {
-            Src s;
-            s.lev = t >= nt0 ? 1 : 0;
-            const Lev& L = s.lev ? L1 : L0;
-            const int tl = s.lev ? t - nt0 : t;
-            int gy, gx;
-            bool valid;
-            if (L.fast) {
-                s.n = tl * 16 + q16;
-                s.qq = -1;
-                const int by = s.n / L.bw, bx = s.n - by * L.bw;
-                valid = s.n < L.bw * L.bh;
-                gy = wrap_add(L.oy, by);
-                gx = wrap_add(L.ox, bx);
-            } else {
-                s.qq = tl >> 2;
-                s.n = (tl & 3) * 16 + q16;
-                gy = wrap_add(m.fy[s.lev][s.qq], (s.n >> 3) - R);
-                gx = wrap_add(m.fx[s.lev][s.qq], (s.n & 7) - R);
-                valid = true;
-            }
-            s.inb = t < ntot && valid && L.ok && gy >= 0 && gy < L.H && gx >= 0 && gx < L.W;
-            s.ptr = reinterpret_cast<const h8_t*>(L.base + (s.inb ? (int64_t)gy * L.s3 + (int64_t)gx * L.s4 : 0));
-            return s;
-        };
-        // loads are unconditional (an out-of-box slot reads the map's first pixel)
-        // and masked at the MFMA: a load under a branch makes the wait counter
-        // unknown at the loop head, and the compiler then waits for everything
-        auto fetch = [&](const Src& s, h8_t* b) {
-#pragma unroll
-            for (int ks = 0; ks < 4; ks++) b[ks] = s.ptr[4 * ks];
-        };
-        auto consume = [&](const Src& s, const h8_t* b) {
-            f4m_t acc = {0.f, 0.f, 0.f, 0.f};
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<half_t*>(p.gt + (ix_ok ? (int64_t)ix * NP * C : 0)), (short)0, ix_ok ? NP * C * 2 : 0,
+                0x00020000);
+            const unsigned voff = qv ? (unsigned)(q16 * C * 2 + 16 * kc) : OOB;
 #pragma unroll
             for (int ks = 0; ks < 4; ks++)
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[ks], s.inb ? b[ks] : hz, acc, 0, 0, 0);
-            // acc[r] = patch pixel 4 kc + r . box slot s.n (out-of-box slots are zero and unread)
+                bq[ks] = __builtin_bit_cast(h8_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 64 * ks, 0, 0));
+        }
+
+        // ---- per level: scaled coordinates, floors, box, per-lane offsets
+        cm_wave_fence();   // the previous edge's epilogue has read wts / raw
+        CmLevel L0, L1;
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                const int row = 4 * kc + r;
-                if (row < NP && (s.qq < 0 || row == s.qq)) rw[s.lev][row][s.n] = acc[r];
+        for (int l = 0; l < 2; l++) {
+            CmLevel& L = l ? L1 : L0;
+            const float x = in.cx / p.scale[l], y = in.cy / p.scale[l];
+            L.fy = floor_to_int_sat(y);
+            L.fx = floor_to_int_sat(x);
+            if (lane < NP) {
+                const float dx = x - floorf(x), dy = y - floorf(y);
+                wts[wave][l][0][lane] = (1.f - dx) * (1.f - dy);
+                wts[wave][l][1][lane] = dx * (1.f - dy);
+                wts[wave][l][2][lane] = (1.f - dx) * dy;
+                wts[wave][l][3][lane] = dx * dy;
+            }
+            int ymin = __builtin_amdgcn_readlane(L.fy, 0), ymax = ymin;
+            int xmin = __builtin_amdgcn_readlane(L.fx, 0), xmax = xmin;
+#pragma unroll
+            for (int q = 1; q < NP; q++) {
+                const int vy = __builtin_amdgcn_readlane(L.fy, q), vx = __builtin_amdgcn_readlane(L.fx, q);
+                ymin = min(ymin, vy); ymax = max(ymax, vy);
+                xmin = min(xmin, vx); xmax = max(xmax, vx);
+            }
+            const bool jok = jx >= 0 && jx < p.N2[l];
+            L.frame = reinterpret_cast<const char*>(p.fmap[l] + (jok ? (int64_t)jx * p.f_s1[l] : 0));
+            L.rowb = p.rowb[l];
+            L.H = p.H2[l];
+            L.W = p.W2[l];
+            L.pixb = p.pixb[l];
+            L.rowext = jok && ix_ok ? p.rowext[l] : 0;
+            L.frameext = jok && ix_ok ? p.frameext[l] : 0;
+            L.fast = ((int64_t)ymax - ymin) <= BOXMAX - D && ((int64_t)xmax - xmin) <= BOXMAX - D;
+            L.oy = wrap_add(ymin, -R);
+            const int ox = wrap_add(xmin, -R);
+            const int bh = ymax - ymin + D, bw = xmax - xmin + D;
+            L.ntiles = L.fast ? bh : NP * 4;
+            const int gx = wrap_add(ox, q16);
+            L.voff = (q16 < bw && gx >= 0 && gx < p.W2[l]) ? (unsigned)(gx * p.pixb[l] + 16 * kc) : OOB;
+            L.wy0 = L.fy - ymin;
+            const int wx0 = L.fx - xmin;
+            // box column 4 kc + r is window column 4 kc + r - wx0 (in -4..15): LDS column + 4
+            L.sbase = l * RL + q16 * RQ + 4 * kc - wx0 + 4;
+        }
+
+        // ---- tiles of both levels: A = 16 pixels (box row, or two window rows), B = the patch.
+        // fetch and consume each walk the flat tile sequence with a cursor of
+        // scalar state advanced by increments (the level switch is a rare branch)
+        const int ntot = L0.ntiles + L1.ntiles;
+        struct FCur {
+            int lev, tl, ntl, fast, gy, H, W, pixb, num;
+            const char* base;   // fast: the current row; wide: the frame
+            const char* frame;
+            int64_t rowb;
+            unsigned voff;
+            int fy, fx;         // per lane
+        };
+        auto fstart = [&](const CmLevel& L, int lev) {
+            FCur c;
+            c.lev = lev;
+            c.tl = 0;
+            c.ntl = L.ntiles;
+            c.fast = L.fast;
+            c.gy = L.oy;
+            c.H = L.H;
+            c.W = L.W;
+            c.pixb = L.pixb;
+            c.num = L.fast ? L.rowext : L.frameext;
+            c.frame = L.frame;
+            c.base = L.frame + (int64_t)L.oy * L.rowb;
+            c.rowb = L.rowb;
+            c.voff = L.voff;
+            c.fy = L.fy;
+            c.fx = L.fx;
+            return c;
+        };
+        FCur fc = fstart(L0, 0);
+        auto fetch = [&](h8_t* a) {
+            if (fc.tl == fc.ntl) {
+                if (fc.lev == 0) {
+                    fc = fstart(L1, 1);
+                } else {   // past the last tile: nothing to read
+                    fc.lev = 2;
+                    fc.fast = 1;
+                    fc.num = 0;
+                    fc.ntl = 0x7fffffff;
+                }
+            }
+            const char* base;
+            int num;
+            unsigned voff;
+            if (fc.fast) {
+                base = fc.base;
+                num = (unsigned)fc.gy < (unsigned)fc.H ? fc.num : 0;
+                voff = fc.voff;
+                fc.base += fc.rowb;
+                fc.gy = wrap_add(fc.gy, 1);
+            } else {
+                const int qq = fc.tl >> 2, tt = fc.tl & 3;
+                const int gy = wrap_add(__builtin_amdgcn_readlane(fc.fy, qq), 2 * tt + (q16 >> 3) - R);
+                const int gx = wrap_add(__builtin_amdgcn_readlane(fc.fx, qq), (q16 & 7) - R);
+                const bool inb = gy >= 0 && gy < fc.H && gx >= 0 && gx < fc.W;
+                base = fc.frame;
+                num = fc.num;
+                voff = inb ? (unsigned)(gy * (int)fc.rowb + gx * fc.pixb + 16 * kc) : OOB;
+            }
+            fc.tl++;
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, num, 0x00020000);
+#pragma unroll
+            for (int ks = 0; ks < 4; ks++) {
+                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 64 * ks, 0, 0);
+                a[ks] = __builtin_bit_cast(h8_t, v);
             }
         };
-        Src s0 = locate(0), s1 = locate(1), s2 = locate(2);
-        h8_t b0[4], b1[4], b2[4];
+        int clev = 0, ctl = 0, cntl = L0.ntiles, cfast = L0.fast, cwy0 = L0.wy0, csb = L0.sbase;
+        auto consume = [&](int t, const h8_t* a) {
+            if (t >= ntot) return;
+            f4m_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < 4; ks++) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[ks], bq[ks], acc, 0, 0, 0);
+            // acc[r] = pixel 4 kc + r (of this tile's 16) . patch pixel (lane & 15)
+            if (ctl == cntl) {
+                clev = 1;
+                ctl = 0;
+                cntl = L1.ntiles;
+                cfast = L1.fast;
+                cwy0 = L1.wy0;
+                csb = L1.sbase;
+            }
+            if (cfast) {
+                const int wy = ctl - cwy0;
+                if (qv && (unsigned)wy < (unsigned)D) {
+                    float* dst = rw + csb + wy * RW;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) dst[r] = acc[r];
+                }
+            } else {
+                const int qq = ctl >> 2, tt = ctl & 3;
+                if (q16 == qq) {
+                    float* dst = rw + clev * RL + qq * RQ + (2 * tt + (kc >> 1)) * RW + 4 * (kc & 1) + 4;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) dst[r] = acc[r];
+                }
+            }
+            ctl++;
+        };
         // issue order must match consume order, or the wait at the loop head
         // (merged over the entry and the back edge) drains the whole ring
-        fetch(s0, b0);
+        h8_t b0[4], b1[4], b2[4], b3[4];
+        fetch(b0);
         __builtin_amdgcn_sched_barrier(0);
-        fetch(s1, b1);
+        fetch(b1);
         __builtin_amdgcn_sched_barrier(0);
-        fetch(s2, b2);
+        fetch(b2);
         __builtin_amdgcn_sched_barrier(0);
-        for (int t = 0; t < ntot; t += 3) {
-            consume(s0, b0);
-            s0 = locate(t + 3);
-            fetch(s0, b0);
-            if (t + 1 < ntot) consume(s1, b1);
-            s1 = locate(t + 4);
-            fetch(s1, b1);
-            if (t + 2 < ntot) consume(s2, b2);
-            s2 = locate(t + 5);
-            fetch(s2, b2);
+        fetch(b3);
+        __builtin_amdgcn_sched_barrier(0);
+        for (int t = 0; t < ntot; t += 4) {
+            consume(t, b0);
+            fetch(b0);
+            consume(t + 1, b1);
+            fetch(b1);
+            consume(t + 2, b2);
+            fetch(b2);
+            consume(t + 3, b3);
+            fetch(b3);
         }
         cm_wave_fence();
 
         // ---- bilinear 8x8 -> 7x7 per pixel and level (fp32), stacked row [x][y][P][P][level]
         half_t* orow = p.out + (int64_t)e * p.o_e;
-        for (int t = lane; t < DO * DO * NP; t += 64) {
-            const int pos = t / NP, q = t - pos * NP;
-            const int bxo = pos / DO, ay = pos - bxo * DO;   // x offset (outer), y offset
-            float v[2];
 #pragma unroll
-            for (int lev = 0; lev < 2; lev++) {
-                const float x = m.xs[lev][q], y = m.ys[lev][q];
-                const float dx = x - floorf(x), dy = y - floorf(y);
-                int base, st;
-                if (m.fast[lev]) {
-                    st = m.bw[lev];
-                    base = (m.fy[lev][q] - wrap_add(m.oy[lev], R)) * st + (m.fx[lev][q] - wrap_add(m.ox[lev], R));
-                } else {
-                    st = D;
-                    base = 0;
+        for (int i = 0; i < 7; i++) {
+            const int t = lane + 64 * i;
+            if (t < DO * DO * NP) {
+                const int q = eq[i];
+                float v[2];
+#pragma unroll
+                for (int lev = 0; lev < 2; lev++) {
+                    const float* r0 = rw + lev * RL + eoff[i];
+                    v[lev] = wts[wave][lev][0][q] * r0[0] + wts[wave][lev][1][q] * r0[1] +
+                             wts[wave][lev][2][q] * r0[RW] + wts[wave][lev][3][q] * r0[RW + 1];
                 }
-                const float* r0 = &rw[lev][q][base + ay * st + bxo];
-                v[lev] = (1.f - dx) * (1.f - dy) * r0[0] + dx * (1.f - dy) * r0[1] + (1.f - dx) * dy * r0[st] +
-                         dx * dy * r0[st + 1];
+                *(half2_t*)(orow + 2 * t) = half2_t{(half_t)v[0], (half_t)v[1]};
             }
-            *(half2_t*)(orow + 2 * t) = half2_t{(half_t)v[0], (half_t)v[1]};
         }
     }
 }
@@ -416,11 +510,18 @@ extern "C" int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, co
                        "fmaps must be channel-last with 16-byte aligned pixels");
         p.fmap[l] = (const half_t*)fmaps[l];
         p.f_s1[l] = ft[1];
-        p.f_s3[l] = ft[3];
-        p.f_s4[l] = ft[4];
         p.N2[l] = (int)fs[1];
         p.H2[l] = (int)fs[3];
         p.W2[l] = (int)fs[4];
+        // buffer offsets are 32-bit with OOB = 2^31 as "nothing": every pixel of a frame must lie below it
+        const int64_t rowext = fs[4] > 0 ? ((fs[4] - 1) * ft[4] + cm::C) * 2 : 0;
+        const int64_t frameext = fs[3] > 0 && fs[4] > 0 ? (fs[3] - 1) * ft[3] * 2 + rowext : 0;
+        DPVO_CHECK_ARG(frameext < (int64_t)cm::OOB - 256 && ft[3] * 2 < (int64_t)cm::OOB,
+                       "one frame of a feature map must span less than 2 GiB");
+        p.rowb[l] = ft[3] * 2;
+        p.pixb[l] = (int)(ft[4] * 2);
+        p.rowext[l] = (int)rowext;
+        p.frameext[l] = (int)frameext;
         p.scale[l] = level_scale[l];
     }
     DPVO_CHECK_ARG(reinterpret_cast<uintptr_t>(table) % 16 == 0, "table must be 16-byte aligned");
@@ -430,7 +531,10 @@ extern "C" int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, co
     DPVO_CHECK_ARG(reinterpret_cast<uintptr_t>(corr) % 4 == 0 && p.o_e % 2 == 0, "corr rows must be 4-byte aligned");
     if (E == 0) return 0;
     // persistent: a few workgroups per CU, each wave walking a grid-stride range of edges
-    const unsigned grid = (unsigned)std::min<int64_t>((E + cm::WAVES - 1) / cm::WAVES, 256 * 3);  // LDS: 3 per CU
+    // (a multiple of 8 once there are 8 workgroups' worth of edges: see cm_range)
+    int64_t g = std::min<int64_t>((E + cm::WAVES - 1) / cm::WAVES, 256 * 3);   // LDS and VGPRs: 3 per CU
+    if (g > 8) g &= ~int64_t(7);
+    const unsigned grid = (unsigned)g;
     hipLaunchKernelGGL(corr_mfma_kernel, dim3(grid), dim3(64 * cm::WAVES), 0, as_stream(stream), p);
     DPVO_CHECK_LAUNCH();
     return 0;

@@ -144,6 +144,75 @@ __global__ __launch_bounds__(MM_THREADS) void motion_mag_kernel(const float* pos
     if (t < 2) out[t] = s_cnt[t][0] ? s_sum[t][0] / (float)((int64_t)s_cnt[t][0] * PP) : __builtin_nanf("");
 }
 
+// Keyframe distance matrix for the global BA's distance-based edges
+// (dpvo.py:383-429 compute_keyframe_distance / get_distance_based_edges, which
+// call flow_mag twice and .item() once per frame pair -- O(n^2) host syncs).
+// dist[a][b] = mean over frame a's M patches and P*P pixels of flow_mag(a -> b)
+// (projective_ops.py:111-121), the same per-pixel arithmetic as
+// motion_mag_kernel.  One workgroup per (a, block of KF_TB targets): frame a's
+// back-projected pixels and their Gaa projection are staged in LDS once, each
+// target's sum is reduced in a fixed tree order (deterministic).
+constexpr int KF_THREADS = 256, KF_TB = 16;
+__global__ __launch_bounds__(KF_THREADS) void keyframe_flow_kernel(const float* poses, const float* patches, int P,
+                                                                  const float* intr, int64_t n, int64_t M,
+                                                                  float beta, float* dist)
+{
+    extern __shared__ float kf_sh[];
+    __shared__ float red[KF_THREADS];
+    const int t = threadIdx.x;
+    const int64_t a = blockIdx.x, b0 = (int64_t)blockIdx.y * KF_TB;
+    const int64_t PP = (int64_t)P * P, NPX = M * PP;
+    float* X0s = kf_sh;            // [4][NPX]
+    float* c0s = kf_sh + 4 * NPX;  // [2][NPX]
+    const G3 Pa = G3::load(poses + a * 7);
+    const G3 Pai = Pa.inv();
+    const G3 g0 = Pa.mul(Pai);     // transform(ii, ii): Gaa, as the reference composes it
+    const float* ka = intr + a * 4;
+    for (int64_t px = t; px < NPX; px += KF_THREADS) {
+        const int64_t k = px / PP, q = px - k * PP;
+        const float* pa = patches + (M * a + k) * 3 * PP;
+        const float X0[4] = {(pa[q] - ka[2]) / ka[0], (pa[PP + q] - ka[3]) / ka[1], 1.0f, pa[2 * PP + q]};
+        float X1[4];
+        g0.act4(X0, X1);
+        const float d = 1.0f / fmaxf(X1[2], 0.1f);
+#pragma unroll
+        for (int c = 0; c < 4; c++) X0s[c * NPX + px] = X0[c];
+        c0s[px] = ka[0] * (d * X1[0]) + ka[2];
+        c0s[NPX + px] = ka[1] * (d * X1[1]) + ka[3];
+    }
+    __syncthreads();
+    for (int bi = 0; bi < KF_TB; bi++) {
+        const int64_t b = b0 + bi;
+        if (b >= n) break;
+        const G3 g1 = G3::load(poses + b * 7).mul(Pai);
+        G3 g2 = g1;
+        g2.so3.q.x = 0.f; g2.so3.q.y = 0.f; g2.so3.q.z = 0.f; g2.so3.q.w = 1.f;
+        const float* kb = intr + b * 4;
+        float sum = 0.f;
+        for (int64_t px = t; px < NPX; px += KF_THREADS) {
+            const float X0[4] = {X0s[px], X0s[NPX + px], X0s[2 * NPX + px], X0s[3 * NPX + px]};
+            const float x0 = c0s[px], y0 = c0s[NPX + px];
+            float X1[4], X2[4];
+            g1.act4(X0, X1);
+            g2.act4(X0, X2);
+            const float d1 = 1.0f / fmaxf(X1[2], 0.1f), d2 = 1.0f / fmaxf(X2[2], 0.1f);
+            const float x1 = kb[0] * (d1 * X1[0]) + kb[2], y1 = kb[1] * (d1 * X1[1]) + kb[3];
+            const float x2 = kb[0] * (d2 * X2[0]) + kb[2], y2 = kb[1] * (d2 * X2[1]) + kb[3];
+            const float f1 = sqrtf((x1 - x0) * (x1 - x0) + (y1 - y0) * (y1 - y0));
+            const float f2 = sqrtf((x2 - x0) * (x2 - x0) + (y2 - y0) * (y2 - y0));
+            sum += beta * f1 + (1.0f - beta) * f2;
+        }
+        red[t] = sum;
+        __syncthreads();
+        for (int w = KF_THREADS / 2; w > 0; w >>= 1) {
+            if (t < w) red[t] += red[t + w];
+            __syncthreads();
+        }
+        if (t == 0) dist[a * n + b] = red[0] / (float)NPX;
+        __syncthreads();
+    }
+}
+
 }  // namespace dpvo
 
 using namespace dpvo;
@@ -185,6 +254,27 @@ extern "C" int dpvo_motion_mag(const float* poses, const float* patches, int P, 
     DPVO_CHECK_ARG(out && (num_edges == 0 || (poses && patches && intrinsics && ii && jj && kk)), "null operand");
     hipLaunchKernelGGL(motion_mag_kernel, dim3(1), dim3(MM_THREADS), 0, as_stream(stream), poses, patches, P,
                        intrinsics, ii, jj, kk, num_edges, i, j, beta, out);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" size_t dpvo_keyframe_flow_lds_bytes(int P, int64_t patches_per_frame)
+{
+    return (size_t)6 * P * P * patches_per_frame * sizeof(float);
+}
+
+extern "C" int dpvo_keyframe_flow(const float* poses, const float* patches, int P, const float* intrinsics,
+                                  int64_t num_frames, int64_t patches_per_frame, float beta, float* dist, void* stream)
+{
+    DPVO_CHECK_ARG(P >= 1 && num_frames >= 0 && patches_per_frame >= 1, "bad sizes");
+    DPVO_CHECK_ARG(num_frames < 65536 * (int64_t)KF_TB, "too many frames");
+    if (num_frames == 0) return 0;
+    DPVO_CHECK_ARG(poses && patches && intrinsics && dist, "null operand");
+    const size_t lds = dpvo_keyframe_flow_lds_bytes(P, patches_per_frame);
+    DPVO_CHECK_ARG(lds + KF_THREADS * sizeof(float) <= 160 * 1024, "one frame's patches do not fit in LDS");
+    const dim3 grid((unsigned)num_frames, (unsigned)((num_frames + KF_TB - 1) / KF_TB));
+    hipLaunchKernelGGL(keyframe_flow_kernel, grid, dim3(KF_THREADS), lds, as_stream(stream), poses, patches, P,
+                       intrinsics, num_frames, patches_per_frame, beta, dist);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

@@ -26,6 +26,7 @@
 
 #include <algorithm>
 #include <stdlib.h>
+#include <type_traits>
 
 namespace dpvo {
 namespace {
@@ -127,15 +128,46 @@ struct YMapFull {   // v1: 128-row tile over the consumed stage + extra region
     __device__ int off(int r, int byte) const { return ytile_off(cur_buf, r, byte); }
 };
 
-template <int FLAGS, int R, typename YMap>
-__device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, int64_t M, const char* smem, YMap ym,
-                                              int lrow0, int64_t row0, int lane, const EpiConsts& k)
+// The row epilogue in two halves: epi_load issues a batch's residual / gate
+// operand loads, epi_finish combines them with y and runs LN / heads / stores.
+// (v4 issues batch b + 1's loads before finishing batch b.)
+template <int R>
+struct EpiOps {
+    float2_t base[R][3];   // res32
+    half2_t add[R][3];     // res16[idx] or gate16
+};
+
+template <int FLAGS, int R>
+__device__ __forceinline__ void epi_load(const dpvo_rowgemm_args& p, int64_t M, int64_t row0, int lane, EpiOps<R>& o)
 {
-    float2_t v[R][3];
-    int64_t rows[R];
+    if (!(FLAGS & (RG_RES | RG_GATE))) return;
 #pragma unroll
     for (int q = 0; q < R; q++) {
-        rows[q] = row0 + q < M ? row0 + q : M - 1;   // clamped for loads; stores skip rows >= M
+        const int64_t row = row0 + q < M ? row0 + q : M - 1;   // clamped for loads; stores skip rows >= M
+        const float* r32 = (const float*)p.res32 + row * p.ldr;
+        const half_t* r16 = nullptr;
+        if (FLAGS & RG_GATE) {
+            r16 = (const half_t*)p.gate16 + row * RG_BN;
+        } else if (p.res16) {
+            const int64_t s = p.res16_idx ? p.res16_idx[row] : row;
+            r16 = s >= 0 ? (const half_t*)p.res16 + s * RG_BN : nullptr;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int c = 128 * j + 2 * lane;
+            o.base[q][j] = *(const float2_t*)(r32 + c);
+            o.add[q][j] = r16 ? *(const half2_t*)(r16 + c) : half2_t{(half_t)0, (half_t)0};
+        }
+    }
+}
+
+template <int FLAGS, int R, typename YMap>
+__device__ __forceinline__ void epi_finish(const dpvo_rowgemm_args& p, int64_t M, const char* smem, YMap ym, int lrow0,
+                                           int64_t row0, int lane, const EpiConsts& k, const EpiOps<R>& o)
+{
+    float2_t v[R][3];
+#pragma unroll
+    for (int q = 0; q < R; q++) {
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             const half2_t y = *(const half2_t*)(smem + ym.off(lrow0 + q, (128 * j + 2 * lane) * 2));
@@ -143,36 +175,15 @@ __device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, int64_
         }
     }
     if (FLAGS & (RG_RES | RG_GATE)) {
-        float2_t base[R][3];
-        float2_t add[R][3];
-#pragma unroll
-        for (int q = 0; q < R; q++) {
-            const float* r32 = (const float*)p.res32 + rows[q] * p.ldr;
-            const half_t* r16 = nullptr;
-            if (FLAGS & RG_GATE) {
-                r16 = (const half_t*)p.gate16 + rows[q] * RG_BN;
-            } else if (p.res16) {
-                const int64_t s = p.res16_idx ? p.res16_idx[rows[q]] : rows[q];
-                r16 = (const half_t*)p.res16 + (s >= 0 ? s : 0) * RG_BN;
-                if (s < 0) r16 = nullptr;
-            }
-#pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const int c = 128 * j + 2 * lane;
-                base[q][j] = *(const float2_t*)(r32 + c);
-                half2_t h = half2_t{(half_t)0, (half_t)0};
-                if (r16) h = *(const half2_t*)(r16 + c);
-                add[q][j] = float2_t{(float)h.x, (float)h.y};
-            }
-        }
 #pragma unroll
         for (int q = 0; q < R; q++)
 #pragma unroll
             for (int j = 0; j < 3; j++) {
+                const float2_t add = float2_t{(float)o.add[q][j].x, (float)o.add[q][j].y};
                 if (FLAGS & RG_GATE)   // x + fp16(gate * res)   (blocks.py:30, fp16 product)
-                    v[q][j] = base[q][j] + float2_t{hround(add[q][j].x * v[q][j].x), hround(add[q][j].y * v[q][j].y)};
+                    v[q][j] = o.base[q][j] + float2_t{hround(add.x * v[q][j].x), hround(add.y * v[q][j].y)};
                 else                   // (res32 + res16) + y
-                    v[q][j] = (base[q][j] + add[q][j]) + v[q][j];
+                    v[q][j] = (o.base[q][j] + add) + v[q][j];
             }
     }
     if (FLAGS & RG_LN) {
@@ -235,6 +246,16 @@ __device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, int64_
                 *(half2_t*)((half_t*)p.out16 + (row0 + q) * p.ldo16 + c) = half2_t{(half_t)v[q][j].x, (half_t)v[q][j].y};
         }
     }
+}
+
+
+template <int FLAGS, int R, typename YMap>
+__device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, int64_t M, const char* smem, YMap ym,
+                                              int lrow0, int64_t row0, int lane, const EpiConsts& k)
+{
+    EpiOps<R> o;
+    epi_load<FLAGS, R>(p, M, row0, lane, o);
+    epi_finish<FLAGS, R>(p, M, smem, ym, lrow0, row0, lane, k, o);
 }
 
 template <int FLAGS>
@@ -940,6 +961,283 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
     }
 }
 
+// ---------------------------------------------------------------------------
+// v4: one GEMM, or two chained (CHAIN), per 128-row tile, with the operand
+// streams decoupled from the MFMA waves.  v1-v3 stage W through LDS next to A
+// and synchronise all eight waves twice per k-step: every k-step then pays one
+// load latency (one stage in flight) and the waves' LDS reads and MFMAs run in
+// lockstep instead of overlapping.  Here
+//   - W never touches LDS: wave w owns output columns [48 w, 48 w + 48) and
+//     loads its own W fragments (3 x 16 B per lane per 32-wide k-step) straight
+//     into a 4-step register ring (W is L2-resident: 295 KB per layer);
+//   - A (the HBM stream, rows gathered through a_idx) goes global -> LDS by
+//     LDS-DMA into an 8-stage ring (8 KB per 32-wide stage), issued 3 groups of
+//     2 stages ahead, one barrier per group;
+//   - the 128 x 384 fp16 y tile (96 KB) holds GEMM1's activation (GEMM2's A
+//     operand) and the final y for the row epilogue (epilogue_rows, as v1-v3).
+// The flat sequence of (tile, k-step) runs persistently per workgroup, so the
+// next tile's first A stages and W fragments load under this tile's epilogue.
+// LDS: 96 KB + 64 KB = 160 KB (one workgroup, 8 waves, per CU).
+// ---------------------------------------------------------------------------
+constexpr int R4_BK = 32, R4_NS = 8, R4_G = 2, R4_AD = 3, R4_WD = 4;
+constexpr int R4_A_STAGE = RG_BM * R4_BK * 2;        // 8 KB
+constexpr int R4_Y = RG_BM * 768;                    // 96 KB
+constexpr int R4_LDS = R4_Y + R4_NS * R4_A_STAGE;    // 160 KB
+static_assert(R4_NS == (R4_AD + 1) * R4_G, "A ring = the groups in flight + the one being read");
+
+// DBG (timing experiments only, DPVO_RG4_DBG): 1 no epilogue, 2 no MFMA, 4 no A loads, 8 no W loads
+template <int F2, bool CHAIN, int DBG = 0>
+__global__ __launch_bounds__(RG_THREADS, 1) void rowgemm4_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p)
+{
+    __shared__ __attribute__((aligned(16))) char smem[R4_LDS];
+    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int fr = lane & 15, fq = lane >> 4;
+    const int K1 = p1.K;
+    const int S1 = K1 / R4_BK, S2 = CHAIN ? RG_BN / R4_BK : 0, S = S1 + S2;
+    const int GPT = S / R4_G;   // groups per tile
+    const int64_t Mrows = p1.M_dev ? min(*p1.M_dev, p1.M) : p1.M;
+    const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
+    if ((int64_t)blockIdx.x >= ntiles) return;
+    const int64_t my_tiles = (ntiles - 1 - blockIdx.x) / gridDim.x + 1;
+    const int64_t total_groups = my_tiles * GPT;
+    const YMapChunk ym;
+
+    // ---- W fragment streams: lane (fr, fq) of n-tile nt reads W row 48 w + 16 nt + fr, k 8 fq .. + 8
+    const half_t* w1b[3];
+    const half_t* w2b[3];
+#pragma unroll
+    for (int nt = 0; nt < 3; nt++) {
+        const int n = 48 * wave + 16 * nt + fr;
+        w1b[nt] = (const half_t*)p1.W + (int64_t)n * K1 + 8 * fq;
+        w2b[nt] = CHAIN ? (const half_t*)p.W + (int64_t)n * RG_BN + 8 * fq : w1b[nt];
+    }
+    const __amdgpu_buffer_rsrc_t nothing = __builtin_amdgcn_make_buffer_rsrc((void*)p1.bias, (short)0, 0, 0x00020000);
+    h8_t wr[R4_WD][3];
+    int wstep = 0;   // k-step (0 .. S-1) of the next W fetch, periodic: W does not depend on the tile
+    // W loads are issued by inline asm and waited for with counted vmcnt: the
+    // compiler's own wait placement goes conservative (vmcnt(0)) across the
+    // persistent loop's branches and would drain the ring every group.  Every
+    // k-step issues exactly 3 of them and every group start exactly 2 A-stream
+    // operations, so a fixed count covers the steady state (see step / group).
+    auto fetch_w = [&](h8_t (&dst)[3]) __attribute__((always_inline)) {
+        const bool g1 = wstep < S1;
+        const int k0 = R4_BK * (g1 ? wstep : wstep - S1);
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+            if (DBG & 8)
+                __builtin_amdgcn_raw_buffer_store_b32(0, nothing, 0, 0, 0);
+            else
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[nt]) : "v"((g1 ? w1b[nt] : w2b[nt]) + k0));
+        }
+        wstep = wstep + 1 == S ? 0 : wstep + 1;
+    };
+
+    // ---- A stream: LDS-DMA of 32-wide k-stages; wave w fills rows 16 w .. 16 w + 15
+    // (lane L: row 16 w + L / 4, 16-byte chunk L % 4), stage slots in issue order.
+    // Every group start issues exactly 3 vm operations -- 2 stage loads or 2
+    // dummies, and the next tile's gather index or a dummy -- so the counted
+    // waits below hold.  Dummies are stores through a zero-range descriptor:
+    // they count in vmcnt, touch no memory and, unlike a dummy load, leave no
+    // in-flight write to a register the compiler may have handed to something else.
+    const int arow = 16 * wave + (lane >> 2);
+    auto dummy_a = [&]() __attribute__((always_inline)) { __builtin_amdgcn_raw_buffer_store_b32(0, nothing, 0, 0, 0); };
+    // the next tile's gather index, loaded a whole tile (>= 3 groups) before its
+    // use, by asm: a compiler-visible load would get a compiler wait at the use,
+    // counted over the compiler's own loads only, i.e. a vmcnt(0) draining
+    // every stream once per tile.  The group-start wait covers it.
+    int64_t idx_next = 0;
+    auto fetch_idx = [&](int64_t t_ord) __attribute__((always_inline)) {
+        const int64_t m = (blockIdx.x + t_ord * gridDim.x) * RG_BM + arow;
+        if (p1.a_idx && t_ord < my_tiles && m < Mrows)
+            asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(idx_next) : "v"(p1.a_idx + m));
+        else
+            dummy_a();
+    };
+    auto row_of = [&](int64_t t_ord, int64_t idx) __attribute__((always_inline)) {
+        const int64_t m = (blockIdx.x + t_ord * gridDim.x) * RG_BM + arow;
+        const half_t* row = (const half_t*)p1.zero_row;
+        if (m < Mrows) {
+            const int64_t src = p1.a_idx ? idx : m;
+            if (src >= 0 && src < p1.a_rows) row = (const half_t*)p1.A + src * p1.lda;
+        }
+        return row + 8 * (lane & 3);
+    };
+    const half_t* asrc = nullptr;
+    int astage = 0;
+    int64_t ai_t = 0;   // tile ordinal (0 .. my_tiles) of the A cursor
+    int ac_gs = 0;      // its tile-local group
+    // advance the A cursor by one flat group: its stage loads when that group is
+    // a GEMM1 group, and on entering a tile the index fetch for the tile after
+    auto a_cursor_step = [&]() __attribute__((always_inline)) {
+        if (ac_gs < S1 / R4_G && ai_t < my_tiles) {
+            if (ac_gs == 0) {
+                if (GPT < 3) asm volatile("s_waitcnt vmcnt(0)" : "+v"(idx_next));   // fetched < 3 groups ago
+                asrc = row_of(ai_t, idx_next);
+            }
+#pragma unroll
+            for (int st = 0; st < R4_G; st++) {
+                const int k0 = R4_BK * (R4_G * ac_gs + st);
+                if (DBG & 4)
+                    dummy_a();
+                else
+                    glds16(asrc + k0, smem + R4_Y + (astage % R4_NS) * R4_A_STAGE + wave * 1024);
+                astage++;
+            }
+        } else {
+            dummy_a();
+            dummy_a();
+        }
+        if (ac_gs == 0)
+            fetch_idx(ai_t + 1);
+        else
+            dummy_a();
+        if (++ac_gs == GPT) {
+            ac_gs = 0;
+            ai_t++;
+        }
+    };
+
+    f4_t acc[8][3];
+    auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int mt = 0; mt < 8; mt++)
+#pragma unroll
+            for (int nt = 0; nt < 3; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+    };
+    // acc + bias -> act -> fp16 -> y tile: lane (fr, fq) holds row 16 mt + fr, columns 48 w + 16 nt + 4 fq + r
+    auto acc_to_y = [&](const h4_t (&bias)[3], bool relu, bool sigm) __attribute__((always_inline)) {
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+            const int col = 48 * wave + 16 * nt + 4 * fq;
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) {
+                h4_t y;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    half_t v = (half_t)(acc[mt][nt][r] + (float)bias[nt][r]);
+                    if (relu) v = v > (half_t)0 ? v : (half_t)0;
+                    if (sigm) v = (half_t)fast_sigmoid((float)v);
+                    y[r] = v;
+                }
+                *(h4_t*)(smem + ym.off(16 * mt + fr, col * 2)) = y;
+            }
+        }
+    };
+    auto sync_lds = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    // biases preloaded (a load at a GEMM's end would wait for every stream)
+    h4_t bias1[3], bias2[3];
+#pragma unroll
+    for (int nt = 0; nt < 3; nt++) {
+        const int col = 48 * wave + 16 * nt + 4 * fq;
+        bias1[nt] = *(const h4_t*)((const half_t*)p1.bias + col);
+        bias2[nt] = *(const h4_t*)((const half_t*)p.bias + col);
+    }
+
+    // ---- one k-step: A fragments (ring stage or y tile) x W fragments of ring slot SL
+    int cstage = 0;   // A stages consumed
+    auto step = [&](auto SLC, bool g1, int k2) __attribute__((always_inline)) {
+        constexpr int SL = decltype(SLC)::value;
+        // W(f) was issued R4_WD steps ago; 3 (R4_WD - 1) W loads and two group
+        // starts' 3 A-stream operations have been issued since (more around a
+        // tile's epilogue, which only makes this wait conservative)
+        asm volatile("s_waitcnt vmcnt(15)" : "+v"(wr[SL][0]), "+v"(wr[SL][1]), "+v"(wr[SL][2]));
+        h8_t a[8];
+        if (g1) {
+            const char* st = smem + R4_Y + (cstage % R4_NS) * R4_A_STAGE + fr * 64 + 16 * fq;
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) a[mt] = *(const h8_t*)(st + mt * 1024);
+            cstage++;
+        } else {
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) a[mt] = *(const h8_t*)(smem + ym.off(16 * mt + fr, (4 * k2 + fq) * 16));
+        }
+        if (!(DBG & 2)) {
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++)
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++)
+                    acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[SL][nt], a[mt], acc[mt][nt], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) acc[mt][0][0] += (float)a[mt][0] + (float)wr[SL][0][0];
+        }
+        // the refill goes after the MFMAs that read the slot: hoisted above them it
+        // would need fresh registers, and the wait for the slot's old loads would
+        // then also wait for the refill just issued
+        __builtin_amdgcn_sched_barrier(0);
+        fetch_w(wr[SL]);   // this slot's next use is R4_WD steps ahead
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: tile 0's gather index, W for steps 0 .. WD-1, A for flat groups 0 .. AD-1
+    fetch_idx(0);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(idx_next));
+#pragma unroll
+    for (int i = 0; i < R4_WD; i++) fetch_w(wr[i]);
+    for (int i = 0; i < R4_AD; i++) a_cursor_step();
+    zero_acc();
+
+    int64_t ti = 0;   // tile ordinal of the current group
+    int gs = 0;       // tile-local group
+    auto group = [&](auto PC, int64_t g) __attribute__((always_inline)) {
+        constexpr int P = decltype(PC)::value;
+        // this group's A stages were issued R4_AD groups ago; every group since
+        // issued 2 x 3 W fetches after them (the prologue is the exception)
+        // (lgkmcnt: acc_to_y's y-tile writes are published by this barrier)
+        if (g < R4_AD)
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        a_cursor_step();   // the ring slot it fills was read before this barrier
+        const bool g1 = gs < S1 / R4_G;
+        const int k2 = R4_G * (gs - S1 / R4_G);
+        step(std::integral_constant<int, 2 * P>{}, g1, k2);
+        step(std::integral_constant<int, 2 * P + 1>{}, g1, k2 + 1);
+        const int64_t tile = blockIdx.x + ti * gridDim.x;
+        if (CHAIN && gs == S1 / R4_G - 1) {
+            // GEMM1 done: its activation becomes GEMM2's A operand (the next
+            // group's barrier publishes it; nothing reads y until then)
+            acc_to_y(bias1, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
+            zero_acc();
+        }
+        if (gs == GPT - 1 && (DBG & 1)) zero_acc();
+        if (gs == GPT - 1 && !(DBG & 1)) {
+            if (CHAIN) sync_lds();   // every wave's last GEMM2 read of y is done
+            acc_to_y(CHAIN ? bias2 : bias1, F2 & RG_RELU, F2 & RG_SIGMOID);
+            sync_lds();
+            EpiConsts kc;   // loaded here, not held across the k-loop (register budget)
+            load_consts<F2>(p, lane, kc);
+            // the wave's 16 rows in 4 batches, each batch's residual / gate loads
+            // issued one batch ahead (a dependent gather index costs one more trip)
+            const int64_t r0 = tile * RG_BM + 16 * __builtin_amdgcn_readfirstlane(wave);
+            EpiOps<4> ops[2];
+            epi_load<F2, 4>(p, Mrows, r0, lane, ops[0]);
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                if (b + 1 < 4) epi_load<F2, 4>(p, Mrows, r0 + 4 * (b + 1), lane, ops[(b + 1) & 1]);
+                epi_finish<F2, 4>(p, Mrows, smem, ym, wave * 16 + 4 * b, r0 + 4 * b, lane, kc, ops[b & 1]);
+            }
+            zero_acc();
+        }
+        if (++gs == GPT) {
+            gs = 0;
+            ti++;
+        }
+    };
+    for (int64_t g = 0; g < total_groups; g += 2) {
+        group(std::integral_constant<int, 0>{}, g);
+        if (g + 1 < total_groups) group(std::integral_constant<int, 1>{}, g + 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing W prefetches
+}
+
 // v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16   (one wave per row)
 __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
 {
@@ -1040,12 +1338,61 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
     }
     static const int version = [] {
         // 1: one 128-row workgroup per CU; 2: two 64-row workgroups per CU;
-        // 3 (default): v1 tiling, A stream two stages ahead, transposed accumulators.
+        // 3 (default): v1 tiling, A stream two stages ahead, transposed accumulators;
+        // 4: W fragments streamed to registers, 8-stage A ring (rowgemm4_kernel) --
+        // measured no faster at C3 (profiles/r2/NOTES.md), kept for the experiment.
         // (Measured and dropped: stage fills through registers instead of LDS-DMA,
         // and v2 + register fills -- neither beat v3 on the C3 update operator.)
         const char* v = getenv("DPVO_ROWGEMM");
         return v ? atoi(v) : 3;
     }();
+    if (version == 4) {
+        const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
+        const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+        static const int dbg = [] {
+            const char* v = getenv("DPVO_RG4_DBG");
+            return v ? atoi(v) : 0;
+        }();
+        if (dbg && f == 0) {   // timing experiments (scripts/bench_rg4_dbg.py)
+            switch (dbg) {
+#define R4D_CASE(D)                                                                                                  \
+    case (D):                                                                                                        \
+        hipLaunchKernelGGL((rowgemm4_kernel<0, false, (D)>), dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, \
+                           *a);                                                                                      \
+        break;
+                R4D_CASE(1) R4D_CASE(2) R4D_CASE(3) R4D_CASE(4) R4D_CASE(5) R4D_CASE(6) R4D_CASE(8) R4D_CASE(9)
+                R4D_CASE(12) R4D_CASE(13) R4D_CASE(14) R4D_CASE(15)
+#undef R4D_CASE
+            default:
+                set_error("DPVO_RG4_DBG: unsupported value");
+                return -1;
+            }
+            DPVO_CHECK_LAUNCH();
+            return 0;
+        }
+        switch (f) {
+#define R4_CASE(F)                                                                                                \
+    case (F):                                                                                                     \
+        hipLaunchKernelGGL((rowgemm4_kernel<(F), false>), dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, \
+                           *a);                                                                                   \
+        break;
+            R4_CASE(0)
+            R4_CASE(DPVO_RG_RELU)
+            R4_CASE(DPVO_RG_SIGMOID)
+            R4_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
+            R4_CASE(DPVO_RG_RES)
+            R4_CASE(DPVO_RG_RES | DPVO_RG_LN)
+            R4_CASE(DPVO_RG_GATE | DPVO_RG_LN)
+            R4_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
+            R4_CASE(DPVO_RG_GATE)
+#undef R4_CASE
+        default:
+            set_error("dpvo_rowgemm: unsupported epilogue flag combination " + std::to_string(f));
+            return -1;
+        }
+        DPVO_CHECK_LAUNCH();
+        return 0;
+    }
     if (version == 2) {
         const int64_t nt2 = (a->M + R2_BM - 1) / R2_BM;
         const unsigned grid = (unsigned)std::min<int64_t>(nt2, 2 * (int64_t)g_num_cus);
@@ -1147,6 +1494,29 @@ extern "C" int dpvo_rowchain(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_arg
     dpvo_rowgemm_args a2 = *g2;
     a2.M = g1->M;
     a2.M_dev = g1->M_dev;
+    static const bool v4 = [] {
+        const char* v = getenv("DPVO_ROWGEMM");
+        return v && atoi(v) == 4;
+    }();
+    if (v4 && g1->K % 64 == 0) {
+        switch (f) {
+#define RC4_CASE(F)                                                                                              \
+    case (F):                                                                                                    \
+        hipLaunchKernelGGL((rowgemm4_kernel<(F), true>), dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *g1, \
+                           a2);                                                                                  \
+        break;
+            RC4_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
+            RC4_CASE(DPVO_RG_RES)
+            RC4_CASE(DPVO_RG_GATE | DPVO_RG_LN)
+            RC4_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
+#undef RC4_CASE
+        default:
+            set_error("dpvo_rowchain: unsupported epilogue flag combination " + std::to_string(f));
+            return -1;
+        }
+        DPVO_CHECK_LAUNCH();
+        return 0;
+    }
     switch (f) {
 #define RCH_CASE(F)                                                                                              \
     case (F):                                                                                                    \

@@ -345,6 +345,24 @@ class DPVO:
         return (0.5 * (fi(i, j).mean() + fi(j, i).mean())).item()
 
     def get_distance_based_edges(self):
+        """(ii, jj) device tensors: the sequential edges, then every (i, j),
+        j >= i + 2, whose keyframe distance is below DISTANCE_THRESH, in the
+        reference's row-major order (dpvo.py:409-429).  All pair distances come
+        from one keyframe_flow launch and one compaction -- the reference's
+        loop makes two flow_mag calls and a host read per pair."""
+        d = self.device
+        if not self.use_distance_edges or self.n < 2:
+            e = torch.zeros(0, dtype=torch.long, device=d)
+            return e, e
+        n = self.n
+        D = pops.keyframe_flow(SE3(self.poses), self.patches, self.intrinsics, n, self.M, beta=0.5)
+        dist = 0.5 * (D + D.t())
+        near = torch.triu(dist < self.distance_thresh, diagonal=2).nonzero()
+        seq = torch.arange(n - 1, device=d)
+        return torch.cat([seq, near[:, 0]]), torch.cat([seq + 1, near[:, 1]])
+
+    def _distance_edges_loop(self):
+        """the reference's pair loop (dpvo.py:409-429), for tests"""
         if not self.use_distance_edges or self.n < 2:
             return [], []
         ii = list(range(self.n - 1))
@@ -371,7 +389,7 @@ class DPVO:
                 for j in range(i + 10, min(i + 20, self.n)):
                     ii_e.append(i)
                     jj_e.append(j)
-        if not ii_e:
+        if len(ii_e) == 0:
             return
         d, M = self.device, self.M
         ie = torch.as_tensor(ii_e, device=d)

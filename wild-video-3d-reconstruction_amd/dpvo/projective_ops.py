@@ -80,6 +80,20 @@ def motion_mag_pair(poses, patches, intrinsics, ii, jj, kk, i, j, beta=0.5):
     return out
 
 
+def keyframe_flow(poses, patches, intrinsics, n, M, beta=0.5):
+    """[n, n] device matrix: dist[a, b] = mean flow_mag of frame a's M patches
+    into frame b (projective_ops.py:111-121) -- every pair of
+    compute_keyframe_distance (dpvo.py:383-407) in one launch; the reference's
+    pair distance is 0.5 (dist[i, j] + dist[j, i])."""
+    data = poses.data.contiguous()
+    patches, intrinsics = patches.contiguous(), intrinsics.contiguous()
+    P = patches.shape[-1]
+    out = torch.empty(n, n, dtype=torch.float32, device=data.device)
+    H.check(H.lib().dpvo_keyframe_flow(H.ptr(data), H.ptr(patches), P, H.ptr(intrinsics), int(n), int(M), float(beta),
+                                       H.ptr(out), H.stream_of(data)))
+    return out
+
+
 def transform(poses, patches, intrinsics, ii, jj, kk, depth=False, valid=False, jacobian=False, tonly=False):
     """Reproject patch kk from frame ii into frame jj (poses are world->camera)."""
     if not jacobian and _fusable(poses, patches, intrinsics):
