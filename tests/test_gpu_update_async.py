@@ -1,0 +1,70 @@
+"""DPVO.update() without host synchronisation, and replayed from a HIP graph
+(VERDICT r1 item 6).  BA's Cholesky status is written to a device word and
+read at keyframe()'s existing host read (or check_ba()); the reference raises
+inside the call (ba_cuda.cu:521) -- same error, one frame later."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def make(seed=3, buffer=72):
+    from dpvo.synthetic import steady_state_tracker
+    return steady_state_tracker("dpvo_2k", buffer=buffer, seed=seed)
+
+
+def test_update_makes_no_host_sync():
+    slam = make()
+    with torch.no_grad():
+        slam.update()                       # caches (gmap table, packed weights) filled
+        torch.cuda.synchronize()
+        torch.cuda.set_sync_debug_mode("error")
+        try:
+            slam.update()
+        finally:
+            torch.cuda.set_sync_debug_mode("default")
+    slam.check_ba()                         # and the BA status was fine
+
+
+def test_graph_replay_equals_eager():
+    a, b = make(seed=5), make(seed=5)
+    with torch.no_grad():
+        for _ in range(4):
+            a.update()
+            b.update_graphed()
+    torch.cuda.synchronize()
+    n, m = a.n, a.pg.m
+    assert b._ugraph is not None                       # calls 2-4 were replays
+    assert torch.equal(a.pg.poses_[:n], b.pg.poses_[:n])
+    assert torch.equal(a.pg.patches_[:m], b.pg.patches_[:m])
+    assert torch.equal(a.pg.net, b.pg.net)
+    assert torch.equal(a.pg.points_[:m], b.pg.points_[:m])
+    assert torch.equal(a.pg.target, b.pg.target) and torch.equal(a.pg.weight, b.pg.weight)
+
+
+def test_graph_recaptures_when_edges_change():
+    slam = make(seed=6)
+    with torch.no_grad():
+        slam.update_graphed()
+        g0 = slam._ugraph[1]
+        slam.update_graphed()
+        assert slam._ugraph[1] is g0
+        keep = torch.arange(slam.pg.ii.numel() - 500, device=slam.device)
+        slam.pg.ii, slam.pg.jj, slam.pg.kk = slam.pg.ii[keep], slam.pg.jj[keep], slam.pg.kk[keep]
+        slam.pg.net, slam.pg.target, slam.pg.weight = slam.pg.net[:, keep], slam.pg.target[:, keep], slam.pg.weight[:, keep]
+        slam.update_graphed()
+        assert slam._ugraph[1] is not g0
+    assert torch.isfinite(slam.pg.poses_[:slam.n]).all()
+
+
+def test_deferred_ba_failure_raises_at_the_next_host_read():
+    slam = make(seed=7)
+    with torch.no_grad():
+        slam.update()
+        slam._ba_fail.fill_(7)              # as if a BA Cholesky had failed at minor 7
+        with pytest.raises(RuntimeError, match="leading minor of order 7 is not positive-definite"):
+            slam.keyframe()
+        slam.check_ba()                     # reported once, then cleared
+        slam._ba_fail.fill_(-1)
+        with pytest.raises(RuntimeError, match="patch index out of range"):
+            slam.check_ba()

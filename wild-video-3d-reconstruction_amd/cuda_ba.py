@@ -8,7 +8,9 @@ Same module name, functions and argument meaning as dpvo/fastba/ba.cpp:236-241
 when the Schur system is not positive definite (torch::linalg::cholesky in
 ba_cuda.cu:521 raises); it costs one device->host read of a status word per
 call.  Set it to False for fully asynchronous / graph-captured use; the
-status is then left in ``last_status`` (a device tensor).
+status is then left in ``last_status`` (a device tensor).  A caller may
+instead pass ``status=`` (a device int32 tensor): the call then never reads
+it, and the caller raises later (DPVO.update does, at keyframe()'s host read).
 
 Windows of up to 12 optimised poses (DPVO's sliding window) take the
 deterministic per-patch path: no float atomics, bitwise repeatable.  It
@@ -32,10 +34,25 @@ DETERMINISTIC = True
 last_status = None
 
 
-def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, iterations, csr=None):
+def raise_for_status(s):
+    """the reference's error for a BA status word (0: no error)."""
+    s = int(s)
+    if s > 0:
+        raise RuntimeError(
+            "linalg.cholesky: The factorization could not be completed because the input is not positive-"
+            f"definite (the leading minor of order {s} is not positive-definite).")
+    if s < 0:
+        raise RuntimeError("cuda_ba.forward: patch index out of range")
+
+
+def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, iterations, csr=None,
+            status=None):
     """ba.cpp:31-43 -> ba_cuda.cu:422-540.  Updates poses and patches in place; returns [].
     csr (optional, not in the reference): (offs int32 [E+1], perm int32 [E],
-    groups int64 [1]) of update_ops.group_by(kk) for these edges."""
+    groups int64 [1]) of update_ops.group_by(kk) for these edges.
+    status (optional, not in the reference): a device int32 [1] the call's
+    status word is written to instead of being read here -- no host
+    synchronisation; the caller checks it later (raise_for_status)."""
     global last_status
     H.on_gpu(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk)
     for name, t in (("poses", poses), ("patches", patches), ("intrinsics", intrinsics), ("target", target),
@@ -53,7 +70,12 @@ def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t
     flags = (1 if SPARSE else 0) | (0 if DETERMINISTIC else 2)
     nbytes = H.lib().dpvo_ba_workspace_bytes_ex(E, num_patches, max(N, 0), flags)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=poses.device)
-    status = torch.zeros(1, dtype=torch.int32, device=poses.device)
+    deferred = status is not None
+    if deferred:
+        if status.dtype != torch.int32 or status.numel() < 1 or status.device != poses.device:
+            raise RuntimeError("status must be a device int32 tensor of at least one element")
+    else:
+        status = torch.zeros(1, dtype=torch.int32, device=poses.device)
     offs = perm = groups = None
     if csr is not None:
         offs, perm, groups = csr
@@ -66,14 +88,8 @@ def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t
         H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(t0), int(t1), int(iterations), flags, H.ptr(offs), H.ptr(perm),
         H.ptr(groups), H.ptr(ws), nbytes, H.ptr(status), H.stream_of(poses)))
     last_status = status
-    if CHECK_CHOLESKY:
-        s = int(status.item())
-        if s > 0:
-            raise RuntimeError(
-                "linalg.cholesky: The factorization could not be completed because the input is not positive-"
-                f"definite (the leading minor of order {s} is not positive-definite).")
-        if s < 0:
-            raise RuntimeError("cuda_ba.forward: patch index out of range")
+    if CHECK_CHOLESKY and not deferred:
+        raise_for_status(status.item())
     return []
 
 

@@ -17,6 +17,7 @@ import torch
 import torch.nn.functional as F
 
 import cuda_corr
+import cuda_ba
 import update_ops
 
 from . import altcorr, fastba
@@ -78,6 +79,11 @@ class DPVO:
         self.pg = PatchGraph(cfg, P, DIM, self.pmem, self.M, h, w, RES, device=self.device, dtype=dt)
         self.warm_up = 10
         self._lmbda = torch.as_tensor([1e-4], device=self.device)
+        # BA status words (cuda_ba.forward(status=)): the last call's, and the
+        # first failure since the last host check -- update() never syncs
+        self._ba_status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._ba_fail = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self._ugraph = None
         self._identity = SE3.Identity(1, device=self.device)
 
     # ------------------------------------------------------------------ state views
@@ -157,6 +163,7 @@ class DPVO:
         return dP * self.get_pose(t0)
 
     def terminate(self):
+        self.check_ba()
         if self.enable_global_ba:
             self.global_bundle_adjustment()
         self.traj = {self.pg.tstamps_[i].item(): self.pg.poses_[i] for i in range(self.n)}
@@ -289,18 +296,64 @@ class DPVO:
         with Timer("BA", enabled=self.enable_timing):
             t0_ = self.n - self.cfg.OPTIMIZATION_WINDOW if self.is_initialized else 1
             t0 = max(t0_, t0 or 1)
+            defer = getattr(self.cfg, "DEFER_BA_CHECK", True)
+            if defer:
+                self._ba_status.zero_()
             fastba.BA(self.poses, self.patches, self.intrinsics, target, weight, self._lmbda, self.pg.ii, self.pg.jj,
-                      self.pg.kk, t0, self.n, getattr(self.cfg, "BA_ITERATIONS", 2), csr=kk_groups[1:])
+                      self.pg.kk, t0, self.n, getattr(self.cfg, "BA_ITERATIONS", 2), csr=kk_groups[1:],
+                      status=self._ba_status if defer else None)
+            if defer:   # keep the first failure until a host read looks at it
+                torch.where(self._ba_fail == 0, self._ba_status, self._ba_fail, out=self._ba_fail)
             m = self.pg.m
             pops.point_cloud_centre(SE3(self.poses), self.patches[:, :m], self.intrinsics, self.ix[:m],
                                     out=self.pg.points_[:m])
+
+    def check_ba(self, status=None):
+        """raise the reference's BA error (ba_cuda.cu:521) if an update() since
+        the last check failed; status: that word already read by the caller."""
+        if status is None:
+            status = int(self._ba_fail.item())
+        if status:
+            self._ba_fail.zero_()
+            cuda_ba.raise_for_status(status)
+
+    def update_graphed(self, t0=None):
+        """update(), replayed from a HIP graph while the patch graph is
+        unchanged.  The first call for a given edge set runs update() eagerly
+        and captures it (no host synchronisation happens inside update());
+        later calls replay it: one launch instead of ~60 from Python.  The
+        capture is keyed on everything its kernels' arguments depend on (edge
+        tensors, n, t0, the gmap ring's version); keyframe() / new frames
+        change the key and the next call captures again."""
+        if not getattr(self.cfg, "DEFER_BA_CHECK", True):
+            raise RuntimeError("update_graphed needs cfg.DEFER_BA_CHECK (no host read inside update())")
+        key = (self.pg.ii.data_ptr(), self.pg.jj.data_ptr(), self.pg.kk.data_ptr(), self.pg.ii.numel(), self.n,
+               t0, self.gmap_._version, self.pg.net.data_ptr(), self.pg.net.shape)
+        if self._ugraph is not None and self._ugraph[0] == key:
+            self._ugraph[1].replay()
+            self.pg.target, self.pg.weight = self._ugraph[2]
+            return
+        self._ugraph = None
+        self.update(t0)                    # this call's update, eagerly (also warms every cache)
+        net_in = self.pg.net               # the state the graph reads and (copied back) writes
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.update(t0)
+            net_in.copy_(self.pg.net)
+        outs = (self.pg.target, self.pg.weight)
+        self.pg.net = net_in
+        self._ugraph = ((self.pg.ii.data_ptr(), self.pg.jj.data_ptr(), self.pg.kk.data_ptr(), self.pg.ii.numel(),
+                         self.n, t0, self.gmap_._version, net_in.data_ptr(), net_in.shape), g, outs)
 
     def keyframe(self):
         """drop a redundant keyframe, retire old edges (dpvo.py:605-658)."""
         k = self.n - self.cfg.KEYFRAME_INDEX
         i, j = k - 1, k + 1
-        # one host read for both directions (the reference reads each, :609)
-        m = sum(self._motionmag_dev(i, j).tolist())
+        # one host read for both directions (the reference reads each, :609),
+        # and for the deferred BA status of the update()s since the last one
+        vals = torch.cat([self._motionmag_dev(i, j), self._ba_fail.float()]).tolist()
+        self.check_ba(int(vals[2]))
+        m = vals[0] + vals[1]
         if m / 2 < self.cfg.KEYFRAME_THRESH:
             t0, t1 = self.pg.tstamps_[k - 1:k + 1].tolist()
             dP = SE3(self.pg.poses_[k]) * SE3(self.pg.poses_[k - 1]).inv()
