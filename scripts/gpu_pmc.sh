@@ -13,7 +13,7 @@ i=0
 IFS=';' read -ra GROUPS_ <<< "$PASSES"
 for G in "${GROUPS_[@]}"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $G --kernel-include-regex "${KREGEX}" -f csv -d "$OUT/p$i" -o run -- python "$REPO/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/p$i.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --pmc $G --kernel-include-regex "${KREGEX}" -f csv -d "$OUT/p$i" -o run -- python "$REPO/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --e2e-frames 0 > "$OUT/p$i.log" 2>&1
   rc=$?; echo "pass $i ($G) rc=$rc"
   [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.log"; exit $rc; }
 done

@@ -1562,8 +1562,7 @@ static size_t nb_sort_temp_bytes(int64_t E)
 constexpr int BD_NMAX = 12;
 constexpr int BD_N6MAX = 6 * BD_NMAX;     // 72
 constexpr int BD_WAVES = 4;
-constexpr int BD_GRID = 256;
-constexpr int BD_OWN = 11;                // augmented lower-triangle entries per solve thread (2700 / 256)
+constexpr int BD_GRID = 1024;   // 4 waves each: 4096 waves, enough to hide the per-patch load chains
 
 struct BdLayout {
     size_t hdr, gid, offs, perm, groups, gbws, gbws_bytes, Em, Cg, ug, Hpart, H, dX, total;
@@ -1935,88 +1934,144 @@ __global__ __launch_bounds__(1024) void bd_reduce_kernel(BdParams p, int nparts)
 }
 
 // damping S += diag(1e-4 S + 1) (ba_cuda.cu:517-518), fp32 Cholesky of the
-// augmented [S; g^T] (one barrier per column), back substitution, retraction
+// augmented [S; g^T], back substitution, retraction.  The factor is blocked by
+// pose (6 x 6 blocks): per block column one thread factors the diagonal block,
+// one thread per remaining row solves its panel row, and the trailing update
+// (a 6-term dot product per entry) is spread over the workgroup -- three
+// barriers per pose instead of one per column.  The augmented row n rides
+// along as an extra panel row, so it ends as z = L^-1 g.
+constexpr int BS_LD = BD_N6MAX + 4;   // 76: quad-aligned rows (the trailing update reads float4s)
+typedef float bs_f4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void bd_solve_kernel(BdParams p)
 {
-    __shared__ float colbuf[2][BD_N6MAX + 1];
-    __shared__ float Lm[(BD_N6MAX + 1) * BD_N6MAX];
+    __shared__ __attribute__((aligned(16))) float A[(BD_N6MAX + 1) * BS_LD];   // lower triangle, rows 0..n (row n = g^T)
+    __shared__ __attribute__((aligned(16))) float PT[6][BS_LD];                // the current panel, transposed
     __shared__ float xs[BD_N6MAX];
     __shared__ float dinv[BD_N6MAX];
+    __shared__ int sfail;
     if (*(volatile int*)p.status != 0) return;
-    const int n = p.n6, tid = threadIdx.x;
-    const int ntri = n * (n + 1) / 2, ne = ntri + n;
-    float a[BD_OWN];
-    int rr[BD_OWN], cc[BD_OWN];
+    const int n = p.n6, tid = threadIdx.x, N = p.N;
+    // every load issued before any is used: one L2 round trip, not one per entry
+    constexpr int NLD = ((BD_N6MAX + 1) * BD_N6MAX + 255) / 256;
+    float hv[NLD];
 #pragma unroll
-    for (int s = 0; s < BD_OWN; s++) {
-        const int t = tid + 256 * s;
-        int r = -1, c = -1;
-        float v = 0.f;
-        if (t < ntri) {
-            r = (int)((sqrtf(8.f * (float)t + 1.f) - 1.f) * 0.5f);
-            while (r * (r + 1) / 2 > t) r--;
-            while ((r + 1) * (r + 2) / 2 <= t) r++;
-            c = t - r * (r + 1) / 2;
-            v = p.H[tri_up(c, r, n)];
+    for (int s2 = 0; s2 < NLD; s2++) {
+        const int t = tid + 256 * s2;
+        const int r = t / max(n, 1), c = t - r * n;
+        int src = -1;
+        if (t < (n + 1) * n) src = r == n ? p.nup + c : (c <= r ? tri_up(c, r, n) : -1);
+        hv[s2] = p.H[src < 0 ? 0 : src];
+        if (src < 0) hv[s2] = 0.f;
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < NLD; s2++) {
+        const int t = tid + 256 * s2;
+        if (t < (n + 1) * n) {
+            const int r = t / n, c = t - r * n;
+            float v = hv[s2];
             if (r == c) v += 1e-4f * v + 1.0f;
-        } else if (t < ne) {
-            r = n;
-            c = t - ntri;
-            v = p.H[p.nup + c];
+            A[r * BS_LD + c] = v;
         }
-        rr[s] = r;
-        cc[s] = c;
-        a[s] = v;
-        if (c == 0) colbuf[0][r] = v;
     }
-    // clamped copies of the owned (row, column) pairs: the column reads below
-    // are issued together, unconditionally, and waited for once per column
-    int rq[BD_OWN], cq[BD_OWN];
+    if (tid == 0) sfail = 0;
+    __syncthreads();
+    for (int kb = 0; kb < N; kb++) {
+        const int k0 = 6 * kb;
+        // 1. the diagonal block, in place (one thread; the pivots in column order)
+        if (tid == 0) {
+            float L[6][6];
 #pragma unroll
-    for (int s = 0; s < BD_OWN; s++) {
-        rq[s] = rr[s] < 0 ? 0 : rr[s];
-        cq[s] = cc[s] < 0 ? 0 : cc[s];
-    }
-    int fail = 0;
-    for (int j = 0; j < n; j++) {
+            for (int i = 0; i < 6; i++)
+#pragma unroll
+                for (int j = 0; j <= i; j++) L[i][j] = A[(k0 + i) * BS_LD + k0 + j];
+            int fail = 0;
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                float d = L[j][j];
+#pragma unroll
+                for (int t = 0; t < j; t++) d -= L[j][t] * L[j][t];
+                if (!(d > 0.f) && !fail) fail = k0 + j + 1;
+                const float l = sqrtf(d), il = 1.0f / l;
+                L[j][j] = l;
+                dinv[k0 + j] = il;
+#pragma unroll
+                for (int i = j + 1; i < 6; i++) {
+                    float v = L[i][j];
+#pragma unroll
+                    for (int t = 0; t < j; t++) v -= L[i][t] * L[j][t];
+                    L[i][j] = v * il;
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 6; i++)
+#pragma unroll
+                for (int j = 0; j <= i; j++) A[(k0 + i) * BS_LD + k0 + j] = L[i][j];
+            sfail = fail;
+        }
         __syncthreads();
-        const float* cur = colbuf[j & 1];
-        float* nxt = colbuf[(j + 1) & 1];
-        float vr[BD_OWN], vc[BD_OWN];
+        if (sfail) break;
+        // 2. panel rows below the block (and the augmented row n): x L_kk^T = a
+        const int c1 = k0 + 6;   // first trailing column
+        const int rows = n + 1 - c1;
+        if (tid < rows) {
+            const int r = c1 + tid;
+            float x[6];
 #pragma unroll
-        for (int s = 0; s < BD_OWN; s++) {
-            vr[s] = cur[rq[s]];
-            vc[s] = cur[cq[s]];
-        }
-        const float d = cur[j];
-        if (!(d > 0.f)) {
-            fail = j + 1;
-            break;
-        }
-        const float invd = 1.0f / d, invl = 1.0f / sqrtf(d);
-        if (tid == 0) dinv[j] = invl;
+            for (int t = 0; t < 6; t++) {
+                float v = A[r * BS_LD + k0 + t];
 #pragma unroll
-        for (int s = 0; s < BD_OWN; s++) {
-            const int c = cc[s];
-            const float na = a[s] - vr[s] * vc[s] * invd;
-            if (c == j) Lm[rq[s] * n + j] = a[s] * invl;
-            a[s] = c > j ? na : a[s];
-            if (c == j + 1) nxt[rq[s]] = a[s];
+                for (int s2 = 0; s2 < t; s2++) v -= A[(k0 + t) * BS_LD + k0 + s2] * x[s2];
+                x[t] = v * dinv[k0 + t];
+            }
+#pragma unroll
+            for (int t = 0; t < 6; t++) {
+                A[r * BS_LD + k0 + t] = x[t];
+                PT[t][r] = x[t];
+            }
         }
+        __syncthreads();
+        // 3. trailing update A[r][c] -= L[r][k0:k0+6] . L[c][k0:k0+6] for c1 <= c <= r
+        // (row n: every c < n), four columns per item from the transposed panel
+        const int q0 = c1 >> 2, nq = ((n + 3) >> 2) - q0;
+        for (int it = tid; it < rows * nq; it += 256) {
+            const int ri = it / nq;
+            const int r = c1 + ri, c0 = 4 * (q0 + it - ri * nq);
+            if (r < n && c0 > r) continue;
+            float lr[6];
+#pragma unroll
+            for (int t = 0; t < 6; t++) lr[t] = PT[t][r];
+            bs_f4 v = *(const bs_f4*)(A + r * BS_LD + c0);
+            bs_f4 u = v;
+#pragma unroll
+            for (int t = 0; t < 6; t++) {
+                const bs_f4 lc = *(const bs_f4*)(&PT[t][c0]);
+                u.x -= lr[t] * lc.x;
+                u.y -= lr[t] * lc.y;
+                u.z -= lr[t] * lc.z;
+                u.w -= lr[t] * lc.w;
+            }
+            // only c1 <= c (and c <= r below row n, c < n on it) change
+            const int lim = r < n ? r : n - 1;
+            v.x = (c0 + 0 >= c1 && c0 + 0 <= lim) ? u.x : v.x;
+            v.y = (c0 + 1 >= c1 && c0 + 1 <= lim) ? u.y : v.y;
+            v.z = (c0 + 2 >= c1 && c0 + 2 <= lim) ? u.z : v.z;
+            v.w = (c0 + 3 >= c1 && c0 + 3 <= lim) ? u.w : v.w;
+            *(bs_f4*)(A + r * BS_LD + c0) = v;
+        }
+        __syncthreads();
     }
-    if (fail) {
-        if (tid == 0) atomicExch(p.status, fail);
+    if (sfail) {
+        if (tid == 0) atomicExch(p.status, sfail);
         return;
     }
-    __syncthreads();
     // L^T x = z, z = row n of the augmented factor; lane c holds x_c / z_c
     if (tid < 64) {
-        float z0 = tid < n ? Lm[n * n + tid] : 0.f, z1 = tid + 64 < n ? Lm[n * n + tid + 64] : 0.f;
+        float z0 = tid < n ? A[n * BS_LD + tid] : 0.f, z1 = tid + 64 < n ? A[n * BS_LD + tid + 64] : 0.f;
         for (int j = n - 1; j >= 0; j--) {
             const float zj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(j < 64 ? z0 : z1), j & 63));
             const float xj = zj * dinv[j];
-            if (tid < j) z0 -= Lm[j * n + tid] * xj;
-            if (tid + 64 < j) z1 -= Lm[j * n + tid + 64] * xj;
+            if (tid < j) z0 -= A[j * BS_LD + tid] * xj;
+            if (tid + 64 < j) z1 -= A[j * BS_LD + tid + 64] * xj;
             if (tid == (j & 63)) {
                 if (j < 64) z0 = xj;
                 else z1 = xj;
