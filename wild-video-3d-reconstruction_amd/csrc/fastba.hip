@@ -1625,9 +1625,11 @@ __device__ __forceinline__ int tri_up(int a, int b, int n6) { return a * (2 * n6
 __device__ __forceinline__ float wave64_allsum(float s)
 {
     s = row16_sum(s);
-    s += __shfl_xor(s, 16);
-    s += __shfl_xor(s, 32);
-    return s;
+    // gfx950 lane swaps (VALU, no LDS round trip): rows 0+1 / 2+3, then halves
+    auto h = __builtin_amdgcn_permlane16_swap(__float_as_int(s), __float_as_int(s), false, false);
+    s = __int_as_float(h[0]) + __int_as_float(h[1]);
+    auto w = __builtin_amdgcn_permlane32_swap(__float_as_int(s), __float_as_int(s), false, false);
+    return __int_as_float(w[0]) + __int_as_float(w[1]);
 }
 
 __device__ __forceinline__ unsigned wave_or(unsigned v)
@@ -1884,6 +1886,7 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         if (lane + 64 < n6) Er[lane + 64] = e1;
         if (lane == 0) { p.Cg[g] = Ck; p.ug[g] = uk; }
         // Schur term: H -= Q e e^T (upper), g -= Q u e, over the touched poses
+        // (e_a from the lanes' registers: no LDS round trip per entry)
         const float Q = 1.0f / (Ck + lm);
         const float qu = Q * uk;
         for (unsigned tm = touched; tm; tm &= tm - 1) {
@@ -1891,12 +1894,15 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
 #pragma unroll
             for (int t = 0; t < 6; t++) {
                 const int a = 6 * pa + t;
-                const float qa = Q * ev[a];
+                const float ea = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a < 64 ? e0 : e1), a & 63));
+                const float qa = Q * ea;
                 if (lane >= a && lane < n6) atomicAdd(&part[tri_up(a, lane, n6)], -qa * e0);
                 if (lane + 64 >= a && lane + 64 < n6) atomicAdd(&part[tri_up(a, lane + 64, n6)], -qa * e1);
-                if (lane == 0) part[nup + a] -= qu * ev[a];
             }
         }
+        // g -= Q u e over the touched poses' entries, one lane per entry
+        if (lane < n6 && (touched >> (lane / 6) & 1)) part[nup + lane] -= qu * e0;
+        if (lane + 64 < n6 && (touched >> ((lane + 64) / 6) & 1)) part[nup + lane + 64] -= qu * e1;
         wave_lds_fence();
     }
     if (!pose_terms) return;
