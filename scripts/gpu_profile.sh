@@ -16,7 +16,7 @@ rc=$?; echo "trace rc=$rc"; tail -3 "$OUT/trace.log"
 [ $rc -eq 0 ] || exit $rc
 [ "${PMC:-1}" = "1" ] || exit 0
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "${KREGEX:-corr_mfma}" -f csv -d "$OUT/pmc_$C" -o run -- python "$REPO/bench.py" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pmc_$C.log" 2>&1
+  timeout -k 10 600 rocprofv3 --pmc $C --kernel-include-regex "${KREGEX:-corr_mfma}" -f csv -d "$OUT/pmc_$C" -o run -- python "$REPO/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --e2e-frames 0 > "$OUT/pmc_$C.log" 2>&1
   rc=$?; echo "pmc $C rc=$rc"; tail -2 "$OUT/pmc_$C.log"
   [ $rc -eq 0 ] || exit $rc
 done

@@ -17,11 +17,15 @@ import sys
 KERNEL = re.compile(os.environ.get("KREGEX", r"corr_mfma_kernel|corr_s?fast_kernel<2"))
 
 
+NAMES = set()
+
+
 def per_dispatch(d, counter):
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter and KERNEL.search(r["Kernel_Name"]):
+                NAMES.add(r["Kernel_Name"].split("(")[0])
                 vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     if not vals:
         raise SystemExit(f"no {counter} rows for the altcorr kernel under {d}")
@@ -37,7 +41,7 @@ def main():
     med = lambda v: v[len(v) // 2]
     fetch = med(fk) * 1024 * 2      # KB -> B, gfx950 x2 for 16-B/lane streaming reads
     write = med(wk) * 1024
-    res = {"kernel": "corr_sfast_kernel<2,16>", "edges": edges, "fetch_bytes": round(fetch),
+    res = {"kernel": " / ".join(sorted(NAMES)), "edges": edges, "fetch_bytes": round(fetch),
            "write_bytes": round(write), "hbm_bytes_per_launch": round(fetch + write),
            "bytes_per_edge": round((fetch + write) / edges, 1), "dispatches": [len(fk), len(wk)],
            "note": "rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes; FETCH x2 (gfx950); "

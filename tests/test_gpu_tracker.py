@@ -258,3 +258,76 @@ def test_motion_mag_matches_oracle(slam):
                     assert abs(g - w) <= 1e-4 * max(1.0, abs(w)), (i, j, g, w)
         # the tracker's single-direction accessor agrees with the pair
         assert abs(slam.motionmag(n - 5, n - 3) - ref(n - 5, n - 3)) <= 1e-4 * max(1.0, ref(n - 5, n - 3))
+
+
+class _RefEdges:
+    """The reference's edge bookkeeping written out with Python lists:
+    __edges_forw / __edges_back appended per frame (dpvo.py:756-769, 860-861),
+    keyframe()'s removal and renumbering (:605-640) and the removal window
+    (:657).  Independent of the tracker's tensor code."""
+
+    def __init__(self, cfg):
+        self.M, self.r = cfg.PATCHES_PER_FRAME, cfg.PATCH_LIFETIME
+        self.win, self.kfi = cfg.REMOVAL_WINDOW, cfg.KEYFRAME_INDEX
+        self.n = 0
+        self.ii, self.jj, self.kk = [], [], []
+
+    def add_frame(self):
+        self.n += 1
+        n, M, r = self.n, self.M, self.r
+        for k in range(M * max(n - r, 0), M * max(n - 1, 0)):       # forward: old patches -> new frame
+            self.kk.append(k); self.jj.append(n - 1); self.ii.append(k // M)
+        for k in range(M * max(n - 1, 0), M * n):                    # backward: new patches -> recent frames
+            for j in range(max(n - r, 0), n):
+                self.kk.append(k); self.jj.append(j); self.ii.append(k // M)
+
+    def keyframe(self, drop):
+        k = self.n - self.kfi
+        e = list(zip(self.ii, self.jj, self.kk))
+        if drop:
+            e = [(i, j, kk) for i, j, kk in e if i != k and j != k]
+            e = [(i - 1 if i > k else i, j - 1 if j > k else j, kk - self.M if i > k else kk) for i, j, kk in e]
+            self.n -= 1
+        e = [(i, j, kk) for i, j, kk in e if kk // self.M >= self.n - self.win]
+        self.ii, self.jj, self.kk = (list(t) for t in zip(*e)) if e else ([], [], [])
+
+
+def test_edge_construction_follows_reference_rules():
+    """Row a9: the tracker's (ii, jj, kk) after every frame equals the
+    reference's rules applied to the same frame / keyframe decisions; the
+    keyframe threshold alternates so both the drop and the keep path run."""
+    from dpvo.config import make_cfg
+    from dpvo.dpvo import DPVO
+    from dpvo.net import VONet
+    from dpvo.synthetic import image_stream
+    torch.manual_seed(0)
+    net = VONet()
+    with torch.no_grad():
+        net.update.d[1].weight.mul_(40.0)  # random weights: make the motion probe pass
+    cfg = make_cfg("fast", BUFFER_SIZE=64)
+    intr = torch.tensor([320.0, 320.0, 320.0, 240.0], device="cuda")
+    ref = _RefEdges(cfg)
+    decisions = []
+    with torch.no_grad():
+        slam = DPVO(cfg, net, ht=384, wd=512)
+        orig_kf = slam.keyframe
+
+        def keyframe():
+            drop = len(decisions) % 2 == 0
+            slam.cfg.KEYFRAME_THRESH = float("inf") if drop else -1.0
+            decisions.append(drop)
+            orig_kf()
+        slam.keyframe = keyframe
+        for t, img in image_stream(26):
+            n0, init0, nd = slam.n, slam.is_initialized, len(decisions)
+            slam(t, img, None, None, intr)
+            if not init0 and slam.n == n0:
+                continue                       # skipped by the motion probe: no frame, no edges
+            ref.add_frame()
+            if len(decisions) > nd:
+                ref.keyframe(decisions[-1])
+            assert slam.n == ref.n
+            assert slam.pg.ii.tolist() == ref.ii, t
+            assert slam.pg.jj.tolist() == ref.jj, t
+            assert slam.pg.kk.tolist() == ref.kk, t
+    assert True in decisions and False in decisions
