@@ -28,9 +28,8 @@ namespace dpvo {
 
 namespace cm {
 constexpr int R = 3, D = 8, DO = 7, NP = 9, C = 128, BOXMAX = 12, WAVES = 4;
-constexpr int RW = 20;            // LDS window row: 8 columns at 4..11, the rest catches out-of-window box columns
-constexpr int RQ = D * RW + 4;    // LDS window stride per patch pixel
-constexpr int RL = NP * RQ;       // per level
+constexpr int RS = 148;           // LDS row per patch pixel: the box's <= 144 pixels (+ pad: rows 4 apart, 16 banks apart)
+constexpr int RL = NP * RS;       // per level
 constexpr unsigned OOB = 0x80000000u;   // a buffer offset past every descriptor's range: the load returns 0
 }  // namespace cm
 
@@ -110,34 +109,35 @@ __device__ __forceinline__ CmEdgeIn cm_load_edge(const CorrMfmaParams& p, int sl
 
 // Per edge and level: the pixels the nine 8x8 windows need.  When the nine
 // floors lie within 4 of each other ("fast") that is one box of at most 12x12
-// pixels, visited one box ROW per tile: the A operand is 16 consecutive
-// pixels of the row (lanes past the box width read nothing), so a lane's load
-// offset is the same for every row of the level and the row itself is the
-// buffer descriptor's base -- wave-uniform scalar work.  Otherwise each patch
-// pixel's own window is visited, two window rows (16 pixels) per tile.
+// pixels, enumerated row-major and visited 16 pixels per tile: every lane of
+// every tile loads a box pixel (only the last tile has a tail), which keeps the
+// vector-memory address work -- what bounds this kernel -- at the box's size.
+// Each lane walks its pixel (box row, column) by increments.  Otherwise each
+// patch pixel's own window is visited, two window rows (16 pixels) per tile.
+// Either way the product of tile pixel n and patch pixel q lands at
+// raw[level][q][16 tile + n]: four consecutive floats per lane.
 struct CmLevel {
     const char* frame;    // this target frame's map (byte pointer), wave-uniform
     int64_t rowb;         // row stride in bytes
-    int H, W, pixb, rowext, frameext;
-    int fast, oy, ntiles;
-    // per lane (fast): load offset of box column (lane & 15); window origin of
-    // patch pixel (lane & 15) inside the box; LDS slot base and row mask
-    unsigned voff;
-    int wy0, sbase;
-    int fy, fx;           // per lane: floors of patch pixel (lane & 15) (wide path)
+    int H, W, pixb, frameext;
+    int fast, oy, ox, bw, npx, ntiles;
+    int by, bx;           // per lane: box pixel (lane & 15) of the first tile (fast)
+    int fy, fx;           // per lane: floors of patch pixel (lane & 15)
 };
 
 // One wave per edge, persistent over a contiguous per-XCD range of edge
 // slots.  The next edge's indices and coordinates are in flight while the
 // current edge runs; the tiles of both levels are one flat sequence whose A
 // fragments are loaded four tiles ahead (a static register ring).  Products
-// land in a per-wave LDS window [level][patch pixel][8][RW] (fp32), from which
-// the bilinear epilogue writes 256-byte coalesced rows.
+// land in a per-wave LDS box [level][patch pixel][RS] (fp32), from which the
+// bilinear epilogue reads each pixel's window and writes 256-byte coalesced rows.
 __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParams p)
 {
     using namespace cm;
-    __shared__ float raw[WAVES][2 * RL];
+    __shared__ __attribute__((aligned(16))) float raw[WAVES][2 * RL];
     __shared__ float wts[WAVES][2][4][16];   // bilinear weights per level and patch pixel
+    __shared__ int ebase[WAVES][2][16];      // window origin of each patch pixel inside its raw row
+    __shared__ int estr[WAVES][2];           // raw row stride of the window (box width, or 8)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const CmRange rg = cm_range(p.E, wave);
     int slot = rg.slot;
@@ -147,14 +147,15 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
     const bool qv = q16 < NP;
 
     // epilogue: output t = lane + 64 i is (x offset, y offset, patch pixel) = ((t / 9) / 7, (t / 9) % 7, t % 9)
-    int eoff[7], eq[7];
+    int eq[7], ex[7], ey[7];
 #pragma unroll
     for (int i = 0; i < 7; i++) {
         const int t = min(lane + 64 * i, DO * DO * NP - 1);
         const int pos = t / NP, q = t - pos * NP;
         const int bxo = pos / DO, ay = pos - bxo * DO;
         eq[i] = q;
-        eoff[i] = q * RQ + ay * RW + bxo + 4;
+        ex[i] = bxo;
+        ey[i] = ay;
     }
 
     CmEdgeIn nin = cm_load_edge(p, slot, q16);
@@ -178,8 +179,8 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
                 bq[ks] = __builtin_bit_cast(h8_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 64 * ks, 0, 0));
         }
 
-        // ---- per level: scaled coordinates, floors, box, per-lane offsets
-        cm_wave_fence();   // the previous edge's epilogue has read wts / raw
+        // ---- per level: scaled coordinates, floors, box, per-lane walk start
+        cm_wave_fence();   // the previous edge's epilogue has read wts / raw / ebase
         CmLevel L0, L1;
 #pragma unroll
         for (int l = 0; l < 2; l++) {
@@ -187,13 +188,6 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
             const float x = in.cx / p.scale[l], y = in.cy / p.scale[l];
             L.fy = floor_to_int_sat(y);
             L.fx = floor_to_int_sat(x);
-            if (lane < NP) {
-                const float dx = x - floorf(x), dy = y - floorf(y);
-                wts[wave][l][0][lane] = (1.f - dx) * (1.f - dy);
-                wts[wave][l][1][lane] = dx * (1.f - dy);
-                wts[wave][l][2][lane] = (1.f - dx) * dy;
-                wts[wave][l][3][lane] = dx * dy;
-            }
             int ymin = __builtin_amdgcn_readlane(L.fy, 0), ymax = ymin;
             int xmin = __builtin_amdgcn_readlane(L.fx, 0), xmax = xmin;
 #pragma unroll
@@ -208,32 +202,35 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
             L.H = p.H2[l];
             L.W = p.W2[l];
             L.pixb = p.pixb[l];
-            L.rowext = jok && ix_ok ? p.rowext[l] : 0;
             L.frameext = jok && ix_ok ? p.frameext[l] : 0;
             L.fast = ((int64_t)ymax - ymin) <= BOXMAX - D && ((int64_t)xmax - xmin) <= BOXMAX - D;
             L.oy = wrap_add(ymin, -R);
-            const int ox = wrap_add(xmin, -R);
-            const int bh = ymax - ymin + D, bw = xmax - xmin + D;
-            L.ntiles = L.fast ? bh : NP * 4;
-            const int gx = wrap_add(ox, q16);
-            L.voff = (q16 < bw && gx >= 0 && gx < p.W2[l]) ? (unsigned)(gx * p.pixb[l] + 16 * kc) : OOB;
-            L.wy0 = L.fy - ymin;
-            const int wx0 = L.fx - xmin;
-            // box column 4 kc + r is window column 4 kc + r - wx0 (in -4..15): LDS column + 4
-            L.sbase = l * RL + q16 * RQ + 4 * kc - wx0 + 4;
+            L.ox = wrap_add(xmin, -R);
+            L.bw = L.fast ? xmax - xmin + D : D;
+            const int bh = L.fast ? ymax - ymin + D : D;
+            L.npx = L.bw * bh;
+            L.ntiles = L.fast ? (L.npx + 15) / 16 : NP * 4;
+            L.by = q16 / L.bw;
+            L.bx = q16 - L.by * L.bw;
+            if (lane < NP) {
+                const float dx = x - floorf(x), dy = y - floorf(y);
+                wts[wave][l][0][lane] = (1.f - dx) * (1.f - dy);
+                wts[wave][l][1][lane] = dx * (1.f - dy);
+                wts[wave][l][2][lane] = (1.f - dx) * dy;
+                wts[wave][l][3][lane] = dx * dy;
+                // the window of pixel q starts at box (fy - ymin, fx - xmin); wide: its own 8 x 8
+                ebase[wave][l][lane] = L.fast ? (L.fy - ymin) * L.bw + (L.fx - xmin) : 0;
+            }
+            if (lane == 0) estr[wave][l] = L.bw;
         }
 
-        // ---- tiles of both levels: A = 16 pixels (box row, or two window rows), B = the patch.
-        // fetch and consume each walk the flat tile sequence with a cursor of
-        // scalar state advanced by increments (the level switch is a rare branch)
+        // ---- tiles of both levels: A = 16 box pixels (or two window rows), B = the patch.
         const int ntot = L0.ntiles + L1.ntiles;
         struct FCur {
-            int lev, tl, ntl, fast, gy, H, W, pixb, num;
-            const char* base;   // fast: the current row; wide: the frame
-            const char* frame;
+            int lev, tl, ntl, fast, oy, ox, bw, npx, H, W, pixb, num;
             int64_t rowb;
-            unsigned voff;
-            int fy, fx;         // per lane
+            const char* frame;
+            int by, bx, fy, fx;   // per lane
         };
         auto fstart = [&](const CmLevel& L, int lev) {
             FCur c;
@@ -241,15 +238,18 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
             c.tl = 0;
             c.ntl = L.ntiles;
             c.fast = L.fast;
-            c.gy = L.oy;
+            c.oy = L.oy;
+            c.ox = L.ox;
+            c.bw = L.bw;
+            c.npx = L.npx;
             c.H = L.H;
             c.W = L.W;
             c.pixb = L.pixb;
-            c.num = L.fast ? L.rowext : L.frameext;
-            c.frame = L.frame;
-            c.base = L.frame + (int64_t)L.oy * L.rowb;
+            c.num = L.frameext;
             c.rowb = L.rowb;
-            c.voff = L.voff;
+            c.frame = L.frame;
+            c.by = L.by;
+            c.bx = L.bx;
             c.fy = L.fy;
             c.fx = L.fx;
             return c;
@@ -261,67 +261,54 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
                     fc = fstart(L1, 1);
                 } else {   // past the last tile: nothing to read
                     fc.lev = 2;
-                    fc.fast = 1;
                     fc.num = 0;
                     fc.ntl = 0x7fffffff;
                 }
             }
-            const char* base;
-            int num;
-            unsigned voff;
+            int gy, gx;
+            bool inb;
             if (fc.fast) {
-                base = fc.base;
-                num = (unsigned)fc.gy < (unsigned)fc.H ? fc.num : 0;
-                voff = fc.voff;
-                fc.base += fc.rowb;
-                fc.gy = wrap_add(fc.gy, 1);
+                gy = wrap_add(fc.oy, fc.by);
+                gx = wrap_add(fc.ox, fc.bx);
+                inb = 16 * fc.tl + q16 < fc.npx;
+                // next tile: 16 pixels on (the box is at least 8 wide: at most two row wraps)
+                fc.bx += 16;
+                if (fc.bx >= fc.bw) { fc.bx -= fc.bw; fc.by++; }
+                if (fc.bx >= fc.bw) { fc.bx -= fc.bw; fc.by++; }
             } else {
                 const int qq = fc.tl >> 2, tt = fc.tl & 3;
-                const int gy = wrap_add(__builtin_amdgcn_readlane(fc.fy, qq), 2 * tt + (q16 >> 3) - R);
-                const int gx = wrap_add(__builtin_amdgcn_readlane(fc.fx, qq), (q16 & 7) - R);
-                const bool inb = gy >= 0 && gy < fc.H && gx >= 0 && gx < fc.W;
-                base = fc.frame;
-                num = fc.num;
-                voff = inb ? (unsigned)(gy * (int)fc.rowb + gx * fc.pixb + 16 * kc) : OOB;
+                gy = wrap_add(__builtin_amdgcn_readlane(fc.fy, qq), 2 * tt + (q16 >> 3) - R);
+                gx = wrap_add(__builtin_amdgcn_readlane(fc.fx, qq), (q16 & 7) - R);
+                inb = true;
             }
+            inb = inb && gy >= 0 && gy < fc.H && gx >= 0 && gx < fc.W;
+            const unsigned voff = inb ? (unsigned)(gy * (int)fc.rowb + gx * fc.pixb + 16 * kc) : OOB;
             fc.tl++;
             const __amdgpu_buffer_rsrc_t rs =
-                __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(base), (short)0, num, 0x00020000);
+                __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(fc.frame), (short)0, fc.num, 0x00020000);
 #pragma unroll
             for (int ks = 0; ks < 4; ks++) {
                 const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 64 * ks, 0, 0);
                 a[ks] = __builtin_bit_cast(h8_t, v);
             }
         };
-        int clev = 0, ctl = 0, cntl = L0.ntiles, cfast = L0.fast, cwy0 = L0.wy0, csb = L0.sbase;
+        int clev = 0, ctl = 0, cntl = L0.ntiles;
         auto consume = [&](int t, const h8_t* a) {
             if (t >= ntot) return;
             f4m_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int ks = 0; ks < 4; ks++) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[ks], bq[ks], acc, 0, 0, 0);
-            // acc[r] = pixel 4 kc + r (of this tile's 16) . patch pixel (lane & 15)
+            // acc[r] = tile pixel 4 kc + r . patch pixel (lane & 15)
             if (ctl == cntl) {
                 clev = 1;
                 ctl = 0;
                 cntl = L1.ntiles;
-                cfast = L1.fast;
-                cwy0 = L1.wy0;
-                csb = L1.sbase;
             }
-            if (cfast) {
-                const int wy = ctl - cwy0;
-                if (qv && (unsigned)wy < (unsigned)D) {
-                    float* dst = rw + csb + wy * RW;
-#pragma unroll
-                    for (int r = 0; r < 4; r++) dst[r] = acc[r];
-                }
-            } else {
-                const int qq = ctl >> 2, tt = ctl & 3;
-                if (q16 == qq) {
-                    float* dst = rw + clev * RL + qq * RQ + (2 * tt + (kc >> 1)) * RW + 4 * (kc & 1) + 4;
-#pragma unroll
-                    for (int r = 0; r < 4; r++) dst[r] = acc[r];
-                }
+            const bool fast = clev ? L1.fast : L0.fast;
+            // wide path: tile ctl holds rows 2 (ctl & 3) .. + 1 of pixel ctl / 4's window only
+            if (qv && (fast || q16 == (ctl >> 2))) {
+                const int n = fast ? 16 * ctl : 16 * (ctl & 3);
+                *(f4m_t*)(rw + clev * RL + q16 * RS + n + 4 * kc) = acc;
             }
             ctl++;
         };
@@ -350,6 +337,7 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
 
         // ---- bilinear 8x8 -> 7x7 per pixel and level (fp32), stacked row [x][y][P][P][level]
         half_t* orow = p.out + (int64_t)e * p.o_e;
+        const int st0 = estr[wave][0], st1 = estr[wave][1];
 #pragma unroll
         for (int i = 0; i < 7; i++) {
             const int t = lane + 64 * i;
@@ -358,9 +346,10 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
                 float v[2];
 #pragma unroll
                 for (int lev = 0; lev < 2; lev++) {
-                    const float* r0 = rw + lev * RL + eoff[i];
+                    const int st = lev ? st1 : st0;
+                    const float* r0 = rw + lev * RL + q * RS + ebase[wave][lev][q] + ey[i] * st + ex[i];
                     v[lev] = wts[wave][lev][0][q] * r0[0] + wts[wave][lev][1][q] * r0[1] +
-                             wts[wave][lev][2][q] * r0[RW] + wts[wave][lev][3][q] * r0[RW + 1];
+                             wts[wave][lev][2][q] * r0[st] + wts[wave][lev][3][q] * r0[st + 1];
                 }
                 *(half2_t*)(orow + 2 * t) = half2_t{(half_t)v[0], (half_t)v[1]};
             }

@@ -985,7 +985,8 @@ constexpr int R4_Y = RG_BM * 768;                    // 96 KB
 constexpr int R4_LDS = R4_Y + R4_NS * R4_A_STAGE;    // 160 KB
 static_assert(R4_NS == (R4_AD + 1) * R4_G, "A ring = the groups in flight + the one being read");
 
-// DBG (timing experiments only, DPVO_RG4_DBG): 1 no epilogue, 2 no MFMA, 4 no A loads, 8 no W loads
+// DBG (timing experiments only, DPVO_RG4_DBG): 1 no epilogue, 2 no MFMA, 4 no A loads, 8 no W loads,
+// 16 no row pass (acc -> y tile only)
 template <int F2, bool CHAIN, int DBG = 0>
 __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm4_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p)
 {
@@ -1212,6 +1213,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm4_kernel(dpvo_rowgemm_ar
             if (CHAIN) sync_lds();   // every wave's last GEMM2 read of y is done
             acc_to_y(CHAIN ? bias2 : bias1, F2 & RG_RELU, F2 & RG_SIGMOID);
             sync_lds();
+            if (!(DBG & 16)) {
             EpiConsts kc;   // loaded here, not held across the k-loop (register budget)
             load_consts<F2>(p, lane, kc);
             // the wave's 16 rows in 4 batches, each batch's residual / gate loads
@@ -1223,6 +1225,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm4_kernel(dpvo_rowgemm_ar
             for (int b = 0; b < 4; b++) {
                 if (b + 1 < 4) epi_load<F2, 4>(p, Mrows, r0 + 4 * (b + 1), lane, ops[(b + 1) & 1]);
                 epi_finish<F2, 4>(p, Mrows, smem, ym, wave * 16 + 4 * b, r0 + 4 * b, lane, kc, ops[b & 1]);
+            }
             }
             zero_acc();
         }
@@ -1349,10 +1352,8 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
     if (version == 4) {
         const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
         const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
-        static const int dbg = [] {
-            const char* v = getenv("DPVO_RG4_DBG");
-            return v ? atoi(v) : 0;
-        }();
+        const char* dbgs = getenv("DPVO_RG4_DBG");   // read per call: timing experiments switch it in-process
+        const int dbg = dbgs ? atoi(dbgs) : 0;
         if (dbg && f == 0) {   // timing experiments (scripts/bench_rg4_dbg.py)
             switch (dbg) {
 #define R4D_CASE(D)                                                                                                  \
@@ -1361,7 +1362,7 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
                            *a);                                                                                      \
         break;
                 R4D_CASE(1) R4D_CASE(2) R4D_CASE(3) R4D_CASE(4) R4D_CASE(5) R4D_CASE(6) R4D_CASE(8) R4D_CASE(9)
-                R4D_CASE(12) R4D_CASE(13) R4D_CASE(14) R4D_CASE(15)
+                R4D_CASE(12) R4D_CASE(13) R4D_CASE(14) R4D_CASE(15) R4D_CASE(16) R4D_CASE(22) R4D_CASE(30)
 #undef R4D_CASE
             default:
                 set_error("DPVO_RG4_DBG: unsupported value");
