@@ -1272,18 +1272,23 @@ __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
             v[2 * j + 1] = a.y;
         }
         if (p.ln_g) {
+            // row reductions with DPP rotations and gfx950 lane swaps: VALU only,
+            // no LDS round trip (the butterfly's order, so every lane agrees)
+            auto allsum = [](float x) {
+                x = rowsum16(x);
+                auto h = __builtin_amdgcn_permlane16_swap(__float_as_int(x), __float_as_int(x), false, false);
+                x = __int_as_float(h[0]) + __int_as_float(h[1]);
+                auto w = __builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(x), false, false);
+                return __int_as_float(w[0]) + __int_as_float(w[1]);
+            };
             float s = 0.f;
 #pragma unroll
             for (int j = 0; j < 6; j++) s += v[j];
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
-            const float mean = s * (1.f / RG_BN);
+            const float mean = allsum(s) * (1.f / RG_BN);
             float q = 0.f;
 #pragma unroll
             for (int j = 0; j < 6; j++) q += (v[j] - mean) * (v[j] - mean);
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) q += __shfl_xor(q, o);
-            const float rstd = rsqrtf(q * (1.f / RG_BN) + p.ln_eps);
+            const float rstd = rsqrtf(allsum(q) * (1.f / RG_BN) + p.ln_eps);
 #pragma unroll
             for (int j = 0; j < 3; j++) {
                 const int c = 128 * j + 2 * lane;
