@@ -246,6 +246,13 @@ int dpvo_transform(const float* poses, const float* patches, int P, const float*
 int dpvo_motion_mag(const float* poses, const float* patches, int P, const float* intrinsics, const int64_t* ii,
                     const int64_t* jj, const int64_t* kk, int64_t num_edges, int64_t i, int64_t j, float beta,
                     float* out, void* stream);
+/* The same over many workgroups (a caller-provided workspace of
+ * dpvo_motion_mag_workspace_bytes for the per-workgroup partials, summed in a
+ * fixed order by a second launch). */
+size_t dpvo_motion_mag_workspace_bytes(int64_t num_edges);
+int dpvo_motion_mag_ws(const float* poses, const float* patches, int P, const float* intrinsics, const int64_t* ii,
+                       const int64_t* jj, const int64_t* kk, int64_t num_edges, int64_t i, int64_t j, float beta,
+                       float* out, void* workspace, size_t workspace_bytes, void* stream);
 
 /* Keyframe distance matrix of the global BA's distance-based edges
  * (replaces the O(n^2) loop of dpvo.py:383-429 -- two flow_mag calls and one

@@ -59,6 +59,9 @@ _SIGNATURES = {
     "dpvo_transform": (_ip, [_vp, _vp, _ip, _vp, _vp, _vp, _vp, _i64, _ip, _vp, _vp, _vp]),
     "dpvo_point_cloud": (_ip, [_vp, _vp, _ip, _vp, _vp, _i64, _ip, _vp, _vp]),
     "dpvo_motion_mag": (_ip, [_vp, _vp, _ip, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _fp, _vp, _vp]),
+    "dpvo_motion_mag_workspace_bytes": (ctypes.c_size_t, [_i64]),
+    "dpvo_motion_mag_ws": (_ip, [_vp, _vp, _ip, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _fp, _vp, _vp, ctypes.c_size_t,
+                                 _vp]),
     "dpvo_keyframe_flow_lds_bytes": (ctypes.c_size_t, [_ip, _i64]),
     "dpvo_keyframe_flow": (_ip, [_vp, _vp, _ip, _vp, _i64, _i64, _fp, _vp, _vp]),
     "dpvo_softagg_workspace_bytes": (_sz, [_i64, _i64]),

@@ -74,9 +74,11 @@ def motion_mag_pair(poses, patches, intrinsics, ii, jj, kk, i, j, beta=0.5):
     patches, intrinsics = patches.contiguous(), intrinsics.contiguous()
     ii, jj, kk = H.idx64(ii), H.idx64(jj), H.idx64(kk)
     out = torch.empty(2, dtype=torch.float32, device=data.device)
-    H.check(H.lib().dpvo_motion_mag(H.ptr(data), H.ptr(patches), patches.shape[-1], H.ptr(intrinsics), H.ptr(ii),
-                                    H.ptr(jj), H.ptr(kk), ii.numel(), int(i), int(j), float(beta), H.ptr(out),
-                                    H.stream_of(data)))
+    nb = H.lib().dpvo_motion_mag_workspace_bytes(ii.numel())
+    ws = torch.empty(nb, dtype=torch.uint8, device=data.device)
+    H.check(H.lib().dpvo_motion_mag_ws(H.ptr(data), H.ptr(patches), patches.shape[-1], H.ptr(intrinsics), H.ptr(ii),
+                                       H.ptr(jj), H.ptr(kk), ii.numel(), int(i), int(j), float(beta), H.ptr(out),
+                                       H.ptr(ws), nb, H.stream_of(data)))
     return out
 
 
