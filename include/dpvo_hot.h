@@ -356,6 +356,13 @@ typedef struct dpvo_rowgemm_args {
 } dpvo_rowgemm_args;
 int dpvo_rowgemm(const dpvo_rowgemm_args* args, void* stream);
 
+/* Two plain rowgemms (flags 0) on the same A in one launch: SoftAgg's f and g
+ * Linears (blocks.py:33-37 -- agg.f(x), agg.g(x)).  a and b must agree on A,
+ * lda, a_idx, a_rows, K, M and M_dev; each has its own W, bias and outputs.
+ * Every 128-row tile of A is multiplied by a's W then b's W back to back, so
+ * the second pass reads A from L2 rather than HBM. */
+int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_args* b, void* stream);
+
 /* Two chained rowgemms, Y = epi2(act1(A W1^T + b1) W2^T + b2), with the 384-wide
  * intermediate kept on chip (the update operator's Linear -> ReLU -> Linear
  * pairs).  g1: A, lda, a_idx, a_rows, W (K1 % 32 == 0), bias, zero_row, M,
@@ -364,9 +371,20 @@ int dpvo_rowgemm(const dpvo_rowgemm_args* args, void* stream);
  * of dpvo_rowgemm (its A, M and M_dev are taken from g1). */
 int dpvo_rowchain(const dpvo_rowgemm_args* first, const dpvo_rowgemm_args* second, void* stream);
 
+/* The GRU's GatedResidual (blocks.py:27-30) in one launch:
+ *   gate = sigmoid(fp16(A Wg^T + bg)),  Y = epi2(act1(A W1^T + b1) W2^T + b2)
+ * with second->flags including DPVO_RG_GATE (GATE|LN or GATE|HEADS) and
+ * second->gate16 == NULL: the gate never leaves the chip.  gate: W ([384][K1],
+ * like first's W) and bias only.  Same results as dpvo_rowgemm(A, Wg, bg,
+ * DPVO_RG_SIGMOID) -> gate16 followed by dpvo_rowchain. */
+int dpvo_rowchain_gated(const dpvo_rowgemm_args* gate, const dpvo_rowgemm_args* first,
+                        const dpvo_rowgemm_args* second, void* stream);
+
 /* Row add + LayerNorm over 384-wide rows (one pass):
  *   v = a[m] (+ b16[b_idx[m]])  [-> LayerNorm]  -> out32 [M][384] / out16 [M][384]
- * a is fp16 (a_f16=1) or fp32 with row stride lda; b_idx[m] < 0 adds nothing.
+ * a is fp16 (a_f16=1) or fp32 with row stride lda (a multiple of 4); b_idx[m] < 0
+ * adds nothing.  Vector access: a, out32, ln_g / ln_b 16-byte aligned (a 8-byte
+ * when fp16), b16 and out16 8-byte aligned.
  * Used for `net + h(y)[:, jx]` after SoftAgg and the GRU's first LayerNorm. */
 typedef struct dpvo_rowadd_args {
     const void* a; int a_f16; int64_t lda; int64_t M;

@@ -121,6 +121,23 @@ def test_gated_residual_and_heads(with_ln):
         close16(heads, want)
 
 
+@pytest.mark.parametrize("M", [1, 127, 3000, 40000])
+def test_rowgemm_pair_equals_two_launches(M):
+    """SoftAgg's f / g in one launch sharing A: bit-identical to two rowgemms."""
+    import update_ops as U
+    A = torch.randn(M, D, device="cuda").half()
+    (wa, ba), (wb, bb) = lin(D, 5), lin(D, 6)
+    Wa, ba16 = U.pack_linear(wa, ba)
+    Wb, bb16 = U.pack_linear(wb, bb)
+    f, g = U.rowgemm_pair(A, Wa, ba16, Wb, bb16)
+    assert torch.equal(f, U.rowgemm(A, Wa, ba16)[1])
+    assert torch.equal(g, U.rowgemm(A, Wb, bb16)[1])
+    # device row count (the SoftAgg h GEMM's G): rows past it untouched
+    Md = torch.tensor([M // 2], dtype=torch.int64, device="cuda")
+    f2, g2 = U.rowgemm_pair(A, Wa, ba16, Wb, bb16, M_dev=Md)
+    assert torch.equal(f2[:M // 2], f[:M // 2]) and torch.equal(g2[:M // 2], g[:M // 2])
+
+
 def test_rowadd_ln():
     import update_ops as U
     M = 3000
@@ -135,6 +152,15 @@ def test_rowadd_ln():
     want = torch.nn.functional.layer_norm(a + hk[jx].float(), (D,), g, be, 1e-3)
     torch.testing.assert_close(o32, want, rtol=1e-4, atol=1e-4)
     close16(o16, want.half())
+    # fp16 input with a padded row stride, out-of-range gather rows add nothing
+    a16 = torch.randn(M, D + 4, device="cuda").half()[:, :D]
+    jx[::7] = -1
+    jx[1::7] = 500
+    o32, o16 = U.rowadd_ln(a16, hk, jx, ln=(g, be, 1e-3))
+    add = torch.where((jx >= 0) & (jx < 500), 1.0, 0.0)[:, None] * hk[jx.clamp(0, 499)].float()
+    want = torch.nn.functional.layer_norm(a16.float() + add, (D,), g, be, 1e-3)
+    torch.testing.assert_close(o32, want, rtol=1e-4, atol=1e-4)
+    assert U.rowadd_ln(a[:0], hk, jx[:0])[0].shape == (0, D)
 
 
 def test_errors():
@@ -234,3 +260,33 @@ def test_rowchain_is_two_rowgemms(case):
         assert (r is None) == (g is None)
         if r is not None:
             assert torch.equal(r, g)
+
+
+@pytest.mark.parametrize("M", [1, 1000, 50000])
+@pytest.mark.parametrize("last", [False, True])
+def test_rowchain_gated_is_gate_gemm_plus_chain(M, last):
+    """dpvo_rowchain_gated (gate Linear + sigmoid on chip, y stored as
+    fp16(gate * y)) is bit-identical to rowgemm(SIGMOID) -> gate16 followed by
+    the GATE chain: the GRU's GatedResidual (blocks.py:27-30)."""
+    import update_ops as U
+    torch.manual_seed(4)
+    dev = "cuda"
+    A = (torch.randn(M, 384, device=dev) * 0.5).half()
+    lin_ = lambda s: U.pack_linear(torch.randn(384, 384, device=dev) / s, torch.randn(384, device=dev) * 0.1)
+    (Wg, bg), (W1, b1), (W2, b2) = lin_(20.0), lin_(20.0), lin_(20.0)
+    res32 = torch.randn(M, 384, device=dev)
+    if last:
+        heads = (torch.randn(4, 384, device=dev).half() * 0.05, torch.randn(4, device=dev).half())
+        kw = dict(flags=U.GATE | U.HEADS, res32=res32, heads=heads, want32=True, want16=False)
+    else:
+        ln = (torch.rand(384, device=dev) + 0.5, torch.randn(384, device=dev) * 0.1, 1e-3)
+        kw = dict(flags=U.GATE | U.LN, res32=res32, ln=ln, want32=True)
+    _, g16, _ = U.rowgemm(A, Wg, bg, flags=U.SIGMOID)
+    ref = U.rowchain(A, W1, b1, W2, b2, flags1=U.RELU, gate16=g16, **kw)
+    got = U.rowchain(A, W1, b1, W2, b2, flags1=U.RELU, gate=(Wg, bg), **kw)
+    for r, g in zip(ref, got):
+        assert (r is None) == (g is None)
+        if r is not None:
+            assert torch.equal(r, g)
+    with pytest.raises(RuntimeError):
+        U.rowchain(A, W1, b1, W2, b2, flags1=U.RELU, gate16=g16, gate=(Wg, bg), **kw)

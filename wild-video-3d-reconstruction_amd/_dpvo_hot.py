@@ -72,7 +72,9 @@ _SIGNATURES = {
     "dpvo_softagg_csr": (_ip, [_ip, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _ip, _fp, _vp, _vp]),
     "dpvo_neighbors_csr": (_ip, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),
     "dpvo_rowgemm": (_ip, [_vp, _vp]),
+    "dpvo_rowgemm_pair": (_ip, [_vp, _vp, _vp]),
     "dpvo_rowchain": (_ip, [_vp, _vp, _vp]),
+    "dpvo_rowchain_gated": (_ip, [_vp, _vp, _vp, _vp]),
     "dpvo_rowadd_ln": (_ip, [_vp, _vp]),
 }
 EXPORTED = tuple(_SIGNATURES)

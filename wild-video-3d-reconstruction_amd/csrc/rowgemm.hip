@@ -587,8 +587,8 @@ struct YMapSlot {   // 64 rows x 768 B in one W slot, 32-B granules XOR (row/4)&
     __device__ int off(int r, int byte) const { return base + r * 768 + (byte ^ (((r >> 2) & 3) << 5)); }
 };
 
-template <int FLAGS>
-__global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_args p)
+template <int FLAGS, bool DUAL = false>
+__global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_args p, dpvo_rowgemm_args p2)
 {
     __shared__ __attribute__((aligned(16))) char smem[R3_LDS];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -598,8 +598,11 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_ar
     const int64_t Mrows = p.M_dev ? min(*p.M_dev, p.M) : p.M;
     const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
     if ((int64_t)blockIdx.x >= ntiles) return;
-    const int64_t my_tiles = (ntiles - 1 - blockIdx.x) / gridDim.x + 1;
+    // DUAL: a second GEMM on the same A (p2's W, bias, outputs): every tile runs
+    // twice in a row, the second pass's A stream hitting L2
+    const int64_t my_tiles = ((ntiles - 1 - blockIdx.x) / gridDim.x + 1) << (DUAL ? 1 : 0);
     const int64_t total = my_tiles * ksteps;
+    const int64_t wdelta = DUAL ? (const half_t*)p2.W - (const half_t*)p.W : 0;
 
     const half_t* __restrict__ Wt = (const half_t*)p.W;
     const half_t* __restrict__ zero = (const half_t*)p.zero_row;
@@ -622,7 +625,8 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_ar
         return row + 8 * (pch ^ ((r >> 1) & 7));
     };
     // flat step f -> (tile, k-step) of this block
-    auto tile_of = [&](int64_t f) { return (int64_t)blockIdx.x + (f / ksteps) * gridDim.x; };
+    auto tile_of = [&](int64_t f) { return (int64_t)blockIdx.x + ((f / ksteps) >> (DUAL ? 1 : 0)) * gridDim.x; };
+    auto second = [&](int64_t f) { return DUAL && ((f / ksteps) & 1); };
     const half_t* asrc[2];
     int64_t asrc_tile = -1;
     auto issue_a = [&](int64_t f) {
@@ -639,7 +643,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_ar
     };
     auto issue_w = [&](int64_t f) {
         char* sW = smem + (int)(f & 1) * R3_W_SLOT;
-        const int k0 = (int)(f % ksteps) * RG_BK;
+        const int64_t k0 = (f % ksteps) * RG_BK + (second(f) ? wdelta : 0);
 #pragma unroll
         for (int j = 0; j < 6; j++) glds16(wsrc[j] + k0, sW + (wave * 6 + j) * 1024);
     };
@@ -707,11 +711,13 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_ar
         // ---- epilogue of tile t.  y16 = act(fp16(acc + b)): four consecutive
         // columns of one row per (m-tile, n-tile) and lane.
         const int64_t cur_tile = tile_of(i);
+        const bool sec = second(i);
+        const dpvo_rowgemm_args& pe = sec ? p2 : p;
         typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
         h4_t y16[4][6];
 #pragma unroll
         for (int nt = 0; nt < 6; nt++) {
-            const h4_t bias = *(const h4_t*)((const half_t*)p.bias + wn * 96 + nt * 16 + 4 * fq);
+            const h4_t bias = *(const h4_t*)((const half_t*)pe.bias + wn * 96 + nt * 16 + 4 * fq);
 #pragma unroll
             for (int mt = 0; mt < 4; mt++) {
 #pragma unroll
@@ -747,7 +753,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_ar
             const int64_t row0 = cur_tile * RG_BM + (lr >> 5) * 64 + h * 32 + (lr & 31);
 #pragma unroll
             for (int q0 = 0; q0 < 8; q0 += RB)
-                epilogue_rows<FLAGS, RB>(p, Mrows, smem, ym, lr + q0, row0 + q0, lane, kc);
+                epilogue_rows<FLAGS, RB>(pe, Mrows, smem, ym, lr + q0, row0 + q0, lane, kc);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
@@ -776,8 +782,16 @@ struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflic
     __device__ int off(int r, int byte) const { return r * 768 + (((byte >> 4) ^ (r & 15)) << 4) + (byte & 15); }
 };
 
-template <int F2>
-__global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p)
+// GATED (the GRU's GatedResidual, blocks.py:27-30): after GEMM2 has put y in
+// the y tile, a third GEMM on the same A (re-read from L2) gives
+// gate = sigmoid(A Wg^T + bg) in the accumulators, and every lane rewrites its
+// own y tile elements as fp16(gate * y) -- the epilogue then adds them to the
+// residual like RES, which is bit-for-bit the GATE epilogue's
+// x + fp16(gate * y) without the 73 MB gate16 round trip (nor a gate held in
+// registers across the GEMMs).
+template <int F2, bool GATED = false>
+__global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
+                                                                 dpvo_rowgemm_args pg)
 {
     __shared__ __attribute__((aligned(16))) char smem[RC_LDS];
     typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
@@ -827,11 +841,14 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         const int n = (3 * wave + j) * 16 + srow;
         w2src[j] = W2 + (int64_t)n * RG_BN + 8 * (pch ^ ((n >> 2) & 3));
     }
-    auto issue1 = [&](int ks, int buf) {
+    // gate pass: the same stage layout, W pieces from Wg ([384][K1] like W1)
+    const int64_t gdelta = GATED ? (const half_t*)pg.W - W1 : 0;
+    auto issue1 = [&](int ks, int buf, bool gate = false) {
         char* st = smem + RC_Y + buf * RC_STAGE;
         const int k0 = ks * RC_BK;
 #pragma unroll
-        for (int j = 0; j < 4; j++) glds16(g1src[j] + k0, st + (4 * wave + j) * 1024);
+        for (int j = 0; j < 4; j++)
+            glds16(g1src[j] + k0 + (GATED && gate && 4 * wave + j >= 8 ? gdelta : 0), st + (4 * wave + j) * 1024);
     };
     auto issue2 = [&](int ks, int buf) {
         char* st = smem + RC_Y + buf * RC_STAGE + RC_A_STAGE;
@@ -893,19 +910,10 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             }
         }
     };
-    EpiConsts kc;
-    load_consts<F2>(p, lane, kc);
-
-    int64_t tile = blockIdx.x;
-    set_tile(tile);
-    issue1(0, 0);
-    for (; tile < ntiles; tile += gridDim.x) {
-        const bool more = tile + gridDim.x < ntiles;
-        // ---- GEMM1: A (global, gathered) x W1
-        zero_acc();
+    auto gemm1 = [&](bool gate) {
         for (int ks = 0; ks < ks1; ks++) {
             if (ks + 1 < ks1) {
-                issue1(ks + 1, (ks + 1) & 1);
+                issue1(ks + 1, (ks + 1) & 1, gate);
                 asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
             } else {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -921,6 +929,15 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             mfma_step(a, b);
             __builtin_amdgcn_s_barrier();
         }
+    };
+    int64_t tile = blockIdx.x;
+    set_tile(tile);
+    issue1(0, 0);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const bool more = tile + gridDim.x < ntiles;
+        // ---- GEMM1: A (global, gathered) x W1
+        zero_acc();
+        gemm1(false);
         // ---- intermediate -> y tile; W2's first stage into the released stage 0
         acc_to_y((const half_t*)p1.bias, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
         issue2(0, 0);
@@ -947,12 +964,38 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             __builtin_amdgcn_s_barrier();
         }
         acc_to_y((const half_t*)p.bias, F2 & RG_RELU, F2 & RG_SIGMOID);
+        if (GATED) {
+            // ---- gate: A x Wg -> sigmoid (rowgemm's SIGMOID rounding) -> y = fp16(gate * y)
+            issue1(0, 0, true);
+            zero_acc();
+            gemm1(true);
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) {
+                const int col = wn * 96 + nt * 16 + 4 * fq;
+                const h4_t bias = *(const h4_t*)((const half_t*)pg.bias + col);
+#pragma unroll
+                for (int mt = 0; mt < 4; mt++) {
+                    h4_t* yp = (h4_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, col * 2));
+                    h4_t y = *yp;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const half_t g = (half_t)fast_sigmoid((float)(half_t)(acc[mt][nt][r] + (float)bias[r]));
+                        y[r] = (half_t)((float)g * (float)y[r]);
+                    }
+                    *yp = y;
+                }
+            }
+        }
         // ---- the next tile's first GEMM1 stage loads under this epilogue
         if (more) {
             set_tile(tile + gridDim.x);
             issue1(0, 0);
         }
         sync_lds();
+        // LayerNorm / head constants loaded per tile, not held across the GEMMs
+        // (the gated chain's gate already holds 48 VGPRs there)
+        EpiConsts kc;
+        load_consts<F2>(p, lane, kc);
         constexpr int RB = (F2 & (RG_RES | RG_GATE | RG_LN)) ? 4 : 8;
 #pragma unroll 1
         for (int q0 = 0; q0 < 16; q0 += RB)   // one batch live at a time (register budget)
@@ -1241,13 +1284,32 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm4_kernel(dpvo_rowgemm_ar
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // trailing W prefetches
 }
 
-// v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16   (one wave per row)
+// v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16
+// Half a wave per row: lane l of the half covers columns 4l + 128j (j < 3), so
+// every access is a 16-byte (fp32) or 8-byte (fp16) vector and one wave keeps
+// two rows' loads in flight.  HBM-bound: 4 B x 384 in, 6 B x 384 out per row.
+typedef float rl_f4 __attribute__((ext_vector_type(4)));
+typedef half_t rl_h4 __attribute__((ext_vector_type(4)));
+
 __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
 {
-    const int lane = threadIdx.x & 63;
-    for (int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; row < p.M;
-         row += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-        float v[6];
+    const int sub = threadIdx.x & 31;
+    float g[12], bt[12];
+    if (p.ln_g) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const rl_f4 gg = *(const rl_f4*)((const float*)p.ln_g + 128 * j + 4 * sub);
+            const rl_f4 bb = *(const rl_f4*)((const float*)p.ln_b + 128 * j + 4 * sub);
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                g[4 * j + t] = gg[t];
+                bt[4 * j + t] = bb[t];
+            }
+        }
+    }
+    for (int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 5; row < p.M;
+         row += ((int64_t)gridDim.x * blockDim.x) >> 5) {
+        float v[12];
         const half_t* b = nullptr;
         if (p.b16) {
             const int64_t s = p.b_idx ? p.b_idx[row] : row;
@@ -1255,52 +1317,51 @@ __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
         }
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-            const int c = 128 * j + 2 * lane;
-            float2_t a;
+            const int c = 128 * j + 4 * sub;
             if (p.a_f16) {
-                half2_t h = *(const half2_t*)((const half_t*)p.a + row * p.lda + c);
-                a = float2_t{(float)h.x, (float)h.y};
+                const rl_h4 h = *(const rl_h4*)((const half_t*)p.a + row * p.lda + c);
+#pragma unroll
+                for (int t = 0; t < 4; t++) v[4 * j + t] = (float)h[t];
             } else {
-                a = *(const float2_t*)((const float*)p.a + row * p.lda + c);
+                const rl_f4 a = *(const rl_f4*)((const float*)p.a + row * p.lda + c);
+#pragma unroll
+                for (int t = 0; t < 4; t++) v[4 * j + t] = a[t];
             }
-            if (b) {
-                half2_t h = *(const half2_t*)(b + c);
-                a.x += (float)h.x;
-                a.y += (float)h.y;
+        }
+        if (b) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const rl_h4 h = *(const rl_h4*)(b + 128 * j + 4 * sub);
+#pragma unroll
+                for (int t = 0; t < 4; t++) v[4 * j + t] += (float)h[t];
             }
-            v[2 * j] = a.x;
-            v[2 * j + 1] = a.y;
         }
         if (p.ln_g) {
-            // row reductions with DPP rotations and gfx950 lane swaps: VALU only,
-            // no LDS round trip (the butterfly's order, so every lane agrees)
-            auto allsum = [](float x) {
+            // half-wave sums with DPP rotations and a gfx950 lane swap: VALU
+            // only (a + b == b + a, so both lanes of a swapped pair agree)
+            auto halfsum = [](float x) {
                 x = rowsum16(x);
                 auto h = __builtin_amdgcn_permlane16_swap(__float_as_int(x), __float_as_int(x), false, false);
-                x = __int_as_float(h[0]) + __int_as_float(h[1]);
-                auto w = __builtin_amdgcn_permlane32_swap(__float_as_int(x), __float_as_int(x), false, false);
-                return __int_as_float(w[0]) + __int_as_float(w[1]);
+                return __int_as_float(h[0]) + __int_as_float(h[1]);
             };
             float s = 0.f;
 #pragma unroll
-            for (int j = 0; j < 6; j++) s += v[j];
-            const float mean = allsum(s) * (1.f / RG_BN);
+            for (int j = 0; j < 12; j++) s += v[j];
+            const float mean = halfsum(s) * (1.f / RG_BN);
             float q = 0.f;
 #pragma unroll
-            for (int j = 0; j < 6; j++) q += (v[j] - mean) * (v[j] - mean);
-            const float rstd = rsqrtf(allsum(q) * (1.f / RG_BN) + p.ln_eps);
+            for (int j = 0; j < 12; j++) q += (v[j] - mean) * (v[j] - mean);
+            const float rstd = rsqrtf(halfsum(q) * (1.f / RG_BN) + p.ln_eps);
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const int c = 128 * j + 2 * lane;
-                v[2 * j] = (v[2 * j] - mean) * rstd * ((const float*)p.ln_g)[c] + ((const float*)p.ln_b)[c];
-                v[2 * j + 1] = (v[2 * j + 1] - mean) * rstd * ((const float*)p.ln_g)[c + 1] + ((const float*)p.ln_b)[c + 1];
-            }
+            for (int j = 0; j < 12; j++) v[j] = (v[j] - mean) * rstd * g[j] + bt[j];
         }
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-            const int c = 128 * j + 2 * lane;
-            if (p.out32) *(float2_t*)((float*)p.out32 + row * RG_BN + c) = float2_t{v[2 * j], v[2 * j + 1]};
-            if (p.out16) *(half2_t*)((half_t*)p.out16 + row * RG_BN + c) = half2_t{(half_t)v[2 * j], (half_t)v[2 * j + 1]};
+            const int c = 128 * j + 4 * sub;
+            if (p.out32) *(rl_f4*)((float*)p.out32 + row * RG_BN + c) = rl_f4{v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]};
+            if (p.out16)
+                *(rl_h4*)((half_t*)p.out16 + row * RG_BN + c) =
+                    rl_h4{(half_t)v[4 * j], (half_t)v[4 * j + 1], (half_t)v[4 * j + 2], (half_t)v[4 * j + 3]};
         }
     }
 }
@@ -1317,7 +1378,7 @@ using namespace dpvo;
         hipLaunchKernelGGL(rowgemm_kernel<(F)>, dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a); \
         break;
 
-extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
+static int validate_rowgemm(const dpvo_rowgemm_args* a)
 {
     DPVO_CHECK_ARG(a != nullptr, "null args");
     DPVO_CHECK_ARG(a->N == RG_BN, "rowgemm: output width must be 384");
@@ -1337,6 +1398,40 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
     DPVO_CHECK_ARG(!a->out32 || (a->ldo32 % 4 == 0 && ((uintptr_t)a->out32 & 15) == 0),
                    "rowgemm: out32 needs 16-byte aligned rows (ldo32 % 4 == 0)");
     DPVO_CHECK_ARG(((uintptr_t)a->bias & 7) == 0, "rowgemm: bias must be 8-byte aligned");
+    return 0;
+}
+
+static int ensure_num_cus()
+{
+    if (g_num_cus == 0) {
+        int dev = 0;
+        DPVO_CHECK_HIP(hipGetDevice(&dev));
+        DPVO_CHECK_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+        if (g_num_cus <= 0) g_num_cus = 256;
+    }
+    return 0;
+}
+
+extern "C" int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_args* b, void* stream)
+{
+    if (validate_rowgemm(a) || validate_rowgemm(b)) return -1;
+    DPVO_CHECK_ARG(a->flags == 0 && b->flags == 0, "rowgemm_pair: plain GEMMs only (flags 0)");
+    DPVO_CHECK_ARG(a->A == b->A && a->lda == b->lda && a->a_idx == b->a_idx && a->a_rows == b->a_rows &&
+                       a->K == b->K && a->M == b->M && a->M_dev == b->M_dev,
+                   "rowgemm_pair: both GEMMs must share A, K and M");
+    if (a->M <= 0) return 0;
+    if (ensure_num_cus()) return -1;
+    const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
+    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+    hipLaunchKernelGGL((rowgemm3_kernel<0, true>), dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, *b);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
+{
+    if (validate_rowgemm(a)) return -1;
+    const int f = a->flags;
     if (a->M <= 0) return 0;
     if (g_num_cus == 0) {
         int dev = 0;
@@ -1430,7 +1525,7 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
         switch (f) {
 #define R3_CASE(F)                                                                                            \
     case (F):                                                                                                 \
-        hipLaunchKernelGGL(rowgemm3_kernel<(F)>, dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a); \
+        hipLaunchKernelGGL(rowgemm3_kernel<(F)>, dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, *a); \
         break;
             R3_CASE(0)
             R3_CASE(DPVO_RG_RELU)
@@ -1467,7 +1562,8 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
     return 0;
 }
 
-extern "C" int dpvo_rowchain(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args* g2, void* stream)
+static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args* g2, const dpvo_rowgemm_args* gate,
+                           void* stream)
 {
     DPVO_CHECK_ARG(g1 != nullptr && g2 != nullptr, "null args");
     DPVO_CHECK_ARG(g1->N == RG_BN && g2->N == RG_BN, "rowchain: output widths must be 384");
@@ -1485,7 +1581,14 @@ extern "C" int dpvo_rowchain(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_arg
                    "rowchain: the first GEMM takes only an activation");
     const int f = g2->flags;
     DPVO_CHECK_ARG(!((f & DPVO_RG_RES) || (f & DPVO_RG_GATE)) || g2->res32, "rowchain: residual input missing");
-    DPVO_CHECK_ARG(!(f & DPVO_RG_GATE) || g2->gate16, "rowchain: gate input missing");
+    DPVO_CHECK_ARG(!(f & DPVO_RG_GATE) || g2->gate16 || gate, "rowchain: gate input missing");
+    if (gate) {
+        DPVO_CHECK_ARG(f & DPVO_RG_GATE, "rowchain_gated: the second GEMM's flags must include DPVO_RG_GATE");
+        DPVO_CHECK_ARG(!g2->gate16, "rowchain_gated: gate16 must be NULL (the gate is computed on chip)");
+        DPVO_CHECK_ARG(gate->W && gate->bias && ((uintptr_t)gate->W & 15) == 0 && ((uintptr_t)gate->bias & 7) == 0,
+                       "rowchain_gated: gate W (16-byte aligned) and bias (8-byte aligned) are required");
+        DPVO_CHECK_ARG(gate->K == g1->K && gate->N == RG_BN, "rowchain_gated: gate W must be [384][K1] like W1");
+    }
     DPVO_CHECK_ARG(!(f & DPVO_RG_LN) || (g2->ln_g && g2->ln_b), "rowchain: LayerNorm weights missing");
     DPVO_CHECK_ARG(!(f & DPVO_RG_HEADS) || (g2->head_w && g2->head_b && g2->head_out), "rowchain: head weights missing");
     if (g1->M <= 0) return 0;
@@ -1504,7 +1607,7 @@ extern "C" int dpvo_rowchain(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_arg
         const char* v = getenv("DPVO_ROWGEMM");
         return v && atoi(v) == 4;
     }();
-    if (v4 && g1->K % 64 == 0) {
+    if (v4 && !gate && g1->K % 64 == 0) {
         switch (f) {
 #define RC4_CASE(F)                                                                                              \
     case (F):                                                                                                    \
@@ -1523,10 +1626,30 @@ extern "C" int dpvo_rowchain(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_arg
         DPVO_CHECK_LAUNCH();
         return 0;
     }
+    if (gate) {
+        // the gated y goes through the RES epilogue (res16 none): x + fp16(gate * y)
+        a2.gate16 = nullptr;
+        a2.res16 = nullptr;
+        switch (f) {
+#define RCG_CASE(F)                                                                                                   \
+    case (F):                                                                                                         \
+        hipLaunchKernelGGL((rowchain_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES, true>), dim3(grid), dim3(RG_THREADS), \
+                           0, as_stream(stream), *g1, a2, *gate);                                                     \
+        break;
+            RCG_CASE(DPVO_RG_GATE | DPVO_RG_LN)
+            RCG_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
+#undef RCG_CASE
+        default:
+            set_error("dpvo_rowchain_gated: unsupported epilogue flag combination " + std::to_string(f));
+            return -1;
+        }
+        DPVO_CHECK_LAUNCH();
+        return 0;
+    }
     switch (f) {
-#define RCH_CASE(F)                                                                                              \
-    case (F):                                                                                                    \
-        hipLaunchKernelGGL(rowchain_kernel<(F)>, dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *g1, a2); \
+#define RCH_CASE(F)                                                                                                   \
+    case (F):                                                                                                         \
+        hipLaunchKernelGGL(rowchain_kernel<(F)>, dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *g1, a2, a2); \
         break;
         RCH_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
         RCH_CASE(DPVO_RG_RES)
@@ -1541,14 +1664,34 @@ extern "C" int dpvo_rowchain(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_arg
     return 0;
 }
 
+extern "C" int dpvo_rowchain(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args* g2, void* stream)
+{
+    return rowchain_launch(g1, g2, nullptr, stream);
+}
+
+extern "C" int dpvo_rowchain_gated(const dpvo_rowgemm_args* gate, const dpvo_rowgemm_args* g1,
+                                   const dpvo_rowgemm_args* g2, void* stream)
+{
+    DPVO_CHECK_ARG(gate != nullptr, "rowchain_gated: gate args missing");
+    return rowchain_launch(g1, g2, gate, stream);
+}
+
 extern "C" int dpvo_rowadd_ln(const dpvo_rowadd_args* a, void* stream)
 {
-    DPVO_CHECK_ARG(a != nullptr && a->a != nullptr, "rowadd_ln: input missing");
-    DPVO_CHECK_ARG(a->lda >= RG_BN && a->lda % 2 == 0, "rowadd_ln: lda must be even and >= 384");
+    DPVO_CHECK_ARG(a != nullptr, "rowadd_ln: args missing");
+    if (a->M <= 0) return 0;   // (empty tensors may carry null data pointers)
+    DPVO_CHECK_ARG(a->a != nullptr, "rowadd_ln: input missing");
+    DPVO_CHECK_ARG(a->lda >= RG_BN && a->lda % 4 == 0, "rowadd_ln: lda must be a multiple of 4 and >= 384");
+    DPVO_CHECK_ARG((uintptr_t)a->a % (a->a_f16 ? 8 : 16) == 0, "rowadd_ln: input rows must be vector aligned");
+    DPVO_CHECK_ARG(!a->b16 || (uintptr_t)a->b16 % 8 == 0, "rowadd_ln: b16 must be 8-byte aligned");
+    DPVO_CHECK_ARG(!a->ln_g || ((uintptr_t)a->ln_g % 16 == 0 && (uintptr_t)a->ln_b % 16 == 0),
+                   "rowadd_ln: LayerNorm parameters must be 16-byte aligned");
+    DPVO_CHECK_ARG((!a->out32 || (uintptr_t)a->out32 % 16 == 0) && (!a->out16 || (uintptr_t)a->out16 % 8 == 0),
+                   "rowadd_ln: outputs must be vector aligned");
     DPVO_CHECK_ARG(a->out32 || a->out16, "rowadd_ln: no output");
     DPVO_CHECK_ARG(!a->ln_g == !a->ln_b, "rowadd_ln: LayerNorm needs both weight and bias");
     if (a->M <= 0) return 0;
-    const unsigned grid = grid_for(a->M * 64, 256, 16384);
+    const unsigned grid = grid_for(a->M * 32, 256, 16384);
     hipLaunchKernelGGL(rowadd_ln_kernel, dim3(grid), dim3(256), 0, as_stream(stream), *a);
     DPVO_CHECK_LAUNCH();
     return 0;

@@ -107,21 +107,20 @@ class Update(nn.Module):
         for (pf, pg_, ph), key, ln in ((pk["agg_kk"], None, None), (pk["agg_ij"], ii * 12345 + jj, ln0)):
             # unique(key) + CSR on the device (no host sync); G stays on the device
             gid, offs, perm, G = kk_groups if key is None else U.group_by(key, key_bits=ij_bits)
-            _, f16, _ = U.rowgemm(n16, *pf)
-            _, g16, _ = U.rowgemm(n16, *pg_)
+            f16, g16 = U.rowgemm_pair(n16, *pf, *pg_)
             y = U.softagg_csr(f16, g16, offs, perm, G, E)
             _, hy, _ = U.rowgemm(y, *ph, M_dev=G)
             n32, n16 = U.rowadd_ln(n32, hy, gid, ln=ln)
         # gru = LN0 (fused above), GatedResidual, LN1, GatedResidual; then the d / w heads
         for gr, last in ((gr1, False), (gr2, True)):
             pgate, pr1, pr2 = gr
-            _, g16, _ = U.rowgemm(n16, *pgate, flags=U.SIGMOID)
+            # the gate Linear + sigmoid runs in the same launch (gate kept on chip)
             if last:
                 n32, _, heads = U.rowchain(n16, *pr1, *pr2, flags1=U.RELU, flags=U.GATE | U.HEADS, res32=n32,
-                                           gate16=g16, heads=pk["heads"], want32=True, want16=False)
+                                           gate=pgate, heads=pk["heads"], want32=True, want16=False)
             else:
                 n32, n16, _ = U.rowchain(n16, *pr1, *pr2, flags1=U.RELU, flags=U.GATE | U.LN, res32=n32,
-                                         gate16=g16, ln=ln1, want32=True)
+                                         gate=pgate, ln=ln1, want32=True)
         return n32[None], (heads[None, :, :2], heads[None, :, 2:], None)
 
     def forward(self, net, inp, corr, flow, ii, jj, kk, inp_idx=None, index_bounds=None, kk_groups=None):

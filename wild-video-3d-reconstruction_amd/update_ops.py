@@ -77,9 +77,11 @@ def softagg_csr(f, s, offs, perm, groups, max_groups, eps=1e-12):
 
 
 def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=None, res16=None, res16_idx=None,
-             gate16=None, ln=None, heads=None, want32=False, want16=True, M_dev=None):
+             gate16=None, ln=None, heads=None, want32=False, want16=True, M_dev=None, gate=None):
     """rowgemm(rowgemm(A, W1, b1, flags1, a_idx).y16, W2, b2, flags, ...) in one
     launch, the 384-wide intermediate kept on chip (dpvo_rowchain).
+    gate = (Wg, bg) with GATE in flags: gate16 = rowgemm(A, Wg, bg, SIGMOID)
+    computed in the same launch (dpvo_rowchain_gated) instead of passed in.
     Returns (out32, out16, head_out) of the second GEMM."""
     H.on_gpu(A, W1, b1, W2, b2)
     if flags1 is None:
@@ -129,7 +131,18 @@ def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=
     for t, nm in ((res16, "res16"), (gate16, "gate16")):
         if t is not None and (t.dtype != torch.float16 or not t.is_contiguous() or t.shape[-1] != WIDTH):
             raise RuntimeError(f"rowchain: {nm} must be contiguous fp16 [*, 384]")
-    H.check(H.lib().dpvo_rowchain(_ct.byref(g1), _ct.byref(g2), H.stream_of(A)))
+    if gate is not None:
+        Wg, bg = gate
+        H.on_gpu(Wg, bg)
+        if Wg.dtype != torch.float16 or bg.dtype != torch.float16 or Wg.shape != W1.shape or not Wg.is_contiguous():
+            raise RuntimeError("rowchain: gate W must be fp16 contiguous of W1's shape, bias fp16")
+        if gate16 is not None:
+            raise RuntimeError("rowchain: pass either gate16 or gate, not both")
+        gg = RowGemmArgs()
+        gg.W, gg.K, gg.N, gg.bias = _p(Wg), Kp, WIDTH, _p(bg)
+        H.check(H.lib().dpvo_rowchain_gated(_ct.byref(gg), _ct.byref(g1), _ct.byref(g2), H.stream_of(A)))
+    else:
+        H.check(H.lib().dpvo_rowchain(_ct.byref(g1), _ct.byref(g2), H.stream_of(A)))
     return out32, out16, head_out
 
 
@@ -266,6 +279,36 @@ def rowgemm(A, W16, b16, flags=0, a_idx=None, M=None, res32=None, res16=None, re
             raise RuntimeError(f"rowgemm: {nm} must be contiguous fp16 [*, 384]")
     H.check(H.lib().dpvo_rowgemm(_ct.byref(a), H.stream_of(A)))
     return out32, out16, head_out
+
+
+def rowgemm_pair(A, Wa, ba, Wb, bb, M_dev=None):
+    """(A Wa^T + ba, A Wb^T + bb) as fp16 [M, 384] each, one launch sharing A
+    (dpvo_rowgemm_pair: SoftAgg's f and g)."""
+    H.on_gpu(A, Wa, ba, Wb, bb)
+    if any(t.dtype != torch.float16 for t in (A, Wa, ba, Wb, bb)):
+        raise RuntimeError("rowgemm_pair: A, weights and biases must be fp16")
+    if Wa.shape != Wb.shape or Wa.shape[0] != WIDTH or not (Wa.is_contiguous() and Wb.is_contiguous()):
+        raise RuntimeError("rowgemm_pair: Wa and Wb must be contiguous [384, Kp] of one shape")
+    if A.dim() != 2 or A.stride(1) != 1 or A.stride(0) < Wa.shape[1]:
+        raise RuntimeError("rowgemm_pair: A must be [rows, >=Kp] row-contiguous")
+    M, Kp, dev = A.shape[0], Wa.shape[1], A.device
+    outs = []
+    args = []
+    for W, b in ((Wa, ba), (Wb, bb)):
+        o = torch.empty(M, WIDTH, dtype=torch.float16, device=dev)
+        a = RowGemmArgs()
+        a.A, a.lda, a.a_idx, a.a_rows = _p(A), A.stride(0), None, M
+        a.W, a.K, a.N, a.bias, a.zero_row = _p(W), Kp, WIDTH, _p(b), _p(zero_row(dev, Kp))
+        a.M, a.flags = M, 0
+        a.out16, a.ldo16 = _p(o), o.stride(0)
+        if M_dev is not None:
+            if M_dev.dtype != torch.int64 or not M_dev.is_cuda:
+                raise RuntimeError("rowgemm_pair: M_dev must be a device int64 scalar")
+            a.M_dev = M_dev.data_ptr()
+        outs.append(o)
+        args.append(a)
+    H.check(H.lib().dpvo_rowgemm_pair(_ct.byref(args[0]), _ct.byref(args[1]), H.stream_of(A)))
+    return outs[0], outs[1]
 
 
 def rowadd_ln(a, b16=None, b_idx=None, ln=None, want32=True, want16=True):
