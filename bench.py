@@ -390,6 +390,7 @@ def main():
         if args.graph:
             for _ in range(3):
                 slam.update()
+            torch.cuda.synchronize()
             corr_ms = probe.mean_ms()
         slam.check_ba()
         breakdown = phase_breakdown(slam)

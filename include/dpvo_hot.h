@@ -302,8 +302,12 @@ int dpvo_softagg_forward(int dtype, const void* f, int64_t ldf, const void* s, i
  * = number of distinct keys.  Keys must lie in [0, 2^key_bits) when
  * key_bits <= 32 (a 32-bit radix sort over key_bits bits); key_bits in 33..64
  * sorts the full 64-bit key (any int64; gid order is then unsigned order).
- * offs has n+1 entries, perm n. */
+ * offs has n+1 entries, perm n.  With key_bits <= 22 and a workspace of
+ * dpvo_group_by_workspace_bytes_for(n, key_bits) bytes the group-by runs as a
+ * counting sort over 2^key_bits bins (5 launches, same outputs); a workspace of
+ * dpvo_group_by_workspace_bytes(n) bytes always takes the radix-sort path. */
 size_t dpvo_group_by_workspace_bytes(int64_t n);
+size_t dpvo_group_by_workspace_bytes_for(int64_t n, int key_bits);
 int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_t* gid, int* offs, int* perm, int64_t* groups,
                   void* workspace, size_t workspace_bytes, void* stream);
 

@@ -112,9 +112,43 @@ def test_group_by_matches_torch_unique(n, hi):
         assert (inv_c[members] == k).all()
 
 
+@pytest.mark.parametrize("n,bits,distinct", [(1, 1, 1), (1000, 6, 40), (95424, 19, 4416), (95424, 22, 600),
+                                             (20000, 12, 8), (5000, 22, 5000)])
+def test_group_by_counting_sort_equals_radix(n, bits, distinct):
+    """key_bits <= 22 takes the counting-sort path: outputs identical to the
+    stable radix-sort path (groups of 1 .. ~7000 members, > 64 and <= 64)."""
+    import update_ops
+    g = torch.Generator(device="cuda").manual_seed(n + bits)
+    vals = torch.randint(0, 2 ** bits, (distinct,), device="cuda", generator=g)
+    key = vals[torch.randint(0, distinct, (n,), device="cuda", generator=g)]
+    a = update_ops.group_by(key, key_bits=bits)
+    b = update_ops.group_by(key, key_bits=bits, radix=True)
+    G = int(a[3].item())
+    assert torch.equal(a[3], b[3]) and torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])
+    assert torch.equal(a[1][:G + 1], b[1][:G + 1])   # entries past G are unspecified
+    uniq, inv = torch.unique(key, return_inverse=True)
+    assert int(a[3].item()) == uniq.numel() and torch.equal(a[0], inv)
+
+
+def test_group_by_counting_sort_runs_of_equal_keys():
+    """Runs of equal keys (the tracker's edge blocks): one atomic per run in a
+    wave; runs crossing wave and block boundaries, a partial last wave."""
+    import update_ops
+    g = torch.Generator(device="cuda").manual_seed(9)
+    runs = torch.randint(1, 300, (700,), device="cuda", generator=g)
+    vals = torch.randint(0, 2 ** 16, (700,), device="cuda", generator=g)
+    key = torch.repeat_interleave(vals, runs)[:100001]
+    a = update_ops.group_by(key, key_bits=16)
+    b = update_ops.group_by(key, key_bits=16, radix=True)
+    G = int(a[3].item())
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[1][:G + 1], b[1][:G + 1])
+
+
 def test_group_by_empty():
     import update_ops
     gid, offs, perm, G = update_ops.group_by(torch.zeros(0, dtype=torch.int64, device="cuda"))
+    assert int(G.item()) == 0 and gid.numel() == 0
+    gid, offs, perm, G = update_ops.group_by(torch.zeros(0, dtype=torch.int64, device="cuda"), key_bits=12)
     assert int(G.item()) == 0 and gid.numel() == 0
 
 

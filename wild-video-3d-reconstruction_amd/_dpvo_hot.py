@@ -68,6 +68,7 @@ _SIGNATURES = {
     "dpvo_softagg_forward": (_ip, [_ip, _vp, _i64, _vp, _i64, _vp, _i64, _ip, _i64, _fp, _vp, _vp, _sz, _vp]),
     "dpvo_gather_rows": (_ip, [_ip, _vp, _i64, _i64, _vp, _i64, _ip, _ip, _vp, _vp]),
     "dpvo_group_by_workspace_bytes": (_sz, [_i64]),
+    "dpvo_group_by_workspace_bytes_for": (_sz, [_i64, _ip]),
     "dpvo_group_by": (_ip, [_vp, _i64, _ip, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dpvo_softagg_csr": (_ip, [_ip, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _ip, _fp, _vp, _vp]),
     "dpvo_neighbors_csr": (_ip, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),

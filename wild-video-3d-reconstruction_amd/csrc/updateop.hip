@@ -15,6 +15,8 @@
 //
 // Bytes per edge: 2 rows x D x sizeof(T) read once (+12 B of CSR traffic);
 // the kernel is HBM-bound like the GEMMs around it.
+#include <climits>
+
 #include <hipcub/hipcub.hpp>
 
 #include "common.hpp"
@@ -279,6 +281,139 @@ GbLayout gb_layout(int64_t n)
     return L;
 }
 
+// Counting-sort group-by for keys bounded by 2^key_bits <= 2^22 (the tracker's
+// kk < N M and its dense (ii, jj) pair key): a histogram with atomic slots, one
+// exclusive scan over the bins carrying (start, group index) together, a
+// scatter, and a per-group fix-up that restores ascending edge order inside
+// each group (the atomic slots are arrival order) -- the same outputs as the
+// stable radix sort, in 5 launches instead of ~12 (the radix path's merge
+// passes, flags, scan and finish kernels).
+constexpr int CB_MAX_BITS = 22;
+
+struct CbLayout {
+    int64_t hist, pre, slot, ptmp, tmp, tmp_bytes, total;
+};
+
+struct CbCombine {
+    __host__ __device__ int64_t operator()(int c) const { return (int64_t)c | ((int64_t)(c > 0) << 32); }
+};
+
+CbLayout cb_layout(int64_t n, int key_bits)
+{
+    const int64_t B = int64_t(1) << key_bits;
+    CbLayout L;
+    int64_t o = 0;
+    L.hist = o; o += align256(4 * B);
+    L.pre = o;  o += align256(8 * B);
+    L.slot = o; o += align256(4 * n);
+    L.ptmp = o; o += align256(4 * n);
+    L.tmp = o;
+    size_t tb = 0;
+    hipcub::TransformInputIterator<int64_t, CbCombine, const int*> it(nullptr, CbCombine());
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, it, (int64_t*)nullptr, (int)B);
+    L.tmp_bytes = (int64_t)tb;
+    o += align256(L.tmp_bytes);
+    L.total = o;
+    return L;
+}
+
+// runs of equal keys inside a wave take one atomic per run (the run head's),
+// so bins hit by many consecutive edges do not serialise on one address
+__global__ __launch_bounds__(256) void cb_hist_kernel(const int64_t* __restrict__ key, int64_t n, uint32_t mask,
+                                                      int* __restrict__ hist, int* __restrict__ slot)
+{
+    const int lane = threadIdx.x & 63;
+    for (int64_t e0 = blockIdx.x * (int64_t)blockDim.x; e0 < n; e0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = e0 + threadIdx.x;   // uniform trip count: whole waves stay converged
+        const bool valid = e < n;
+        const uint32_t k = valid ? (uint32_t)key[e] & mask : 0xffffffffu;
+        const uint32_t prev = __shfl_up(k, 1);
+        const bool head = valid && (lane == 0 || prev != k);
+        const uint64_t hm = __ballot(head), vm = __ballot(valid);
+        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+        const int hl = 63 - __clzll(hm & upto);                  // my run's head lane
+        const uint64_t above = hm & ~upto;
+        const int end = above ? __ffsll((long long)above) - 1 : 64 - __clzll(vm);   // valid lanes are a prefix
+        int base = 0;
+        if (head) base = atomicAdd(&hist[k], end - lane);
+        base = __shfl(base, valid ? hl : 0);
+        if (valid) slot[e] = base + (lane - hl);
+    }
+}
+
+__global__ __launch_bounds__(256) void cb_scatter_kernel(const int64_t* __restrict__ key, int64_t n, uint32_t mask,
+                                                         const int* __restrict__ hist, const int64_t* __restrict__ pre,
+                                                         const int* __restrict__ slot, int* __restrict__ ptmp,
+                                                         int64_t* __restrict__ gid, int* __restrict__ offs,
+                                                         int64_t* __restrict__ groups)
+{
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = pre[(uint32_t)key[e] & mask];
+        const int start = (int)(p & 0xffffffff), g = (int)(p >> 32), s = slot[e];
+        ptmp[start + s] = (int)e;
+        gid[e] = g;
+        if (s == 0) offs[g] = start;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const int64_t last = pre[mask] + CbCombine()(hist[mask]);
+        const int64_t G = last >> 32;
+        *groups = G;
+        offs[G] = (int)n;
+    }
+}
+
+// one wave per group: members back into ascending edge order (ranks by
+// comparison; edge ids are distinct, so the ranks are a permutation).  Groups
+// of <= 64 rank in registers (readlane broadcasts), up to CB_CAP members
+// through the wave's LDS slice (16-byte broadcast reads), larger ones from
+// global memory (L2).
+constexpr int CB_CAP = 2048;
+constexpr int CB_WAVES = 4;
+
+__global__ __launch_bounds__(64 * CB_WAVES) void cb_fix_kernel(const int* __restrict__ ptmp,
+                                                               const int* __restrict__ offs,
+                                                               const int64_t* __restrict__ groups,
+                                                               int* __restrict__ perm)
+{
+    __shared__ __attribute__((aligned(16))) int buf[CB_WAVES][CB_CAP];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int* mine = buf[w];
+    const int64_t G = *groups;
+    for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < G;
+         g += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        const int b = offs[g], S = offs[g + 1] - b;
+        if (S <= 64) {
+            const int v = lane < S ? ptmp[b + lane] : INT_MAX;
+            int rank = 0;
+            for (int j = 0; j < S; j++) rank += __builtin_amdgcn_readlane(v, j) < v;
+            if (lane < S) perm[b + rank] = v;
+        } else if (S <= CB_CAP) {
+            for (int i = lane; i < S; i += 64) mine[i] = ptmp[b + i];
+            for (int i = S + lane; i < ((S + 3) & ~3); i += 64) mine[i] = INT_MAX;   // pad the last int4
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (int i = lane; i < S; i += 64) {
+                const int v = mine[i];
+                int rank = 0;
+                for (int j = 0; j < S; j += 4) {
+                    const int4 q = *(const int4*)(mine + j);
+                    rank += (q.x < v) + (q.y < v) + (q.z < v) + (q.w < v);
+                }
+                perm[b + rank] = v;
+            }
+            __builtin_amdgcn_wave_barrier();   // every lane's reads before the next group's writes
+        } else {
+            for (int i = lane; i < S; i += 64) {
+                const int v = ptmp[b + i];
+                int rank = 0;
+                for (int j = 0; j < S; j++) rank += ptmp[b + j] < v;
+                perm[b + rank] = v;
+            }
+        }
+    }
+}
+
 // SoftAgg over a prebuilt CSR whose group count lives on the device.  Group
 // members are already in ascending edge order (stable sort): no LDS sort.
 template <typename T>
@@ -406,6 +541,13 @@ extern "C" size_t dpvo_group_by_workspace_bytes(int64_t n)
     return (size_t)gb_layout(n > 0 ? n : 1).total + 256;
 }
 
+extern "C" size_t dpvo_group_by_workspace_bytes_for(int64_t n, int key_bits)
+{
+    size_t r = dpvo_group_by_workspace_bytes(n);
+    if (key_bits >= 1 && key_bits <= CB_MAX_BITS) r = std::max(r, (size_t)cb_layout(n > 0 ? n : 1, key_bits).total + 256);
+    return r;
+}
+
 extern "C" int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_t* gid, int* offs, int* perm,
                              int64_t* groups, void* workspace, size_t workspace_bytes, void* stream)
 {
@@ -418,9 +560,32 @@ extern "C" int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_
         DPVO_CHECK_HIP(hipMemsetAsync(offs, 0, sizeof(int), st));
         return 0;
     }
+    char* ws = (char*)(((uintptr_t)workspace + 255) & ~uintptr_t(255));
+    if (key_bits <= CB_MAX_BITS && workspace != nullptr) {
+        const CbLayout C = cb_layout(n, key_bits);
+        if (workspace_bytes >= (size_t)C.total + 256) {   // else: the radix path below
+            const int64_t B = int64_t(1) << key_bits;
+            const uint32_t mask = (uint32_t)(B - 1);
+            int* hist = (int*)(ws + C.hist);
+            int64_t* pre = (int64_t*)(ws + C.pre);
+            int* slot = (int*)(ws + C.slot);
+            int* ptmp = (int*)(ws + C.ptmp);
+            const unsigned gn = grid_for(n, 256, 2048);
+            DPVO_CHECK_HIP(hipMemsetAsync(hist, 0, 4 * B, st));
+            hipLaunchKernelGGL(cb_hist_kernel, dim3(gn), dim3(256), 0, st, key, n, mask, hist, slot);
+            size_t tb = (size_t)C.tmp_bytes;
+            hipcub::TransformInputIterator<int64_t, CbCombine, const int*> it(hist, CbCombine());
+            DPVO_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(ws + C.tmp, tb, it, pre, (int)B, st));
+            hipLaunchKernelGGL(cb_scatter_kernel, dim3(gn), dim3(256), 0, st, key, n, mask, hist, pre, slot, ptmp, gid,
+                               offs, groups);
+            const unsigned gf = grid_for(std::min<int64_t>(n, B) * 64, 64 * CB_WAVES, 2048);
+            hipLaunchKernelGGL(cb_fix_kernel, dim3(gf), dim3(64 * CB_WAVES), 0, st, ptmp, offs, groups, perm);
+            DPVO_CHECK_LAUNCH();
+            return 0;
+        }
+    }
     const GbLayout L = gb_layout(n);
     DPVO_CHECK_ARG(workspace != nullptr && workspace_bytes >= (size_t)L.total + 256, "workspace too small");
-    char* ws = (char*)(((uintptr_t)workspace + 255) & ~uintptr_t(255));
     int* v_in = (int*)(ws + L.v_in);
     int* flag = (int*)(ws + L.flag);
     int* incl = (int*)(ws + L.incl);

@@ -40,12 +40,14 @@ def key_bits_for(bound):
     return max(1, (int(bound) - 1).bit_length())
 
 
-def group_by(key, key_bits=64):
+def group_by(key, key_bits=64, radix=False):
     """torch.unique(key, return_inverse=True) without a host sync, plus the
     groups' CSR: -> (gid int64 [E], offs int32 [E+1], perm int32 [E],
     groups int64 [1] on the device).  key_bits <= 32 promises keys in
     [0, 2**key_bits) (fewer radix passes: pass key_bits_for(bound) when the
-    caller knows a bound); the default sorts full 64-bit keys."""
+    caller knows a bound); the default sorts full 64-bit keys.  key_bits <= 22
+    runs as a counting sort over 2**key_bits bins unless radix=True (the
+    radix-sort path; same outputs)."""
     if not 1 <= int(key_bits) <= 64:
         raise RuntimeError("group_by: key_bits must be 1..64")
     H.on_gpu(key)
@@ -56,7 +58,8 @@ def group_by(key, key_bits=64):
     offs = torch.empty(n + 1, dtype=torch.int32, device=dev)
     perm = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     groups = torch.empty(1, dtype=torch.int64, device=dev)
-    nbytes = H.lib().dpvo_group_by_workspace_bytes(n)
+    nbytes = (H.lib().dpvo_group_by_workspace_bytes(n) if radix
+              else H.lib().dpvo_group_by_workspace_bytes_for(n, int(key_bits)))
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     H.check(H.lib().dpvo_group_by(H.ptr(key), n, int(key_bits), H.ptr(gid), H.ptr(offs), H.ptr(perm), H.ptr(groups),
                                   H.ptr(ws), nbytes, H.stream_of(key)))
