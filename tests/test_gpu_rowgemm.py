@@ -230,24 +230,29 @@ def test_fused_update_operator_context_index_is_the_gathered_context():
     assert torch.equal(a[1][0], b[1][0]) and torch.equal(a[1][1], b[1][1])
 
 
+@pytest.mark.parametrize("big", [False, True])
 @pytest.mark.parametrize("case", ["corr", "gather_res", "gate_ln", "gate_heads"])
-def test_rowchain_is_two_rowgemms(case):
+def test_rowchain_is_two_rowgemms(case, big):
     """dpvo_rowchain (the intermediate kept in LDS) is bit-identical to two
     rowgemm launches with the intermediate in HBM: same MFMA chunk order,
-    same fp16 rounding of the intermediate."""
+    same fp16 rounding of the intermediate.  big: more 128-row tiles than
+    workgroups, so blocks run several tiles and the row pass of one tile is
+    interleaved with the next tile's first GEMM (ILV)."""
     import update_ops as U
     torch.manual_seed(3)
     M = 1000 if case != "gather_res" else 777
+    if big:
+        M = 70001
     K1 = 896 if case == "corr" else 384
     dev = "cuda"
-    A = (torch.randn(1200, K1, device=dev) * 0.5).half()
+    A = (torch.randn(max(1200, M), K1, device=dev) * 0.5).half()
     W1, b1 = U.pack_linear(torch.randn(384, K1, device=dev) / K1 ** 0.5, torch.randn(384, device=dev) * 0.1)
     W2, b2 = U.pack_linear(torch.randn(384, 384, device=dev) / 20.0, torch.randn(384, device=dev) * 0.1)
     ln = (torch.rand(384, device=dev) + 0.5, torch.randn(384, device=dev) * 0.1, 1e-3)
     res32 = torch.randn(M, 384, device=dev)
     gate16 = torch.rand(M, 384, device=dev).half()
     heads = (torch.randn(4, 384, device=dev).half() * 0.05, torch.randn(4, device=dev).half())
-    a_idx = torch.randint(-1, 1200, (M,), device=dev) if case == "gather_res" else None
+    a_idx = torch.randint(-1, A.shape[0], (M,), device=dev) if case == "gather_res" else None
     kw = {"corr": dict(flags=U.LN | U.LN_RELU, ln=ln),
           "gather_res": dict(flags=U.RES, res32=res32, want32=True),
           "gate_ln": dict(flags=U.GATE | U.LN, res32=res32, gate16=gate16, ln=ln, want32=True),

@@ -789,7 +789,9 @@ struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflic
 // residual like RES, which is bit-for-bit the GATE epilogue's
 // x + fp16(gate * y) without the 73 MB gate16 round trip (nor a gate held in
 // registers across the GEMMs).
-template <int F2, bool GATED = false>
+// DBG (timing experiments only, DPVO_RC_DBG, flag RES; scripts/bench_rc_dbg.py):
+// 1 no row pass, 2 no MFMA, 3 neither
+template <int F2, bool GATED = false, int DBG = 0>
 __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
                                                                  dpvo_rowgemm_args pg)
 {
@@ -882,6 +884,10 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             for (int nt = 0; nt < 6; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
     };
     auto mfma_step = [&](const h8_t (&a)[4], const h8_t (&b)[6]) {
+        if (DBG & 2) {
+            acc[0][0][0] += (float)a[0][0] + (float)b[0][0];
+            return;
+        }
 #pragma unroll
         for (int mt = 0; mt < 4; mt++)
 #pragma unroll
@@ -998,7 +1004,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         load_consts<F2>(p, lane, kc);
         constexpr int RB = (F2 & (RG_RES | RG_GATE | RG_LN)) ? 4 : 8;
 #pragma unroll 1
-        for (int q0 = 0; q0 < 16; q0 += RB)   // one batch live at a time (register budget)
+        for (int q0 = 0; q0 < 16 && !(DBG & 1); q0 += RB)   // one batch live at a time (register budget)
             epilogue_rows<F2, RB>(p, Mrows, smem, ym, wave * 16 + q0, tile * RG_BM + wave * 16 + q0, lane, kc);
         sync_lds();
     }
@@ -1641,6 +1647,22 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
 #undef RCG_CASE
         default:
             set_error("dpvo_rowchain_gated: unsupported epilogue flag combination " + std::to_string(f));
+            return -1;
+        }
+        DPVO_CHECK_LAUNCH();
+        return 0;
+    }
+    if (const char* dbgs = getenv("DPVO_RC_DBG"); dbgs && f == DPVO_RG_RES && !gate) {   // timing experiments
+        switch (atoi(dbgs)) {
+#define RCD_CASE(D)                                                                                               \
+    case (D):                                                                                                     \
+        hipLaunchKernelGGL((rowchain_kernel<DPVO_RG_RES, false, (D)>), dim3(grid), dim3(RG_THREADS), 0,            \
+                           as_stream(stream), *g1, a2, a2);                                                       \
+        break;
+            RCD_CASE(0) RCD_CASE(1) RCD_CASE(2) RCD_CASE(3)
+#undef RCD_CASE
+        default:
+            set_error("DPVO_RC_DBG: unsupported value");
             return -1;
         }
         DPVO_CHECK_LAUNCH();
