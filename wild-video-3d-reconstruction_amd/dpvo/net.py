@@ -5,6 +5,8 @@ native pieces -- altcorr.patchify and fastba.neighbors -- run on the HIP
 library.  Parameter names follow the reference so dpvo.pth loads unchanged.
 Training (VONet.forward, net.py:355-440) is out of scope for this build.
 """
+import copy
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -226,12 +228,14 @@ class Patchifier(nn.Module):
         patches = altcorr.patchify(grid[0], coords, P // 2).view(b, -1, 3, P, P)
         return gmap, imap, patches, clr
 
-    def _ingest(self, image, x, y, return_color):
+    def _ingest(self, image, x, y, return_color, encoders=None):
         """forward() after the centre draw: fixed shapes, no host syncs -- the
-        body of the captured graph."""
+        body of the captured graph.  encoders: (fnet, inet) to run instead of
+        the modules' own (the graph's fp16 copies)."""
+        fnet, inet = encoders or (self.fnet, self.inet)
         images = 2 * (image[None, None] / 255.0) - 0.5
-        fmap = self.fnet(images) / 4.0
-        imap = self.inet(images) / 4.0
+        fmap = fnet(images) / 4.0
+        imap = inet(images) / 4.0
         return (fmap,) + self._gather(images, fmap, imap, x, y, None, return_color)
 
     def _forward_graphed(self, image, M, return_color):
@@ -271,14 +275,23 @@ class Patchifier(nn.Module):
         side = torch.cuda.Stream(device=image.device)
         side.wait_stream(torch.cuda.current_stream(image.device))
         dt = key[5] or torch.float16
+        # under autocast every convolution casts its fp32 weight and bias to the
+        # autocast dtype on each call (the cast cache is off inside a graph):
+        # ~50 cast kernels per frame.  The graph runs copies of the encoders
+        # already in that dtype -- the same values the casts produce, so the
+        # same convolutions (bit-identical to the eager path, test_gpu_tracker)
+        enc = None
+        if amp:
+            enc = tuple(copy.deepcopy(m).to(dt) for m in (self.fnet, self.inet))
         with torch.cuda.stream(side), torch.autocast("cuda", dtype=dt, enabled=amp, cache_enabled=False):
             for _ in range(2):  # warm-up: MIOpen solver selection, allocator pools
-                self._ingest(*static, return_color)
+                self._ingest(*static, return_color, enc)
         torch.cuda.current_stream(image.device).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph), torch.autocast("cuda", dtype=dt, enabled=amp, cache_enabled=False):
-            out = self._ingest(*static, return_color)
+            out = self._ingest(*static, return_color, enc)
         self._graph, self._graph_key, self._g_in, self._g_out = graph, key, static, out
+        self._g_enc = enc   # the graph holds their parameters' addresses
 
 
 class VONet(nn.Module):
