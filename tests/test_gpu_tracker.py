@@ -174,6 +174,25 @@ def test_keyframe_matches_reference_loop(drop):
     assert a.pg.delta.keys() == b.pg.delta.keys()
 
 
+def test_keyframe_raises_on_nan_pose_when_kept():
+    """The keep path raises on a NaN pose at the keyframe index (dpvo.py:647),
+    read with the motion magnitudes; the drop path removes that frame instead."""
+    from dpvo.synthetic import steady_state_tracker
+    with torch.no_grad():
+        for drop in (False, True):
+            s = steady_state_tracker("fast", buffer=96, n=70, seed=4)
+            s.cfg.KEYFRAME_THRESH = 1e9 if drop else -1.0
+            k = s.n - s.cfg.KEYFRAME_INDEX
+            s.pg.poses_[k, 2] = float("nan")
+            if drop:
+                n0 = s.n
+                s.keyframe()
+                assert s.n == n0 - 1
+            else:
+                with pytest.raises(Exception, match="nan"):
+                    s.keyframe()
+
+
 def test_graphed_ingest_matches_eager():
     """Patchifier.forward replayed from its captured HIP graph gives the eager
     launches' results bit for bit (same seed -> same patch centres), and each

@@ -350,8 +350,10 @@ class DPVO:
         k = self.n - self.cfg.KEYFRAME_INDEX
         i, j = k - 1, k + 1
         # one host read for both directions (the reference reads each, :609),
-        # and for the deferred BA status of the update()s since the last one
-        vals = torch.cat([self._motionmag_dev(i, j), self._ba_fail.float()]).tolist()
+        # for the deferred BA status of the update()s since the last one, and
+        # for the pose-NaN check of the keep path (:647, its own read there)
+        vals = torch.cat([self._motionmag_dev(i, j), self._ba_fail.float(),
+                          torch.isnan(self.pg.poses_[k]).any().float()[None]]).tolist()
         self.check_ba(int(vals[2]))
         m = vals[0] + vals[1]
         if m / 2 < self.cfg.KEYFRAME_THRESH:
@@ -382,7 +384,7 @@ class DPVO:
                 self.image_buffer_[dst % self.mem] = self.image_buffer_[src % self.mem]
             self.n -= 1
             self.pg.m -= self.M
-        elif torch.isnan(self.pg.poses_[k]).any():
+        elif vals[3]:
             raise Exception("Error: the estimated pose is nan!")
         self.remove_factors(self.ix[self.pg.kk] < self.n - self.cfg.REMOVAL_WINDOW, store=True)
 
