@@ -146,10 +146,13 @@ __global__ __launch_bounds__(MM_THREADS) void motion_mag_kernel(const float* pos
 }
 
 // The same two means over many workgroups (the single-workgroup scan of the
-// ~95k-edge list takes ~80 us): each workgroup reduces a contiguous chunk of
-// edges in a fixed tree order into part[block] = (sum, count) per direction;
-// motion_mag_final_kernel adds the partials in block order (deterministic).
-constexpr int MM2_THREADS = 256, MM2_MAXBLK = 256;
+// ~95k-edge list takes ~80 us, a latency chain of dependent index loads per
+// thread): one edge per thread (grid-stride past MM2_MAXBLK blocks), each
+// workgroup reduces its threads in a fixed tree order into part[block] =
+// (sum, count) per direction, and motion_mag_final_kernel adds the partials in
+// a fixed order too (deterministic).
+constexpr int MM2_THREADS = 256, MM2_MAXBLK = 4096;
+template <int PT>   // PT = P * P when known at compile time (the P*P pixel loop unrolls), else 0
 __global__ __launch_bounds__(MM2_THREADS) void motion_mag_part_kernel(const float* poses, const float* patches, int P,
                                                                      const float* intr, const int64_t* ii,
                                                                      const int64_t* jj, const int64_t* kk, int64_t E,
@@ -158,12 +161,10 @@ __global__ __launch_bounds__(MM2_THREADS) void motion_mag_part_kernel(const floa
     __shared__ float s_sum[2][MM2_THREADS];
     __shared__ int s_cnt[2][MM2_THREADS];
     const int t = threadIdx.x;
-    const int64_t PP = (int64_t)P * P;
-    const int64_t chunk = (E + gridDim.x - 1) / gridDim.x;
-    const int64_t e0 = blockIdx.x * chunk, e1 = min(E, e0 + chunk);
+    const int64_t PP = PT ? PT : (int64_t)P * P;
     float sum[2] = {0.f, 0.f};
     int cnt[2] = {0, 0};
-    for (int64_t e = e0 + t; e < e1; e += MM2_THREADS) {
+    for (int64_t e = blockIdx.x * (int64_t)MM2_THREADS + t; e < E; e += (int64_t)gridDim.x * MM2_THREADS) {
         const int64_t a = ii[e], b = jj[e];
         const int dir = (a == fi && b == fj) ? 0 : (a == fj && b == fi) ? 1 : -1;
         if (dir < 0) continue;
@@ -174,6 +175,8 @@ __global__ __launch_bounds__(MM2_THREADS) void motion_mag_part_kernel(const floa
         g2.so3.q.x = 0.f; g2.so3.q.y = 0.f; g2.so3.q.z = 0.f; g2.so3.q.w = 1.f;
         const float *ka = intr + a * 4, *kb = intr + b * 4;
         const float* pa = patches + kk[e] * 3 * PP;
+        float s = 0.f;
+#pragma unroll
         for (int64_t q = 0; q < PP; q++) {
             float x0, y0, x1, y1, x2, y2;
             project_px(g0, ka, ka, pa, PP, q, x0, y0);
@@ -181,8 +184,9 @@ __global__ __launch_bounds__(MM2_THREADS) void motion_mag_part_kernel(const floa
             project_px(g2, ka, kb, pa, PP, q, x2, y2);
             const float f1 = sqrtf((x1 - x0) * (x1 - x0) + (y1 - y0) * (y1 - y0));
             const float f2 = sqrtf((x2 - x0) * (x2 - x0) + (y2 - y0) * (y2 - y0));
-            sum[dir] += beta * f1 + (1.0f - beta) * f2;
+            s += beta * f1 + (1.0f - beta) * f2;
         }
+        sum[dir] += s;
         cnt[dir]++;
     }
     for (int d = 0; d < 2; d++) { s_sum[d][t] = sum[d]; s_cnt[d][t] = cnt[d]; }
@@ -198,17 +202,28 @@ __global__ __launch_bounds__(MM2_THREADS) void motion_mag_part_kernel(const floa
     }
 }
 
-__global__ void motion_mag_final_kernel(const float* part, int nblk, int64_t PP, float* out)
+// partials of nblk workgroups -> the two means; 256 threads take strided
+// partials, then a fixed tree (deterministic for a given nblk)
+__global__ __launch_bounds__(MM2_THREADS) void motion_mag_final_kernel(const float* part, int nblk, int64_t PP, float* out)
 {
-    const int d = threadIdx.x;
-    if (d >= 2) return;
-    float s = 0.f;
-    int64_t c = 0;
-    for (int b = 0; b < nblk; b++) {
-        s += part[b * 4 + 2 * d];
-        c += __float_as_int(part[b * 4 + 2 * d + 1]);
+    __shared__ float s_sum[2][MM2_THREADS];
+    __shared__ int s_cnt[2][MM2_THREADS];
+    const int t = threadIdx.x;
+    float sm[2] = {0.f, 0.f};
+    int c[2] = {0, 0};
+    for (int b = t; b < nblk; b += MM2_THREADS)
+        for (int d = 0; d < 2; d++) {
+            sm[d] += part[b * 4 + 2 * d];
+            c[d] += __float_as_int(part[b * 4 + 2 * d + 1]);
+        }
+    for (int d = 0; d < 2; d++) { s_sum[d][t] = sm[d]; s_cnt[d][t] = c[d]; }
+    __syncthreads();
+    for (int w = MM2_THREADS / 2; w > 0; w >>= 1) {
+        if (t < w)
+            for (int d = 0; d < 2; d++) { s_sum[d][t] += s_sum[d][t + w]; s_cnt[d][t] += s_cnt[d][t + w]; }
+        __syncthreads();
     }
-    out[d] = c ? s / (float)(c * PP) : __builtin_nanf("");
+    if (t < 2) out[t] = s_cnt[t][0] ? s_sum[t][0] / (float)((int64_t)s_cnt[t][0] * PP) : __builtin_nanf("");
 }
 
 // Keyframe distance matrix for the global BA's distance-based edges
@@ -361,11 +376,16 @@ extern "C" int dpvo_motion_mag_ws(const float* poses, const float* patches, int 
     DPVO_CHECK_ARG(num_edges >= 0, "negative edge count");
     DPVO_CHECK_ARG(out && (num_edges == 0 || (poses && patches && intrinsics && ii && jj && kk)), "null operand");
     DPVO_CHECK_ARG(workspace && workspace_bytes >= dpvo_motion_mag_workspace_bytes(num_edges), "workspace too small");
-    const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>((num_edges + 1023) / 1024, MM2_MAXBLK));
-    hipLaunchKernelGGL(motion_mag_part_kernel, dim3(nblk), dim3(MM2_THREADS), 0, as_stream(stream), poses, patches, P,
-                       intrinsics, ii, jj, kk, num_edges, i, j, beta, (float*)workspace);
-    hipLaunchKernelGGL(motion_mag_final_kernel, dim3(1), dim3(64), 0, as_stream(stream), (const float*)workspace, nblk,
-                       (int64_t)P * P, out);
+    const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>((num_edges + MM2_THREADS - 1) / MM2_THREADS,
+                                                                  MM2_MAXBLK));
+    if (P == 3)
+        hipLaunchKernelGGL(motion_mag_part_kernel<9>, dim3(nblk), dim3(MM2_THREADS), 0, as_stream(stream), poses,
+                           patches, P, intrinsics, ii, jj, kk, num_edges, i, j, beta, (float*)workspace);
+    else
+        hipLaunchKernelGGL(motion_mag_part_kernel<0>, dim3(nblk), dim3(MM2_THREADS), 0, as_stream(stream), poses,
+                           patches, P, intrinsics, ii, jj, kk, num_edges, i, j, beta, (float*)workspace);
+    hipLaunchKernelGGL(motion_mag_final_kernel, dim3(1), dim3(MM2_THREADS), 0, as_stream(stream),
+                       (const float*)workspace, nblk, (int64_t)P * P, out);
     DPVO_CHECK_LAUNCH();
     return 0;
 }
