@@ -70,7 +70,8 @@ class Update(nn.Module):
                 torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16 and
                 self.FUSED)
 
-    def _forward_fused(self, net, inp, corr, ii, jj, kk, inp_idx=None, index_bounds=None, kk_groups=None):
+    def _forward_fused(self, net, inp, corr, ii, jj, kk, inp_idx=None, index_bounds=None, kk_groups=None,
+                       ij_groups=None):
         """The same dataflow as the reference under autocast, in 19 full-row
         fused GEMMs (csrc/rowgemm.hip; 5 Linear->ReLU->Linear pairs chained,
         14 launches) + 2 SoftAggs: every Linear is an fp16
@@ -111,7 +112,10 @@ class Update(nn.Module):
         ln0, gr1, ln1, gr2 = pk["gru"]
         for (pf, pg_, ph), key, ln in ((pk["agg_kk"], None, None), (pk["agg_ij"], ii * 12345 + jj, ln0)):
             # unique(key) + CSR on the device (no host sync); G stays on the device
-            gid, offs, perm, G = kk_groups if key is None else U.group_by(key, key_bits=ij_bits)
+            if key is None:
+                gid, offs, perm, G = kk_groups
+            else:
+                gid, offs, perm, G = ij_groups if ij_groups is not None else U.group_by(key, key_bits=ij_bits)
             f16, g16 = U.rowgemm_pair(n16, *pf, *pg_)
             y = U.softagg_csr(f16, g16, offs, perm, G, E)
             _, hy, _ = U.rowgemm(y, *ph, M_dev=G)
@@ -128,16 +132,18 @@ class Update(nn.Module):
                                          gate=pgate, ln=ln1, want32=True)
         return n32[None], (heads[None, :, :2], heads[None, :, 2:], None)
 
-    def forward(self, net, inp, corr, flow, ii, jj, kk, inp_idx=None, index_bounds=None, kk_groups=None):
+    def forward(self, net, inp, corr, flow, ii, jj, kk, inp_idx=None, index_bounds=None, kk_groups=None,
+                ij_groups=None):
         """edge hidden state -> (new state, (delta, weight, None)) (net.py:75-93).
 
         Optional, not in the reference: inp_idx -- inp is then the un-gathered
         context ring and the rows are inp[:, inp_idx]; index_bounds =
         (num_patches, num_frames) -- kk < num_patches and ii, jj < num_frames,
-        which narrows the fused path's radix sorts; kk_groups =
-        update_ops.group_by(kk), when the caller already has it."""
+        which narrows the fused path's radix sorts; kk_groups / ij_groups =
+        update_ops.group_by(kk) / group_by(ii * 12345 + jj), when the caller
+        already has them."""
         if self._fusable(net, inp, corr) and (inp_idx is None or inp.is_contiguous()):
-            return self._forward_fused(net, inp, corr, ii, jj, kk, inp_idx, index_bounds, kk_groups)
+            return self._forward_fused(net, inp, corr, ii, jj, kk, inp_idx, index_bounds, kk_groups, ij_groups)
         if inp_idx is not None:
             inp = inp[:, inp_idx]
         net = self.norm(net + inp + self.corr(corr))
