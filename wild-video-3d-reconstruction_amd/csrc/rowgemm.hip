@@ -258,6 +258,186 @@ __device__ __forceinline__ void epilogue_rows(const dpvo_rowgemm_args& p, int64_
     epi_finish<FLAGS, R>(p, M, smem, ym, lrow0, row0, lane, k, o);
 }
 
+// ---- the row epilogue with two rows per wave (v3 / rowchain): half h = lane/32
+// takes row 2i + h, lane s = lane%32 of the half owns columns 4s + 128j (j < 3),
+// so every global access is a 16-byte (fp32) or 8-byte (fp16) vector -- half
+// the store instructions of the one-row-per-wave layout above, whose
+// completions every next-tile k-step wait includes (one vmcnt for loads and
+// stores).  Row sums: a DPP row reduce plus one gfx950 lane swap (a + b == b + a,
+// so every lane of the half agrees).
+typedef float ep_f4 __attribute__((ext_vector_type(4)));
+typedef _Float16 ep_h4 __attribute__((ext_vector_type(4)));
+
+struct EpiConsts2 {
+    ep_f4 g[3], b[3];     // LayerNorm weight / bias at this lane's columns
+    ep_f4 hw[4][3];       // head weights (fp16 values)
+    float hb[4];
+};
+
+template <int FLAGS>
+__device__ __forceinline__ void load_consts2(const dpvo_rowgemm_args& p, int lane, EpiConsts2& k)
+{
+    const int s = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const int c = 128 * j + 4 * s;
+        if (FLAGS & RG_LN) {
+            k.g[j] = *(const ep_f4*)(p.ln_g + c);
+            k.b[j] = *(const ep_f4*)(p.ln_b + c);
+        }
+        if (FLAGS & RG_HEADS) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const ep_h4 w = *(const ep_h4*)((const half_t*)p.head_w + q * RG_BN + c);
+                k.hw[q][j] = ep_f4{(float)w[0], (float)w[1], (float)w[2], (float)w[3]};
+            }
+        }
+    }
+    if (FLAGS & RG_HEADS) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) k.hb[q] = (float)((const half_t*)p.head_b)[q];
+    }
+}
+
+__device__ __forceinline__ float half_sum(float x)
+{
+    x = rowsum16(x);
+    auto h = __builtin_amdgcn_permlane16_swap(__float_as_int(x), __float_as_int(x), false, false);
+    return __int_as_float(h[0]) + __int_as_float(h[1]);
+}
+
+template <int R>   // R rows = R/2 row pairs
+struct EpiOps2 {
+    ep_f4 base[R / 2][3];   // res32
+    ep_h4 add[R / 2][3];    // res16[idx] or gate16
+};
+
+template <int FLAGS, int R>
+__device__ __forceinline__ void epi2_load(const dpvo_rowgemm_args& p, int64_t M, int64_t row0, int lane, EpiOps2<R>& o)
+{
+    if (!(FLAGS & (RG_RES | RG_GATE))) return;
+    const int h = lane >> 5, s = lane & 31;
+#pragma unroll
+    for (int i = 0; i < R / 2; i++) {
+        const int64_t rr = row0 + 2 * i + h;
+        const int64_t row = rr < M ? rr : M - 1;   // clamped for loads; stores skip rows >= M
+        const float* r32 = (const float*)p.res32 + row * p.ldr;
+        const half_t* r16 = nullptr;
+        if (FLAGS & RG_GATE) {
+            r16 = (const half_t*)p.gate16 + row * RG_BN;
+        } else if (p.res16) {
+            const int64_t src = p.res16_idx ? p.res16_idx[row] : row;
+            r16 = src >= 0 ? (const half_t*)p.res16 + src * RG_BN : nullptr;
+        }
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int c = 128 * j + 4 * s;
+            o.base[i][j] = *(const ep_f4*)(r32 + c);
+            o.add[i][j] = r16 ? *(const ep_h4*)(r16 + c) : ep_h4{(half_t)0, (half_t)0, (half_t)0, (half_t)0};
+        }
+    }
+}
+
+template <int FLAGS, int R, typename YMap>
+__device__ __forceinline__ void epi2_finish(const dpvo_rowgemm_args& p, int64_t M, const char* smem, YMap ym, int lrow0,
+                                            int64_t row0, int lane, const EpiConsts2& k, const EpiOps2<R>& o)
+{
+    const int h = lane >> 5, s = lane & 31;
+    ep_f4 v[R / 2][3];
+#pragma unroll
+    for (int i = 0; i < R / 2; i++) {
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const ep_h4 y = *(const ep_h4*)(smem + ym.off(lrow0 + 2 * i + h, (128 * j + 4 * s) * 2));
+            v[i][j] = ep_f4{(float)y[0], (float)y[1], (float)y[2], (float)y[3]};
+        }
+    }
+    if (FLAGS & (RG_RES | RG_GATE)) {
+#pragma unroll
+        for (int i = 0; i < R / 2; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const ep_f4 add = ep_f4{(float)o.add[i][j][0], (float)o.add[i][j][1], (float)o.add[i][j][2],
+                                        (float)o.add[i][j][3]};
+                if (FLAGS & RG_GATE) {   // x + fp16(gate * res)   (blocks.py:30, fp16 product)
+#pragma unroll
+                    for (int t = 0; t < 4; t++) v[i][j][t] = o.base[i][j][t] + hround(add[t] * v[i][j][t]);
+                } else {                 // (res32 + res16) + y
+                    v[i][j] = (o.base[i][j] + add) + v[i][j];
+                }
+            }
+    }
+    if (FLAGS & RG_LN) {
+#pragma unroll
+        for (int i = 0; i < R / 2; i++) {
+            float sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; j++) sm += (v[i][j][0] + v[i][j][1]) + (v[i][j][2] + v[i][j][3]);
+            const float mean = half_sum(sm) * (1.f / RG_BN);
+            float sq = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const ep_f4 d = v[i][j] - mean;
+                sq += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+            }
+            const float rstd = rsqrtf(half_sum(sq) * (1.f / RG_BN) + p.ln_eps);
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                v[i][j] = (v[i][j] - mean) * rstd * k.g[j] + k.b[j];
+                if (FLAGS & RG_LN_RELU)
+#pragma unroll
+                    for (int t = 0; t < 4; t++) v[i][j][t] = fmaxf(v[i][j][t], 0.f);
+            }
+        }
+    }
+    if (FLAGS & RG_HEADS) {
+        // d = W_d relu(v) + b_d ; w = sigmoid(W_w relu(v) + b_w)   (fp16 operands, fp32 accumulate)
+#pragma unroll
+        for (int i = 0; i < R / 2; i++) {
+            float d[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 3; j++)
+#pragma unroll
+                for (int t = 0; t < 4; t++) {
+                    const float x = hround(fmaxf(v[i][j][t], 0.f));
+#pragma unroll
+                    for (int q = 0; q < 4; q++) d[q] += x * k.hw[q][j][t];
+                }
+            half_t ho[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                float z = hround(half_sum(d[q]) + k.hb[q]);
+                if (q >= 2) z = hround(fast_sigmoid(z));
+                ho[q] = (half_t)z;
+            }
+            const int64_t row = row0 + 2 * i + h;
+            if (s == 0 && row < M) *(ep_h4*)((half_t*)p.head_out + row * 4) = ep_h4{ho[0], ho[1], ho[2], ho[3]};
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < R / 2; i++) {
+        const int64_t row = row0 + 2 * i + h;
+        if (row >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int c = 128 * j + 4 * s;
+            if (p.out32) *(ep_f4*)((float*)p.out32 + row * p.ldo32 + c) = v[i][j];
+            if (p.out16)
+                *(ep_h4*)((half_t*)p.out16 + row * p.ldo16 + c) =
+                    ep_h4{(half_t)v[i][j][0], (half_t)v[i][j][1], (half_t)v[i][j][2], (half_t)v[i][j][3]};
+        }
+    }
+}
+
+template <int FLAGS, int R, typename YMap>
+__device__ __forceinline__ void epilogue_rows2(const dpvo_rowgemm_args& p, int64_t M, const char* smem, YMap ym,
+                                               int lrow0, int64_t row0, int lane, const EpiConsts2& k)
+{
+    EpiOps2<R> o;
+    epi2_load<FLAGS, R>(p, M, row0, lane, o);
+    epi2_finish<FLAGS, R>(p, M, smem, ym, lrow0, row0, lane, k, o);
+}
+
 template <int FLAGS>
 __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm_kernel(dpvo_rowgemm_args p)
 {
@@ -668,8 +848,8 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_ar
         w_sw[nt] = (n >> 1) & 7;
     }
 
-    EpiConsts kc;
-    load_consts<FLAGS>(p, lane, kc);
+    EpiConsts2 kc;
+    load_consts2<FLAGS>(p, lane, kc);
     // prologue: A(0), W(0), A(1) -- then every step issues W(i+1), A(i+2)
     issue_a(0);
     issue_w(0);
@@ -748,12 +928,13 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_ar
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
-            constexpr int RB = (FLAGS & (RG_RES | RG_GATE | RG_LN)) ? 4 : 8;   // rows per batch (register budget)
+            // rows per batch (register budget: half of y16 is still live here)
+            constexpr int RB = (FLAGS & (RG_RES | RG_GATE | RG_LN)) ? ((FLAGS & (RG_LN | RG_HEADS)) ? 2 : 4) : 8;
             const int lr = wave * 8;                                             // 8 rows inside one 32-row block
             const int64_t row0 = cur_tile * RG_BM + (lr >> 5) * 64 + h * 32 + (lr & 31);
 #pragma unroll
             for (int q0 = 0; q0 < 8; q0 += RB)
-                epilogue_rows<FLAGS, RB>(pe, Mrows, smem, ym, lr + q0, row0 + q0, lane, kc);
+                epilogue_rows2<FLAGS, RB>(pe, Mrows, smem, ym, lr + q0, row0 + q0, lane, kc);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
@@ -1000,12 +1181,15 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         sync_lds();
         // LayerNorm / head constants loaded per tile, not held across the GEMMs
         // (the gated chain's gate already holds 48 VGPRs there)
-        EpiConsts kc;
-        load_consts<F2>(p, lane, kc);
+        EpiConsts2 kc;
+        load_consts2<F2>(p, lane, kc);
         constexpr int RB = (F2 & (RG_RES | RG_GATE | RG_LN)) ? 4 : 8;
+        dpvo_rowgemm_args pd = p;
+        if (DBG & 32) pd.out32 = pd.out16 = nullptr;   // timing experiment: no row stores
+        constexpr int FE = (DBG & 16) ? (F2 & ~RG_RES) : F2;   // timing experiment: no residual loads
 #pragma unroll 1
         for (int q0 = 0; q0 < 16 && !(DBG & 1); q0 += RB)   // one batch live at a time (register budget)
-            epilogue_rows<F2, RB>(p, Mrows, smem, ym, wave * 16 + q0, tile * RG_BM + wave * 16 + q0, lane, kc);
+            epilogue_rows2<FE, RB>(pd, Mrows, smem, ym, wave * 16 + q0, tile * RG_BM + wave * 16 + q0, lane, kc);
         sync_lds();
     }
 }
@@ -1659,7 +1843,7 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
         hipLaunchKernelGGL((rowchain_kernel<DPVO_RG_RES, false, (D)>), dim3(grid), dim3(RG_THREADS), 0,            \
                            as_stream(stream), *g1, a2, a2);                                                       \
         break;
-            RCD_CASE(0) RCD_CASE(1) RCD_CASE(2) RCD_CASE(3)
+            RCD_CASE(0) RCD_CASE(1) RCD_CASE(2) RCD_CASE(3) RCD_CASE(16) RCD_CASE(32) RCD_CASE(48)
 #undef RCD_CASE
         default:
             set_error("DPVO_RC_DBG: unsupported value");
