@@ -404,6 +404,46 @@ int dpvo_rowadd_ln(const dpvo_rowadd_args* args, void* stream);
 int dpvo_gather_rows(int in_dtype, const void* x, int64_t ldx, int64_t rows, const int64_t* idx, int64_t n, int D,
                      int out_dtype, void* out, void* stream);
 
+
+/* ---------------------------------------------------------------------------
+ * Frame ingest: the Patchifier's two BasicEncoder4 networks
+ * (dpvo/extractor.py:200-264, ResidualBlock :6-53, called from net.py:121-122;
+ * the reference runs them as ~100 cuDNN / ATen launches per frame).
+ * Activations fp16 NHWC.  Each convolution reads x = xform(a, r), the previous
+ * layer's output transformed on load:
+ *   xmode 0: x = a;  1: x = relu(IN(a));  2: x = relu(relu(IN(a)) + IN'(r))
+ * where IN(a) = a * a_ss[2c] + a_ss[2c+1] (identity when a_ss is NULL: norm
+ * 'none') and IN'(r) likewise with r_ss.  With part != NULL the launch also
+ * leaves the instance-norm pairs (rstd, -mean rstd) of its output in ss_out
+ * (per-tile partials in part [tiles][2 cout], reduced in a fixed order by the
+ * last tile; counter must start at 0 and is left at 0).
+ * enc[0..n_enc): up to two encoders (fnet, inet) of the same layer shape in one
+ * launch.  Weights fp16 [ks*ks][cin/32][cout][32]; the stem's [32][160]
+ * (3 x 7 x 7 taps, zero-padded). */
+typedef struct dpvo_conv_args {
+    const void* a; int64_t a_ps; int a_co;   /* input: pixel stride, channel offset (elements) */
+    const float* a_ss;
+    const void* r; int64_t r_ps; int r_co;   /* residual (xmode 2) */
+    const float* r_ss;
+    void* xout; int64_t x_ps;                /* x itself, written (stride-1 3x3 only) or NULL */
+    const void* w; const void* bias;         /* fp16 */
+    void* out; int64_t o_ps; int o_co; float out_scale;   /* out = fp16(fp16(conv + bias) * out_scale) */
+    float* part; unsigned* counter; float* ss_out; float eps;
+} dpvo_conv_args;
+/* number of 8 x 16 output tiles (the part buffer's rows) of a layer */
+int64_t dpvo_encoder_tiles(int Hi, int Wi, int ks, int stride);
+/* conv1 (7x7 s2 p3, 3 -> 32) on the uint8 frame [3][H][W] with 2 (x / 255) - 0.5
+ * (net.py:116) applied on load */
+int dpvo_encoder_stem(const uint8_t* image, int H, int W, const dpvo_conv_args* enc, int n_enc, void* stream);
+/* one layer: (ks, stride, cin -> cout) in {(3,1,32,32), (3,2,32,128: conv | 1x1
+ * downsample as the centre tap), (3,1,64,64), (1,1,64,128)}, xmode per layer */
+int dpvo_encoder_conv(int ks, int stride, int cin, int cout, int xmode, int Hi, int Wi, const dpvo_conv_args* enc,
+                      int n_enc, void* stream);
+/* the final 1x1 convolution (64 -> cout, xmode 2 input) at M pixels (x[m], y[m])
+ * only: out[m * o_ps + o_co + c]; w fp16 [cout][64] */
+int dpvo_encoder_head_at(const dpvo_conv_args* e, int cout, int Hi, int Wi, const int64_t* x, const int64_t* y,
+                         int64_t M, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

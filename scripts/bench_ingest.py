@@ -29,11 +29,22 @@ def main():
     pf = net.patchify
     img = torch.randint(0, 255, (3, 384, 512), device="cuda", dtype=torch.uint8).float()
     res = {}
+    img8 = img.to(torch.uint8)
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+        for native in (True, False):
+            pf.NATIVE_ENCODERS = native
+            tag = "native" if native else "torch"
+            pf.graphed = False
+            res[f"{tag}_eager_ms"] = timed(lambda: pf(img8, 96))
+            pf.graphed = True
+            res[f"{tag}_graph_ms"] = timed(lambda: pf(img8, 96))
+        import encoder_ops
+        enc = encoder_ops.NativeEncoders(pf.fnet, pf.inet)
+        xs = torch.randint(1, 127, (96,), device="cuda")
+        res["native_encoders_only_ms"] = timed(lambda: enc.run(img8, xs, xs % 95 + 1))
+        pf.NATIVE_ENCODERS = False
         pf.graphed = False
         res["eager_ms"] = timed(lambda: pf(img, 96))
-        pf.graphed = True
-        res["graph_ms"] = timed(lambda: pf(img, 96))
         x = 2 * (img[None, None] / 255.0) - 0.5
         res["fnet_eager_ms"] = timed(lambda: pf.fnet(x))
         res["inet_eager_ms"] = timed(lambda: pf.inet(x))

@@ -1,0 +1,27 @@
+"""Native encoders only (both networks, one 512x384 frame) x 20, for
+rocprofv3 --kernel-trace --stats."""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "wild-video-3d-reconstruction_amd")]
+import torch  # noqa: E402
+
+
+def main():
+    import encoder_ops
+    from dpvo.net import Patchifier
+    torch.manual_seed(0)
+    pf = Patchifier(3).cuda().eval()
+    img = torch.randint(0, 255, (3, 384, 512), device="cuda", dtype=torch.uint8)
+    enc = encoder_ops.NativeEncoders(pf.fnet, pf.inet)
+    xs = torch.randint(1, 127, (192,), device="cuda")
+    with torch.no_grad():
+        for _ in range(20):
+            enc.run(img, xs, xs % 95 + 1)
+    torch.cuda.synchronize()
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

@@ -193,14 +193,17 @@ def test_keyframe_raises_on_nan_pose_when_kept():
                     s.keyframe()
 
 
-def test_graphed_ingest_matches_eager():
+@pytest.mark.parametrize("native", [True, False])
+def test_graphed_ingest_matches_eager(native):
     """Patchifier.forward replayed from its captured HIP graph gives the eager
     launches' results bit for bit (same seed -> same patch centres), and each
-    call returns fresh tensors (the next replay does not overwrite them)."""
+    call returns fresh tensors (the next replay does not overwrite them);
+    native = the HIP encoders, else the torch modules."""
     from dpvo.net import Patchifier
     from dpvo.synthetic import image_stream
     torch.manual_seed(0)
     pf = Patchifier(3).cuda().eval()
+    pf.NATIVE_ENCODERS = native
     imgs = [img for _, img in image_stream(3)]
     with torch.no_grad(), torch.autocast("cuda", enabled=True):
         eager = []
@@ -219,7 +222,8 @@ def test_graphed_ingest_matches_eager():
     assert not torch.equal(graphed[0][3], graphed[1][3])  # fresh centres, not aliased outputs
 
 
-def test_graphed_ingest_recaptures_after_reassign():
+@pytest.mark.parametrize("native", [True, False])
+def test_graphed_ingest_recaptures_after_reassign(native):
     """The captured ingest graph holds raw parameter addresses: re-placing the
     parameters (load_state_dict(assign=True) with fresh storage, then
     scaling them) must re-capture, not replay reads of freed memory."""
@@ -227,6 +231,7 @@ def test_graphed_ingest_recaptures_after_reassign():
     from dpvo.synthetic import image_stream
     torch.manual_seed(0)
     pf = Patchifier(3).cuda().eval()
+    pf.NATIVE_ENCODERS = native
     img = next(iter(image_stream(1)))[1]
     with torch.no_grad(), torch.autocast("cuda", enabled=True):
         pf.graphed = True

@@ -177,6 +177,21 @@ class Patchifier(nn.Module):
         # False = the eager launches
         self.graphed = True
         self._graph = self._graph_key = None
+        self._native = None
+
+    # fp16-autocast inference runs both encoders on the HIP library
+    # (encoder_ops / csrc/encoder.hip); False = the modules' torch forward
+    NATIVE_ENCODERS = True
+
+    def _native_encoders(self):
+        if self._native is None:
+            import encoder_ops
+            self._native = encoder_ops.NativeEncoders(self.fnet, self.inet)
+        return self._native
+
+    def _use_native(self, amp_dtype):
+        return (self.NATIVE_ENCODERS and amp_dtype == torch.float16 and not torch.is_grad_enabled() and
+                self.fnet.norm_fn == "instance" and self.inet.norm_fn == "none")
 
     def _image_gradient(self, images):
         gray = ((images + 0.5) * (255.0 / 2)).sum(dim=2)
@@ -192,6 +207,13 @@ class Patchifier(nn.Module):
         if (self.graphed and not gradient_bias and mask is None and disps is None and images.is_cuda and images.dim() == 3
                 and not torch.is_grad_enabled()):
             return self._forward_graphed(images, patches_per_image, return_color)
+        amp = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else None
+        if (self._use_native(amp) and not gradient_bias and mask is None and disps is None and images.is_cuda and
+                images.dim() == 3):
+            x, y = self._draw_centres(images, patches_per_image)
+            fmap, gmap, imap, patches, clr = self._ingest(images, x, y, return_color, "native")
+            index = torch.zeros(patches_per_image, dtype=torch.long, device=images.device)
+            return (fmap, gmap, imap, patches, index) + ((clr,) if return_color else ())
         images = 2 * (images[None, None] / 255.0) - 0.5
         fmap = self.fnet(images) / 4.0
         imap = self.inet(images) / 4.0
@@ -220,16 +242,21 @@ class Patchifier(nn.Module):
             return fmap, gmap, imap, patches, index, clr
         return fmap, gmap, imap, patches, index
 
-    def _gather(self, images, fmap, imap, x, y, disps, return_color):
-        """the four altcorr.patchify gathers at the chosen centres (net.py:301-315)."""
+    def _gather(self, images, fmap, imap, x, y, disps, return_color, imap_at=None):
+        """the four altcorr.patchify gathers at the chosen centres (net.py:301-315).
+        imap_at: inet's output already evaluated at the centres (native encoders):
+        patchify(imap, coords, 0) at integer centres is that row exactly."""
         b, n, c, h, w = fmap.shape
         P = self.patch_size
         coords = torch.stack([x, y], dim=-1).float()
-        imap = altcorr.patchify(imap[0], coords, 0).view(b, -1, DIM, 1, 1)
+        if imap_at is not None:
+            imap = imap_at.float().view(b, -1, DIM, 1, 1)
+        else:
+            imap = altcorr.patchify(imap[0], coords, 0).view(b, -1, DIM, 1, 1)
         gmap = altcorr.patchify(fmap[0], coords, P // 2).view(b, -1, 128, P, P)
         clr = altcorr.patchify(images[0], 4 * (coords + 0.5), 0).view(b, -1, 3) if return_color else None
         if disps is None:
-            disps = torch.ones(b, n, h, w, device=images.device)
+            disps = torch.ones(b, n, h, w, device=fmap.device)
         grid, _ = coords_grid_with_index(disps, device=fmap.device)
         patches = altcorr.patchify(grid[0], coords, P // 2).view(b, -1, 3, P, P)
         return gmap, imap, patches, clr
@@ -237,7 +264,13 @@ class Patchifier(nn.Module):
     def _ingest(self, image, x, y, return_color, encoders=None):
         """forward() after the centre draw: fixed shapes, no host syncs -- the
         body of the captured graph.  encoders: (fnet, inet) to run instead of
-        the modules' own (the graph's fp16 copies)."""
+        the modules' own (the graph's fp16 copies), or "native": both networks
+        on the HIP library (encoder_ops, 11 launches), inet only at the centres."""
+        if encoders == "native":
+            images = 2 * (image[None, None] / 255.0) - 0.5 if return_color else None
+            fmap, imap_at = self._native_encoders().run(image, x, y)
+            gm, im, patches, clr = self._gather(images, fmap, None, x, y, None, return_color, imap_at=imap_at)
+            return fmap, gm, im, patches, clr
         fnet, inet = encoders or (self.fnet, self.inet)
         images = 2 * (image[None, None] / 255.0) - 0.5
         fmap = fnet(images) / 4.0
@@ -251,16 +284,14 @@ class Patchifier(nn.Module):
         no random numbers), so the results are identical to forward()'s; the
         graph reads them from static buffers.  Outputs are returned as clones:
         the next replay overwrites the graph's own."""
-        H, W = image.shape[-2:]
-        h, w = ((H + 1) // 2 + 1) // 2, ((W + 1) // 2 + 1) // 2  # conv1 (s2) then layer2 (s2)
         dev = image.device
-        x = torch.randint(1, w - 1, size=[1, M], device=dev)
-        y = torch.randint(1, h - 1, size=[1, M], device=dev)
+        x, y = self._draw_centres(image, M)
         amp = torch.is_autocast_enabled("cuda")
         # the captured kernels hold raw parameter / buffer addresses and the
         # autocast dtype: any re-placement (.to(), .half(), load_state_dict
-        # with assign=True) or a different autocast dtype re-captures
-        tensors = tuple(t.data_ptr() for t in self.parameters()) + tuple(t.data_ptr() for t in self.buffers())
+        # with assign=True), in-place update or a different autocast dtype re-captures
+        tensors = (tuple((t.data_ptr(), t._version) for t in self.parameters()) +
+                   tuple(t.data_ptr() for t in self.buffers()))
         key = (tuple(image.shape), image.dtype, M, bool(return_color), amp,
                torch.get_autocast_dtype("cuda") if amp else None, dev, tensors)
         if self._graph_key != key:
@@ -275,6 +306,15 @@ class Patchifier(nn.Module):
             return fmap, gmap, imap, patches, index, clr
         return fmap, gmap, imap, patches, index
 
+    @staticmethod
+    def _draw_centres(image, M):
+        """the default centre draw of forward() (net.py:292-294), on the stride-4 map"""
+        H, W = image.shape[-2:]
+        h, w = ((H + 1) // 2 + 1) // 2, ((W + 1) // 2 + 1) // 2  # conv1 (s2) then layer2 (s2)
+        x = torch.randint(1, w - 1, size=[1, M], device=image.device)
+        y = torch.randint(1, h - 1, size=[1, M], device=image.device)
+        return x, y
+
     def _capture(self, image, x, y, return_color, amp, key):
         self._graph = self._graph_key = None
         static = (image.clone(), x.clone(), y.clone())
@@ -287,7 +327,9 @@ class Patchifier(nn.Module):
         # already in that dtype -- the same values the casts produce, so the
         # same convolutions (bit-identical to the eager path, test_gpu_tracker)
         enc = None
-        if amp:
+        if amp and self._use_native(dt):
+            enc = "native"
+        elif amp:
             enc = tuple(copy.deepcopy(m).to(dt) for m in (self.fnet, self.inet))
         with torch.cuda.stream(side), torch.autocast("cuda", dtype=dt, enabled=amp, cache_enabled=False):
             for _ in range(2):  # warm-up: MIOpen solver selection, allocator pools
