@@ -412,23 +412,25 @@ int dpvo_gather_rows(int in_dtype, const void* x, int64_t ldx, int64_t rows, con
  * Activations fp16 NHWC.  Each convolution reads x = xform(a, r), the previous
  * layer's output transformed on load:
  *   xmode 0: x = a;  1: x = relu(IN(a));  2: x = relu(relu(IN(a)) + IN'(r))
- * where IN(a) = a * a_ss[2c] + a_ss[2c+1] (identity when a_ss is NULL: norm
- * 'none') and IN'(r) likewise with r_ss.  With part != NULL the launch also
- * leaves the instance-norm pairs (rstd, -mean rstd) of its output in ss_out
- * (per-tile partials in part [tiles][2 cout], reduced in a fixed order by the
- * last tile; counter must start at 0 and is left at 0).
+ * where IN(a) = (a - mean) * rstd over the Hi x Wi input pixels (instance
+ * norm, affine-free), from a_st: the producing launch's per-tile partials
+ * [a_st_tiles][a_st_ld] floats, (sum, sumsq) of channel c at 2 (a_co + c);
+ * a_st NULL = no norm ('none').  IN'(r) likewise from r_st.  With part != NULL
+ * the launch writes its own output's partials, part[tile][2 cout] -- the next
+ * layer's a_st.  Every consumer reduces the partials itself, in a fixed order.
  * enc[0..n_enc): up to two encoders (fnet, inet) of the same layer shape in one
- * launch.  Weights fp16 [ks*ks][cin/32][cout][32]; the stem's [32][160]
- * (3 x 7 x 7 taps, zero-padded). */
+ * launch.  Weights fp16 [ks*ks][cin/32][cout][32] and the stem's
+ * [5][32][32] (3 x 7 x 7 taps, zero-padded to 160), each 32-wide row's four
+ * 8-value chunks XOR-swizzled by (row >> 2) & 3. */
 typedef struct dpvo_conv_args {
     const void* a; int64_t a_ps; int a_co;   /* input: pixel stride, channel offset (elements) */
-    const float* a_ss;
+    const float* a_st; int a_st_tiles; int a_st_ld;
     const void* r; int64_t r_ps; int r_co;   /* residual (xmode 2) */
-    const float* r_ss;
+    const float* r_st; int r_st_tiles; int r_st_ld;
     void* xout; int64_t x_ps;                /* x itself, written (stride-1 3x3 only) or NULL */
     const void* w; const void* bias;         /* fp16 */
     void* out; int64_t o_ps; int o_co; float out_scale;   /* out = fp16(fp16(conv + bias) * out_scale) */
-    float* part; unsigned* counter; float* ss_out; float eps;
+    float* part; float eps;
 } dpvo_conv_args;
 /* number of 8 x 16 output tiles (the part buffer's rows) of a layer */
 int64_t dpvo_encoder_tiles(int Hi, int Wi, int ks, int stride);

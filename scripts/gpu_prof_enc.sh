@@ -11,7 +11,10 @@ rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 cd $R; f=$(find gpurun_out/prof_$T -name "*kernel_stats.csv" | head -1)
 python - "$f" "${KPAT:-enc_}" <<'PY'
 import csv, sys
+tot = 0
 for r in csv.DictReader(open(sys.argv[1])):
+    tot += float(r["TotalDurationNs"])
     if sys.argv[2] in r["Name"]:
         print(r["Name"][:100], r["Calls"], r["AverageNs"])
+print(f"all kernels: {tot / 1e3:.1f} us in total")
 PY

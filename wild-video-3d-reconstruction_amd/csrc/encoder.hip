@@ -16,11 +16,13 @@
 //    ReLU and the residual add of a ResidualBlock are applied when the NEXT
 //    convolution loads its input (x = relu(relu(IN(y)) + res)); the convolution
 //    that first reads a block output also writes it (the residual of the next
-//    block).  Instance-norm statistics are per-workgroup partial sums in the
-//    producing epilogue; the last workgroup to finish (one device-scope
-//    counter) reduces them in a fixed order (fp64) and leaves the per-channel
-//    (rstd, -mean rstd) pairs for the consumer -- deterministic, no extra
-//    launch.
+//    block).  Instance-norm statistics: each producing workgroup writes its
+//    tile's per-channel (sum, sum of squares); every consuming workgroup
+//    reduces all tiles' partials itself, in one fixed order (fp64), while its
+//    weight DMA is in flight.  No cross-workgroup synchronisation, no extra
+//    launch, identical (rstd, -mean rstd) in every workgroup, deterministic.
+//    (A last-workgroup-reduces scheme measured 19 us more per layer: the
+//    device-scope counter and release fences serialise the 768 workgroups.)
 //  * Both encoders run in the same launches (blockIdx.y = encoder: fnet with
 //    instance norm, inet with none), so every launch has twice the workgroups.
 //  * The inet's final 1x1 convolution (64 -> 384) is evaluated only at the
@@ -38,7 +40,6 @@ typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
 typedef float f4_t __attribute__((ext_vector_type(4)));
 
 constexpr int EN_TH = 8, EN_TW = 16, EN_THREADS = 256;
-constexpr int EN_WROW = 40;   // LDS weight row: 32 K halves + 8 pad (conflict-free 16-B reads)
 
 struct EncBatch {
     dpvo_conv_args e[2];
@@ -46,6 +47,18 @@ struct EncBatch {
 };
 
 __device__ __forceinline__ h8_t load_h8(const half_t* p) { return *(const h8_t*)p; }
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+// global -> LDS DMA: lane l's 16 bytes land at lds_base + 16 l
+__device__ __forceinline__ void wlds16(const void* src, char* lds_base)
+{
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_base, 16, 0, 0);
+}
+// weight row r (32 K halves, 64 B) in LDS: its four 16-byte chunks are stored
+// XOR-swizzled by (r >> 2) & 3 (encoder_ops.pack_conv does the swizzle), so
+// the 16 rows of an MFMA operand read hit 16 distinct bank groups
+__device__ __forceinline__ int wrow(int r, int chunk) { return r * 32 + 8 * (chunk ^ ((r >> 2) & 3)); }
 
 // x = relu(IN(a)) [+ res, relu]  for 8 channels (XMODE 1 / 2); XMODE 0: x = a
 template <int XMODE>
@@ -69,10 +82,10 @@ __device__ __forceinline__ h8_t xform(h8_t a, const float (&as)[16], bool a_norm
 }
 
 // acc (+ bias) -> fp16 -> out; instance-norm partial sums of the stored
-// values -> part[tile]; the last tile reduces them into ss_out.
+// values -> part[tile] (sum, sumsq interleaved per channel).
 template <int COUT>
 __device__ void conv_epilogue(const dpvo_conv_args& e, f4_t (&acc)[2][COUT / 16], int Ho, int Wo, int oy0, int ox0,
-                              int tile, int ntiles, float (*sred)[2 * COUT], double* dred, int* flag)
+                              int tile, float (*sred)[2 * COUT])
 {
     constexpr int NT = COUT / 16;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fq = lane >> 4;
@@ -118,59 +131,57 @@ __device__ void conv_epilogue(const dpvo_conv_args& e, f4_t (&acc)[2][COUT / 16]
             }
         }
     __syncthreads();
-    constexpr int V = 2 * COUT;   // (sum, sumsq) interleaved per channel
+    constexpr int V = 2 * COUT;
     for (int t = tid; t < V; t += EN_THREADS)
         e.part[(int64_t)tile * V + t] = ((sred[0][t] + sred[1][t]) + sred[2][t]) + sred[3][t];
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) *flag = atomicAdd(e.counter, 1u) == (unsigned)(ntiles - 1);
-    __syncthreads();
-    if (!*flag) return;
-    // last workgroup: fixed-order fp64 reduction of every tile's partials.
-    // Thread t owns the float4 quad t % (V/4) of tiles t / (V/4) + SL i: its
-    // loads are independent and issued 8 at a time (one L2 round trip per 8
-    // tiles, not per tile); the SL slices are then summed in slice order.
-    __threadfence();
-    constexpr int Q4 = V / 4, SL = EN_THREADS / Q4;
-    {
-        const int q = tid % Q4, s = tid / Q4;
-        const float4* P = (const float4*)e.part;
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-        for (int g0 = s; g0 < ntiles; g0 += 8 * SL) {
-            float4 v[8];
+}
+
+// Instance-norm pairs (rstd, -mean rstd) of C channels [co, co + C) of a
+// producer's output from its per-tile partials (st: [tiles][ld] floats, (sum,
+// sumsq) per channel) over n pixels -> ss[2 C] in LDS.  Thread t sums the
+// quad t % (2C/4) of tiles t / (2C/4) + SL i (loads issued B tiles at a time),
+// the SL slices are summed in slice order: the same fixed order in every
+// workgroup.  Ends with a barrier.
+template <int C>
+__device__ void reduce_stats(const float* st, int tiles, int ld, int co, double n, float eps, float* ss, double* dred)
+{
+    constexpr int V = 2 * C, Q4 = V / 4, SL = EN_THREADS / Q4;
+    const int tid = threadIdx.x, q = tid % Q4, s = tid / Q4;
+    const float* base = st + 2 * co + 4 * q;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    constexpr int B = 8;   // tiles per thread per batch
+    for (int g0 = s; g0 < tiles; g0 += B * SL) {
+        float4 v[B];
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int g = g0 + u * SL;
-                v[u] = g < ntiles ? P[(int64_t)g * Q4 + q] : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                a0 += (double)v[u].x;
-                a1 += (double)v[u].y;
-                a2 += (double)v[u].z;
-                a3 += (double)v[u].w;
-            }
+        for (int u = 0; u < B; u++) {
+            const int g = g0 + u * SL;
+            v[u] = g < tiles ? *(const float4*)(base + (int64_t)g * ld) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        dred[s * V + 4 * q + 0] = a0;
-        dred[s * V + 4 * q + 1] = a1;
-        dred[s * V + 4 * q + 2] = a2;
-        dred[s * V + 4 * q + 3] = a3;
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            a[0] += (double)v[u].x;
+            a[1] += (double)v[u].y;
+            a[2] += (double)v[u].z;
+            a[3] += (double)v[u].w;
+        }
     }
+#pragma unroll
+    for (int c = 0; c < 4; c++) dred[s * V + 4 * q + c] = a[c];
     __syncthreads();
-    if (tid < COUT) {
+    if (tid < C) {
         double S = 0.0, Q = 0.0;
-        for (int s = 0; s < SL; s++) {
-            S += dred[s * V + 2 * tid];
-            Q += dred[s * V + 2 * tid + 1];
+        for (int k = 0; k < SL; k++) {
+            S += dred[k * V + 2 * tid];
+            Q += dred[k * V + 2 * tid + 1];
         }
-        const double n = (double)Ho * Wo, mean = S / n;
+        const double mean = S / n;
         double var = Q / n - mean * mean;
         var = var > 0.0 ? var : 0.0;
-        const float rstd = 1.f / sqrtf((float)var + e.eps);
-        e.ss_out[2 * tid] = rstd;
-        e.ss_out[2 * tid + 1] = (float)(-mean) * rstd;
+        const float rstd = 1.f / sqrtf((float)var + eps);
+        ss[2 * tid] = rstd;
+        ss[2 * tid + 1] = (float)(-mean) * rstd;
     }
-    if (tid == 0) *e.counter = 0u;   // ready for the next frame (and graph replays)
+    __syncthreads();
 }
 
 // 3x3 (pad 1) or 1x1 (pad 0) convolution, stride S, CIN -> COUT channels, over
@@ -183,57 +194,72 @@ __global__ __launch_bounds__(EN_THREADS) void enc_conv_kernel(EncBatch p)
 {
     constexpr int PAD = KS / 2, IH = (EN_TH - 1) * S + KS, IW = (EN_TW - 1) * S + KS;
     constexpr int CP = CIN + 8, KC = CIN / 32, NT = COUT / 16, TAPS = KS * KS;
-    __shared__ __attribute__((aligned(16))) half_t sW[TAPS * KC * COUT * EN_WROW];
+    __shared__ __attribute__((aligned(16))) half_t sW[TAPS * KC * COUT * 32];
     __shared__ __attribute__((aligned(16))) half_t sX[IH * IW * CP];
     __shared__ float sred[4][2 * COUT];
     __shared__ double dred[4 * EN_THREADS];
-    __shared__ int flag;
+    __shared__ float sss[2][2 * CIN];
 
     const dpvo_conv_args& e = p.e[blockIdx.y];
     const int tile = blockIdx.x;
     const int oy0 = (tile / p.tiles_x) * EN_TH, ox0 = (tile % p.tiles_x) * EN_TW;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fq = lane >> 4;
 
-    // weights: global [tap][kc][co][32] -> LDS rows of 40 halves
+    // Every global read of the prologue is in flight before the first is
+    // used: the weights go global -> LDS by DMA (1 KB per wave instruction;
+    // the host packs them pre-swizzled, see wrow()), the halo loads fill a
+    // fully unrolled register batch.
     {
-        const half_t* w = (const half_t*)e.w;
-        constexpr int CH = TAPS * KC * COUT * 4;
-        for (int c = tid; c < CH; c += EN_THREADS)
-            *(h8_t*)(sW + (c >> 2) * EN_WROW + (c & 3) * 8) = load_h8(w + (int64_t)c * 8);
+        constexpr int NP = TAPS * KC * COUT / 16;   // 1 KB pieces
+        const char* w = (const char*)e.w;
+        for (int pc = wave; pc < NP; pc += 4) wlds16(w + pc * 1024 + lane * 16, (char*)sW + pc * 1024);
     }
-    // input halo, transformed on load (zero outside the map: the conv pads x)
-    {
-        constexpr int CJ = CIN / 8;   // 16-byte chunks per pixel; tid % CJ is fixed per thread
-        const int j = tid % CJ;
-        float as[16], rs[16];
-        const bool a_norm = XMODE != 0 && e.a_ss != nullptr, r_norm = XMODE == 2 && e.r_ss != nullptr;
+    // instance-norm pairs of the input (and residual): reduced while the
+    // weight DMA is in flight, before the halo batch occupies registers
+    const bool a_norm = XMODE != 0 && e.a_st != nullptr, r_norm = XMODE == 2 && e.r_st != nullptr;
+    const double n_in = (double)p.Hi * p.Wi;
+    if (a_norm) reduce_stats<CIN>(e.a_st, e.a_st_tiles, e.a_st_ld, e.a_co, n_in, e.eps, sss[0], dred);
+    if (r_norm) reduce_stats<CIN>(e.r_st, e.r_st_tiles, e.r_st_ld, e.r_co, n_in, e.eps, sss[1], dred);
+    constexpr int CJ = CIN / 8;                   // 16-byte chunks per pixel; tid % CJ is fixed per thread
+    constexpr int NX = (IH * IW * CJ + EN_THREADS - 1) / EN_THREADS;
+    const int j = tid % CJ;
+    const int gy0 = oy0 * S - PAD, gx0 = ox0 * S - PAD;
+    const half_t* A = (const half_t*)e.a;
+    const half_t* R = (const half_t*)e.r;
+    h8_t va[NX], vr[XMODE == 2 ? NX : 1];
 #pragma unroll
-        for (int c = 0; c < 16; c++) {
-            as[c] = a_norm ? e.a_ss[16 * j + c] : 0.f;
-            rs[c] = r_norm ? e.r_ss[16 * j + c] : 0.f;
-        }
-        const half_t* A = (const half_t*)e.a;
-        const half_t* R = (const half_t*)e.r;
+    for (int u = 0; u < NX; u++) {
+        const int it = tid + u * EN_THREADS, q = it / CJ;
+        const int gy = gy0 + q / IW, gx = gx0 + q % IW;
+        const bool ok = it < IH * IW * CJ && gy >= 0 && gy < p.Hi && gx >= 0 && gx < p.Wi;
+        const int64_t pix = ok ? (int64_t)gy * p.Wi + gx : 0;
+        va[u] = ok ? load_h8(A + pix * e.a_ps + e.a_co + 8 * j) : (h8_t)(half_t)0;
+        if (XMODE == 2) vr[u] = ok ? load_h8(R + pix * e.r_ps + e.r_co + 8 * j) : (h8_t)(half_t)0;
+    }
+    float as[16], rs[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        as[c] = a_norm ? sss[0][16 * j + c] : 0.f;
+        rs[c] = r_norm ? sss[1][16 * j + c] : 0.f;
+    }
+    {
         half_t* X = (half_t*)e.xout;
-        const int gy0 = oy0 * S - PAD, gx0 = ox0 * S - PAD;
-        for (int it = tid; it < IH * IW * CJ; it += EN_THREADS) {
-            const int q = it / CJ, qy = q / IW, qx = q % IW;
+#pragma unroll
+        for (int u = 0; u < NX; u++) {
+            const int it = tid + u * EN_THREADS, q = it / CJ, qy = q / IW, qx = q % IW;
+            if (it >= IH * IW * CJ) break;
             const int gy = gy0 + qy, gx = gx0 + qx;
+            const bool ok = gy >= 0 && gy < p.Hi && gx >= 0 && gx < p.Wi;
             h8_t v = (h8_t)(half_t)0;
-            if (gy >= 0 && gy < p.Hi && gx >= 0 && gx < p.Wi) {
-                const int64_t pix = (int64_t)gy * p.Wi + gx;
-                const h8_t a = load_h8(A + pix * e.a_ps + e.a_co + 8 * j);
-                h8_t r = (h8_t)(half_t)0;
-                if (XMODE == 2) r = load_h8(R + pix * e.r_ps + e.r_co + 8 * j);
-                v = xform<XMODE>(a, as, a_norm, r, rs, r_norm);
-                // the block output this conv reads is the next block's residual:
-                // written once, by the tile whose interior holds the pixel
-                if (S == 1 && X != nullptr && qy >= PAD && qy < PAD + EN_TH && qx >= PAD && qx < PAD + EN_TW)
-                    *(h8_t*)(X + pix * e.x_ps + 8 * j) = v;
-            }
+            if (ok) v = xform<XMODE>(va[u], as, a_norm, XMODE == 2 ? vr[u] : va[u], rs, r_norm);
+            // the block output this conv reads is the next block's residual:
+            // written once, by the tile whose interior holds the pixel
+            if (S == 1 && X != nullptr && ok && qy >= PAD && qy < PAD + EN_TH && qx >= PAD && qx < PAD + EN_TW)
+                *(h8_t*)(X + ((int64_t)gy * p.Wi + gx) * e.x_ps + 8 * j) = v;
             *(h8_t*)(sX + q * CP + 8 * j) = v;
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the weight DMA
     __syncthreads();
 
     f4_t acc[2][NT];
@@ -256,13 +282,13 @@ __global__ __launch_bounds__(EN_THREADS) void enc_conv_kernel(EncBatch p)
 #pragma unroll
             for (int mt = 0; mt < NT; mt++) {
                 if (DS && mt >= NT / 2 && tap != TAPS / 2) continue;   // downsample: centre tap only
-                const h8_t wa = *(const h8_t*)(sW + ((tap * KC + kc) * COUT + mt * 16 + px) * EN_WROW + 8 * fq);
+                const h8_t wa = *(const h8_t*)(sW + wrow((tap * KC + kc) * COUT + mt * 16 + px, fq));
 #pragma unroll
                 for (int i = 0; i < 2; i++) acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa, bx[i], acc[i][mt], 0, 0, 0);
             }
         }
     }
-    conv_epilogue<COUT>(e, acc, p.Ho, p.Wo, oy0, ox0, tile, p.ntiles, sred, dred, &flag);
+    conv_epilogue<COUT>(e, acc, p.Ho, p.Wo, oy0, ox0, tile, sred);
 }
 
 // conv1 of BasicEncoder4 (7x7, stride 2, pad 3, 3 -> 32) on the uint8 frame,
@@ -271,45 +297,62 @@ __global__ __launch_bounds__(EN_THREADS) void enc_conv_kernel(EncBatch p)
 // 160 (five 32-wide chunks), im2col in LDS.
 constexpr int ST_K = 160, ST_KP = 168, ST_IH = 2 * (EN_TH - 1) + 7, ST_IW = 2 * (EN_TW - 1) + 7;
 
+template <int K0>   // im2col of K entries [K0, K0 + 80) of one output pixel (offsets compile-time)
+__device__ __forceinline__ void stem_im2col(const half_t* sI, int py, int px, half_t* dst)
+{
+    const half_t* src = sI + 2 * py * ST_IW + 2 * px;
+#pragma unroll
+    for (int g = 0; g < 80; g += 8) {
+        h8_t v;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const int k = K0 + g + i;
+            v[i] = k < 147 ? src[(k / 49) * ST_IH * ST_IW + ((k % 49) / 7) * ST_IW + k % 7] : (half_t)0;
+        }
+        *(h8_t*)(dst + K0 + g) = v;
+    }
+}
+
 __global__ __launch_bounds__(EN_THREADS) void enc_stem_kernel(EncBatch p, const uint8_t* image)
 {
     __shared__ __attribute__((aligned(16))) half_t sA[EN_TH * EN_TW * ST_KP];
-    __shared__ __attribute__((aligned(16))) half_t sW[32 * ST_KP];
+    __shared__ __attribute__((aligned(16))) half_t sW[32 * ST_K];
     __shared__ half_t sI[3 * ST_IH * ST_IW];
     __shared__ float sred[4][64];
-    __shared__ double dred[4 * EN_THREADS];
-    __shared__ int flag;
 
     const dpvo_conv_args& e = p.e[blockIdx.y];
     const int tile = blockIdx.x;
     const int oy0 = (tile / p.tiles_x) * EN_TH, ox0 = (tile % p.tiles_x) * EN_TW;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, fq = lane >> 4;
-    {
-        const half_t* w = (const half_t*)e.w;
-        for (int c = tid; c < 32 * ST_K / 8; c += EN_THREADS)
-            *(h8_t*)(sW + (c / (ST_K / 8)) * ST_KP + (c % (ST_K / 8)) * 8) = load_h8(w + (int64_t)c * 8);
-    }
+    // weights [5 chunks][32 rows][32] (wrow-swizzled): 10 KB by DMA
+    for (int pc = wave; pc < 32 * ST_K / 512; pc += 4)
+        wlds16((const char*)e.w + pc * 1024 + lane * 16, (char*)sW + pc * 1024);
+    // the 3 x 21 x 37 input window: every byte load in flight, then converted
+    constexpr int NI = 3 * ST_IH * ST_IW, NB = (NI + EN_THREADS - 1) / EN_THREADS;
     const int gy0 = 2 * oy0 - 3, gx0 = 2 * ox0 - 3;
-    for (int it = tid; it < 3 * ST_IH * ST_IW; it += EN_THREADS) {
-        const int c = it / (ST_IH * ST_IW), q = it % (ST_IH * ST_IW);
+    uint8_t b[NB];
+#pragma unroll
+    for (int u = 0; u < NB; u++) {
+        const int it = tid + u * EN_THREADS, c = it / (ST_IH * ST_IW), q = it % (ST_IH * ST_IW);
         const int gy = gy0 + q / ST_IW, gx = gx0 + q % ST_IW;
-        half_t v = (half_t)0;
-        if (gy >= 0 && gy < p.Hi && gx >= 0 && gx < p.Wi) {
-            const float u = (float)image[((int64_t)c * p.Hi + gy) * p.Wi + gx];
-            v = (half_t)(2.f * (u / 255.f) - 0.5f);
-        }
-        sI[it] = v;
+        const bool ok = it < NI && gy >= 0 && gy < p.Hi && gx >= 0 && gx < p.Wi;
+        b[u] = ok ? image[((int64_t)c * p.Hi + gy) * p.Wi + gx] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < NB; u++) {
+        const int it = tid + u * EN_THREADS, q = it % (ST_IH * ST_IW);
+        if (it >= NI) break;
+        const int gy = gy0 + q / ST_IW, gx = gx0 + q % ST_IW;
+        const bool ok = gy >= 0 && gy < p.Hi && gx >= 0 && gx < p.Wi;
+        sI[it] = ok ? (half_t)(2.f * ((float)b[u] / 255.f) - 0.5f) : (half_t)0;
     }
     __syncthreads();
-    for (int it = tid; it < EN_TH * EN_TW * ST_K; it += EN_THREADS) {
-        const int pix = it / ST_K, k = it % ST_K;
-        half_t v = (half_t)0;
-        if (k < 147) {
-            const int c = k / 49, ky = (k % 49) / 7, kx = k % 7;
-            v = sI[(c * ST_IH + 2 * (pix / EN_TW) + ky) * ST_IW + 2 * (pix % EN_TW) + kx];
-        }
-        sA[pix * ST_KP + k] = v;
+    {
+        const int pix = tid & 127;
+        if (tid < 128) stem_im2col<0>(sI, pix / EN_TW, pix % EN_TW, sA + pix * ST_KP);
+        else stem_im2col<80>(sI, pix / EN_TW, pix % EN_TW, sA + pix * ST_KP);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the weight DMA
     __syncthreads();
     f4_t acc[2][2];
 #pragma unroll
@@ -324,12 +367,12 @@ __global__ __launch_bounds__(EN_THREADS) void enc_stem_kernel(EncBatch p, const 
         for (int i = 0; i < 2; i++) bx[i] = *(const h8_t*)(sA + ((2 * wave + i) * EN_TW + px) * ST_KP + kc * 32 + 8 * fq);
 #pragma unroll
         for (int mt = 0; mt < 2; mt++) {
-            const h8_t wa = *(const h8_t*)(sW + (mt * 16 + px) * ST_KP + kc * 32 + 8 * fq);
+            const h8_t wa = *(const h8_t*)(sW + wrow(kc * 32 + mt * 16 + px, fq));
 #pragma unroll
             for (int i = 0; i < 2; i++) acc[i][mt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa, bx[i], acc[i][mt], 0, 0, 0);
         }
     }
-    conv_epilogue<32>(e, acc, p.Ho, p.Wo, oy0, ox0, tile, p.ntiles, sred, dred, &flag);
+    conv_epilogue<32>(e, acc, p.Ho, p.Wo, oy0, ox0, tile, sred);
 }
 
 // The final 1x1 convolution (64 -> cout) at given pixels only: out[m] =
@@ -339,19 +382,23 @@ __global__ __launch_bounds__(EN_THREADS) void enc_head_at_kernel(dpvo_conv_args 
                                                                  const int64_t* xs, const int64_t* ys, int64_t M)
 {
     __shared__ float sx[64];
+    __shared__ double dred[4 * EN_THREADS];
+    __shared__ float sss[2][128];
     const int64_t m = blockIdx.x;
     if (m >= M) return;
     const int tid = threadIdx.x;
     const int64_t yy = ys[m], xx = xs[m];
+    if (e.a_st) reduce_stats<64>(e.a_st, e.a_st_tiles, e.a_st_ld, e.a_co, (double)Hi * Wi, e.eps, sss[0], dred);
+    if (e.r_st) reduce_stats<64>(e.r_st, e.r_st_tiles, e.r_st_ld, e.r_co, (double)Hi * Wi, e.eps, sss[1], dred);
     if (tid < 64) {
         float v = 0.f;
         if (yy >= 0 && yy < Hi && xx >= 0 && xx < Wi) {
             const int64_t pix = yy * Wi + xx;
             half_t a = ((const half_t*)e.a)[pix * e.a_ps + e.a_co + tid];
-            if (e.a_ss) a = (half_t)((float)a * e.a_ss[2 * tid] + e.a_ss[2 * tid + 1]);
+            if (e.a_st) a = (half_t)((float)a * sss[0][2 * tid] + sss[0][2 * tid + 1]);
             a = a > (half_t)0 ? a : (half_t)0;
             half_t r = ((const half_t*)e.r)[pix * e.r_ps + e.r_co + tid];
-            if (e.r_ss) r = (half_t)((float)r * e.r_ss[2 * tid] + e.r_ss[2 * tid + 1]);
+            if (e.r_st) r = (half_t)((float)r * sss[1][2 * tid] + sss[1][2 * tid + 1]);
             half_t s = (half_t)((float)a + (float)r);
             v = s > (half_t)0 ? (float)s : 0.f;
         }
@@ -391,7 +438,10 @@ int fill_batch(EncBatch& b, const dpvo_conv_args* enc, int n_enc, int Hi, int Wi
     b.ntiles = b.tiles_x * ((b.Ho + EN_TH - 1) / EN_TH);
     for (int i = 0; i < n_enc; i++) {
         DPVO_CHECK_ARG(enc[i].w && enc[i].bias && enc[i].out, "w, bias and out are required");
-        DPVO_CHECK_ARG(!enc[i].part || (enc[i].counter && enc[i].ss_out), "statistics need counter and ss_out");
+        DPVO_CHECK_ARG(!enc[i].a_st || (enc[i].a_st_tiles > 0 && enc[i].a_st_ld % 4 == 0 && enc[i].a_co % 8 == 0),
+                       "a_st: tiles > 0, row length a multiple of 4");
+        DPVO_CHECK_ARG(!enc[i].r_st || (enc[i].r_st_tiles > 0 && enc[i].r_st_ld % 4 == 0 && enc[i].r_co % 8 == 0),
+                       "r_st: tiles > 0, row length a multiple of 4");
         DPVO_CHECK_ARG(((uintptr_t)enc[i].out & 7) == 0 && enc[i].o_ps % 4 == 0 && enc[i].o_co % 4 == 0,
                        "out must allow 8-byte stores");
     }
