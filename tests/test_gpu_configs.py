@@ -292,3 +292,46 @@ def test_mfma_corr_drift_on_outputs():
     per_element(pa, pb, what="window poses (mfma vs exact corr)")
     per_element(da, db, what="inverse depths (mfma vs exact corr)")
     assert drift["points_norm"] < 1e-3
+
+
+def test_c1_demo_plumbing(tmp_path):
+    """C1 (BASELINE.json configs[0]): dpvo_demo.py's plumbing -- default.yaml
+    (M=384), a 64-frame buffer, 64 synthetic 512x384 frames with
+    calib/tartan.txt's intrinsics (dpvo_demo.py:63-141) -- then the demo's
+    outputs: TUM trajectory, PLY point cloud and COLMAP text model
+    (dpvo_demo.py:129-135,187-205).  The reference runs this on CPU torch; the
+    MI355X build has no CPU path, so it runs the same plumbing on the GPU."""
+    from dpvo import io
+    from dpvo.config import make_cfg
+    from dpvo.dpvo import DPVO
+    from dpvo.net import VONet
+    from dpvo.synthetic import image_stream
+    torch.manual_seed(0)
+    net = VONet()
+    with torch.no_grad():
+        net.update.d[1].weight.mul_(40.0)  # random weights: make the motion probe pass
+    cfg = make_cfg("default", BUFFER_SIZE=64)
+    assert cfg.PATCHES_PER_FRAME == 384
+    fx, fy, cx, cy = 320.0, 320.0, 320.0, 240.0   # calib/tartan.txt
+    intr = torch.tensor([fx, fy, cx, cy], device="cuda")
+    with torch.no_grad():
+        slam = DPVO(cfg, net, ht=384, wd=512)
+        for t, img in image_stream(64):
+            slam(t, img, None, None, intr)
+        points, colors, _ = slam.get_pts_clr_intri()
+        poses, tstamps = slam.terminate()
+    assert poses.shape == (64, 7) and np.isfinite(poses).all() and len(tstamps) == 64
+    assert np.isfinite(points).all() and len(points) == len(colors) > 0
+    traj = io.PoseTrajectory3D.from_dpvo(poses, tstamps)
+    io.save_trajectory_tum_format(traj, tmp_path / "traj.txt")
+    rows = np.loadtxt(tmp_path / "traj.txt")
+    assert rows.shape == (64, 8)
+    np.testing.assert_allclose(rows[:, 1:], poses[:, [0, 1, 2, 3, 4, 5, 6]], rtol=1e-6, atol=1e-6)
+    io.save_ply(tmp_path / "points.ply", points, colors)
+    p2, c2 = io.load_ply(tmp_path / "points.ply")
+    np.testing.assert_allclose(p2, points, rtol=1e-6, atol=1e-6)
+    io.save_output_for_COLMAP(tmp_path / "colmap", tstamps, traj, points, colors / 255.0, False, fx, fy, cx, cy,
+                              H=384, W=512)
+    imgs = [ln for ln in (tmp_path / "colmap" / "images.txt").read_text().splitlines() if ln.strip()]
+    assert len(imgs) == 64
+    assert len((tmp_path / "colmap" / "points3D.txt").read_text().splitlines()) == len(points)
