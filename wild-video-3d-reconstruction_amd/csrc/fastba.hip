@@ -26,6 +26,8 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace dpvo {
@@ -1562,7 +1564,17 @@ static size_t nb_sort_temp_bytes(int64_t E)
 constexpr int BD_NMAX = 12;
 constexpr int BD_N6MAX = 6 * BD_NMAX;     // 72
 constexpr int BD_WAVES = 4;
-constexpr int BD_GRID = 1024;   // 4 waves each: 4096 waves, enough to hide the per-patch load chains
+constexpr int BD_GRID = 512;    // 4 waves each (measured over 256-2048: 512 is fastest at C3 and C2, scripts/exp_bd_grid.sh)
+constexpr int BD_GRID_MAX = 2048;   // workspace sizing (DPVO_BD_GRID timing experiments)
+static int bd_grid()
+{
+    static const int g = [] {
+        const char* e = getenv("DPVO_BD_GRID");
+        const int v = e ? atoi(e) : BD_GRID;
+        return v >= 64 && v <= BD_GRID_MAX ? v : BD_GRID;
+    }();
+    return g;
+}
 
 struct BdLayout {
     size_t hdr, gid, offs, perm, groups, gbws, gbws_bytes, Em, Cg, ug, Hpart, H, dX, total;
@@ -1590,7 +1602,7 @@ static BdLayout bd_layout(int64_t E, int64_t num_patches, int N)
     L.Em = take((size_t)L.mu_max * std::max(L.n6, 1) * 4);
     L.Cg = take((size_t)L.mu_max * 4);
     L.ug = take((size_t)L.mu_max * 4);
-    L.Hpart = take((size_t)BD_GRID * std::max(L.ent, 1) * 4);
+    L.Hpart = take((size_t)BD_GRID_MAX * std::max(L.ent, 1) * 4);
     L.H = take((size_t)std::max(L.ent, 1) * 4);
     L.dX = take((size_t)std::max(L.n6, 1) * 4);
     L.total = off;
@@ -2126,16 +2138,16 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
     const unsigned gR = (unsigned)((L.ent + 63) / 64);
     for (int it = 0; it < iterations; it++) {
         if (it == 0)
-            hipLaunchKernelGGL((bd_patch_kernel<false, true>), dim3(BD_GRID), dim3(64 * BD_WAVES), lds, s, p);
+            hipLaunchKernelGGL((bd_patch_kernel<false, true>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p);
         else
-            hipLaunchKernelGGL((bd_patch_kernel<true, true>), dim3(BD_GRID), dim3(64 * BD_WAVES), lds, s, p);
+            hipLaunchKernelGGL((bd_patch_kernel<true, true>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p);
         if (p.N > 0) {
-            hipLaunchKernelGGL(bd_reduce_kernel, dim3(gR), dim3(1024), 0, s, p, BD_GRID);
+            hipLaunchKernelGGL(bd_reduce_kernel, dim3(gR), dim3(1024), 0, s, p, bd_grid());
             hipLaunchKernelGGL(bd_solve_kernel, dim3(1), dim3(256), 0, s, p);
         }
         DPVO_CHECK_LAUNCH();
     }
-    hipLaunchKernelGGL((bd_patch_kernel<true, false>), dim3(BD_GRID), dim3(64 * BD_WAVES), 0, s, p);
+    hipLaunchKernelGGL((bd_patch_kernel<true, false>), dim3(bd_grid()), dim3(64 * BD_WAVES), 0, s, p);
     DPVO_CHECK_LAUNCH();
     return 0;
 }
