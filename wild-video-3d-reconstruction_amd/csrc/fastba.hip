@@ -1763,7 +1763,10 @@ __device__ __forceinline__ void bd_jterms_add(const BdEdge& o, float* part, floa
     }
 }
 
-template <bool APPLY, bool HESS>
+// DBG (timing experiments only, DPVO_BD_DBG; results are wrong): 1 skips the
+// shared-frame / target-frame pose terms, 2 the Schur update, 4 the
+// workgroup partial's write
+template <bool APPLY, bool HESS, int DBG = 0>
 __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
 {
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -1773,8 +1776,13 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
     const bool pose_terms = HESS && N > 0;
     float* part = sm + wave * ent;
     float* ev = sm + BD_WAVES * ent + wave * BD_N6MAX;
-    if (pose_terms)
+    // (row, column) of every upper-triangle entry k = tri_up(r, c): r | c << 8
+    uint16_t* tri_rc = reinterpret_cast<uint16_t*>(sm + BD_WAVES * ent + BD_WAVES * BD_N6MAX);
+    if (pose_terms) {
         for (int i = threadIdx.x; i < BD_WAVES * ent; i += blockDim.x) sm[i] = 0.f;
+        for (int r = threadIdx.x; r < n6; r += blockDim.x)
+            for (int c = r; c < n6; c++) tri_rc[tri_up(r, c, n6)] = (uint16_t)(r | c << 8);
+    }
     __syncthreads();
     const int64_t G = min(*p.groups, p.mu_max);
     const float lm = p.lmbda[0];
@@ -1843,7 +1851,7 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
             const bool jt = o.jv && !o.self;
             for (int q = 0; q < N && !mixed; q++)
                 mixed = __popcll(__ballot(jt && o.jx == q)) > 1;
-            const int passes = mixed ? 64 : 1;
+            const int passes = (DBG & 1) ? 0 : mixed ? 64 : 1;
             for (int ps = 0; ps < passes; ps++) {
                 const bool act = !mixed || lane == ps;
                 const uint64_t ivm = __ballot(act && o.iv);
@@ -1897,19 +1905,17 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         if (lane < n6) Er[lane] = e0;
         if (lane + 64 < n6) Er[lane + 64] = e1;
         if (lane == 0) { p.Cg[g] = Ck; p.ug[g] = uk; }
-        // Schur term: H -= Q e e^T (upper), g -= Q u e, over the touched poses
-        // (e_a from the lanes' registers: no LDS round trip per entry)
+        // Schur term: H -= Q e e^T (upper) over the touched poses' rows, one
+        // lane per upper-triangle entry (e from the wave's LDS row): each entry
+        // gets -(Q e_r) e_c, the same product and the same single add per patch
+        // as a row-by-row sweep, without its idle lanes and per-row readlanes
         const float Q = 1.0f / (Ck + lm);
         const float qu = Q * uk;
-        for (unsigned tm = touched; tm; tm &= tm - 1) {
-            const int pa = __ffs(tm) - 1;
-#pragma unroll
-            for (int t = 0; t < 6; t++) {
-                const int a = 6 * pa + t;
-                const float ea = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(a < 64 ? e0 : e1), a & 63));
-                const float qa = Q * ea;
-                if (lane >= a && lane < n6) atomicAdd(&part[tri_up(a, lane, n6)], -qa * e0);
-                if (lane + 64 >= a && lane + 64 < n6) atomicAdd(&part[tri_up(a, lane + 64, n6)], -qa * e1);
+        if (!(DBG & 2)) {
+#pragma unroll 4
+            for (int k = lane; k < nup; k += 64) {
+                const int rc = tri_rc[k], r = rc & 255, c = rc >> 8;
+                if (touched >> (r / 6) & 1) atomicAdd(&part[k], -(Q * ev[r]) * ev[c]);
             }
         }
         // g -= Q u e over the touched poses' entries, one lane per entry
@@ -1921,7 +1927,7 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
     // the workgroup's partial: its waves' partials summed in wave order
     __syncthreads();
     float* dst = p.Hpart + (int64_t)blockIdx.x * ent;
-    for (int i = threadIdx.x; i < ent; i += blockDim.x) {
+    for (int i = threadIdx.x; i < ((DBG & 4) ? 0 : ent); i += blockDim.x) {
         float s = sm[i];
 #pragma unroll
         for (int w = 1; w < BD_WAVES; w++) s += sm[w * ent + i];
@@ -2134,13 +2140,27 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
     p.Hpart = (float*)(ws + L.Hpart);
     p.H = (float*)(ws + L.H);
     p.dX = (float*)(ws + L.dX);
-    const size_t lds = (size_t)(BD_WAVES * (p.N > 0 ? L.ent : 0) + BD_WAVES * BD_N6MAX) * 4;
+    const size_t lds = (size_t)(BD_WAVES * (p.N > 0 ? L.ent : 0) + BD_WAVES * BD_N6MAX) * 4 +
+                       (size_t)(p.N > 0 ? L.nup : 0) * 2;
     const unsigned gR = (unsigned)((L.ent + 63) / 64);
+    static const int dbg = getenv("DPVO_BD_DBG") ? atoi(getenv("DPVO_BD_DBG")) : 0;
     for (int it = 0; it < iterations; it++) {
-        if (it == 0)
-            hipLaunchKernelGGL((bd_patch_kernel<false, true>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p);
-        else
-            hipLaunchKernelGGL((bd_patch_kernel<true, true>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p);
+#define BD_HESS(A, D) hipLaunchKernelGGL((bd_patch_kernel<A, true, D>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p)
+#define BD_DBG_CASES(A)                                                                                   \
+        switch (dbg) {                                                                                    \
+        case 1: BD_HESS(A, 1); break;                                                                     \
+        case 2: BD_HESS(A, 2); break;                                                                     \
+        case 3: BD_HESS(A, 3); break;                                                                     \
+        case 7: BD_HESS(A, 7); break;                                                                     \
+        default: BD_HESS(A, 0);                                                                           \
+        }
+        if (it == 0) {
+            BD_DBG_CASES(false)
+        } else {
+            BD_DBG_CASES(true)
+        }
+#undef BD_DBG_CASES
+#undef BD_HESS
         if (p.N > 0) {
             hipLaunchKernelGGL(bd_reduce_kernel, dim3(gR), dim3(1024), 0, s, p, bd_grid());
             hipLaunchKernelGGL(bd_solve_kernel, dim3(1), dim3(256), 0, s, p);
