@@ -230,14 +230,15 @@ class DPVO:
         self.pg.ii = torch.cat([self.pg.ii, self.ix[kk]])
         self.pg.net = torch.cat([self.pg.net, torch.zeros(1, len(kk), self.DIM, **self.kwargs)], dim=1)
 
-    def remove_factors(self, m, store: bool):
+    def remove_factors(self, m, store):
         """Boolean-mask compaction of the edge state (dpvo.py:349-364).  Each
         ``x[mask]`` is a host synchronisation (the output size); here the mask
         becomes an index once (one sync per side) and every tensor is
-        gathered with it."""
+        gathered with it.  store: True (keep the removed edges as inactive
+        factors), False, or a mask inside m: only those are kept."""
         assert self.pg.ii.numel() == self.pg.weight.shape[1]
-        if store:
-            rem = torch.nonzero(m).squeeze(1)
+        if store is not False:
+            rem = torch.nonzero(m if store is True else store).squeeze(1)
             self.pg.ii_inac = torch.cat((self.pg.ii_inac, self.pg.ii[rem]))
             self.pg.jj_inac = torch.cat((self.pg.jj_inac, self.pg.jj[rem]))
             self.pg.kk_inac = torch.cat((self.pg.kk_inac, self.pg.kk[rem]))
@@ -356,11 +357,15 @@ class DPVO:
                           torch.isnan(self.pg.poses_[k]).any().float()[None]]).tolist()
         self.check_ba(int(vals[2]))
         m = vals[0] + vals[1]
+        drop = None
         if m / 2 < self.cfg.KEYFRAME_THRESH:
             t0, t1 = self.pg.tstamps_[k - 1:k + 1].tolist()
             dP = SE3(self.pg.poses_[k]) * SE3(self.pg.poses_[k - 1]).inv()
             self.pg.delta[t1] = (t0, dP)
-            self.remove_factors((self.pg.ii == k) | (self.pg.jj == k), store=False)
+            # the edges of frame k go (remove_factors(store=False), :616-617);
+            # they are compacted away together with the retired ones below (one
+            # gather of the edge state instead of two; stable, so the same order)
+            drop = (self.pg.ii == k) | (self.pg.jj == k)
             # x[x > k] -= 1 as selects: no mask-size synchronisation
             later = self.pg.ii > k
             self.pg.kk = torch.where(later, self.pg.kk - self.M, self.pg.kk)
@@ -386,7 +391,13 @@ class DPVO:
             self.pg.m -= self.M
         elif vals[3]:
             raise Exception("Error: the estimated pose is nan!")
-        self.remove_factors(self.ix[self.pg.kk] < self.n - self.cfg.REMOVAL_WINDOW, store=True)
+        # edges whose patch left the removal window become inactive (:654-658)
+        old = self.ix[self.pg.kk] < self.n - self.cfg.REMOVAL_WINDOW
+        if drop is None:
+            self.remove_factors(old, store=True)
+        else:
+            old &= ~drop
+            self.remove_factors(old | drop, store=old)
 
     # ------------------------------------------------------------------ global BA (C4)
     def compute_keyframe_distance(self, i, j, beta=0.5):
@@ -519,7 +530,7 @@ class DPVO:
         slot = n % self.pmem
         self.imap_[slot] = imap.squeeze()
         self.gmap_[slot] = gmap.squeeze()
-        self.fmap1_[:, slot] = F.avg_pool2d(fmap[0], 1, 1)
+        self.fmap1_[:, slot] = fmap[0]   # avg_pool2d(fmap[0], 1, 1) (dpvo.py:840) is the identity
         self.fmap2_[:, slot] = F.avg_pool2d(fmap[0], 4, 4)
         self.image_buffer_[n % self.mem] = image
         self.counter += 1
@@ -529,8 +540,10 @@ class DPVO:
                 return
         self.pg.n += 1
         self.pg.m += self.M
-        self.append_factors(*self._edges_forw())
-        self.append_factors(*self._edges_back())
+        # forward then backward edges (dpvo.py:799-800) in one append: the
+        # edge state (net: E x 384 fp32) is reallocated once per frame, not twice
+        (kf, jf), (kb, jb) = self._edges_forw(), self._edges_back()
+        self.append_factors(torch.cat([kf, kb]), torch.cat([jf, jb]))
         if self.n == self.warm_up and not self.is_initialized:
             self.is_initialized = True
             for _ in range(12):
