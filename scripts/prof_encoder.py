@@ -27,6 +27,8 @@ def main():
         with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
             pf(img, 192)   # capture
             torch.cuda.synchronize()
+            import time
+            time.sleep(0.5)   # a gap in the kernel trace: what follows is the 20 replays
             for _ in range(20):
                 pf(img, 192)
     torch.cuda.synchronize()
