@@ -355,3 +355,21 @@ def test_edge_construction_follows_reference_rules():
             assert slam.pg.jj.tolist() == ref.jj, t
             assert slam.pg.kk.tolist() == ref.kk, t
     assert True in decisions and False in decisions
+
+
+@pytest.mark.parametrize("preset,buffer,n", [("fast", 96, 70), ("dpvo_2k", 2048, 2040)])
+def test_window_ij_groups_equal_the_operator_key(preset, buffer, n):
+    """DPVO._ij_groups (12-bit window key, counting sort) == the update
+    operator's own group_by(ii * 12345 + jj) (net.py:88): same gid, CSR and
+    group count, so SoftAgg over frame pairs is bit-identical."""
+    import update_ops
+    from dpvo.synthetic import steady_state_tracker
+    with torch.no_grad():
+        s = steady_state_tracker(preset, buffer=buffer, n=n, seed=3)
+        got = s._ij_groups()
+        key = s.pg.ii * 12345 + s.pg.jj
+        want = update_ops.group_by(key, key_bits=update_ops.key_bits_for(s.N * 12345 + 12345))
+    assert got is not None
+    G = int(want[3].item())
+    assert torch.equal(got[3], want[3]) and torch.equal(got[0], want[0]) and torch.equal(got[2], want[2])
+    assert torch.equal(got[1][:G + 1], want[1][:G + 1])   # offs past the group count is scratch

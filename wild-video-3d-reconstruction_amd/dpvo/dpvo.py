@@ -282,6 +282,7 @@ class DPVO:
             # operator's SoftAgg over kk and temporal neighbours, and BA's
             # per-patch reduction all read this CSR
             kk_groups = update_ops.group_by(self.pg.kk, key_bits=update_ops.key_bits_for(self.N * self.M))
+            ij_groups = self._ij_groups()
             with torch.autocast("cuda", enabled=True):
                 corr = self.corr(coords)
                 # ctx = imap[:, kk % (M pmem)] (dpvo.py:718), gathered by the consumer
@@ -289,7 +290,7 @@ class DPVO:
                 self.pg.net, (delta, weight, _) = self.network.update(self.pg.net, self.imap, corr, None, self.pg.ii,
                                                                       self.pg.jj, self.pg.kk, inp_idx=ctx_idx,
                                                                       index_bounds=(self.N * self.M, self.N),
-                                                                      kk_groups=kk_groups)
+                                                                      kk_groups=kk_groups, ij_groups=ij_groups)
             weight = weight.float()
             target = coords[..., self.P // 2, self.P // 2] + delta.float()
         self.pg.target = target
@@ -308,6 +309,22 @@ class DPVO:
             m = self.pg.m
             pops.point_cloud_centre(SE3(self.poses), self.patches[:, :m], self.intrinsics, self.ix[:m],
                                     out=self.pg.points_[:m])
+
+    def _ij_groups(self):
+        """The update operator's SoftAgg over frame pairs groups the edges by
+        ii * 12345 + jj (net.py:88), a key the device group-by must radix-sort
+        (~80 us at C3).  Inside the sliding window every edge has
+        n - 64 <= jj, ii < n: the patch frame ii >= n - REMOVAL_WINDOW - 1
+        (keyframe() retires older ones, dpvo.py:654-658) and the target
+        jj >= ii - PATCH_LIFETIME (dpvo.py:756-769).  So (ii - b) * 64 + (jj - b),
+        b = n - 64, is a 12-bit key in the same lexicographic order: the same
+        groups in the same order (bit-identical results) by a counting sort.
+        None (the operator's own key) when the config's windows could exceed it."""
+        if self.cfg.REMOVAL_WINDOW + self.cfg.PATCH_LIFETIME + 2 > 64 or not getattr(self.cfg, "WINDOW_IJ_KEY", True):
+            return None
+        b = self.n - 64
+        key = (self.pg.ii - b) * 64 + (self.pg.jj - b)
+        return update_ops.group_by(key, key_bits=12)
 
     def check_ba(self, status=None):
         """raise the reference's BA error (ba_cuda.cu:521) if an update() since
