@@ -529,6 +529,7 @@ extern "C" int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, co
     if (g > 8) g &= ~int64_t(7);
     const unsigned grid = (unsigned)g;
     static const bool nostore = getenv("DPVO_CM_DBG") && std::string(getenv("DPVO_CM_DBG")) == "nostore";
+    if (nostore) warn_debug_knob("DPVO_CM_DBG");
     if (nostore)
         hipLaunchKernelGGL(corr_mfma_kernel<false>, dim3(grid), dim3(64 * cm::WAVES), 0, as_stream(stream), p);
     else

@@ -2144,6 +2144,7 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
                        (size_t)(p.N > 0 ? L.nup : 0) * 2;
     const unsigned gR = (unsigned)((L.ent + 63) / 64);
     static const int dbg = getenv("DPVO_BD_DBG") ? atoi(getenv("DPVO_BD_DBG")) : 0;
+    if (dbg) warn_debug_knob("DPVO_BD_DBG");
     for (int it = 0; it < iterations; it++) {
 #define BD_HESS(A, D) hipLaunchKernelGGL((bd_patch_kernel<A, true, D>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p)
 #define BD_DBG_CASES(A)                                                                                   \

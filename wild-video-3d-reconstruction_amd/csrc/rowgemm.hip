@@ -1645,6 +1645,7 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
         const char* dbgs = getenv("DPVO_RG4_DBG");   // read per call: timing experiments switch it in-process
         const int dbg = dbgs ? atoi(dbgs) : 0;
         if (dbg && f == 0) {   // timing experiments (scripts/bench_rg4_dbg.py)
+            warn_debug_knob("DPVO_RG4_DBG");
             switch (dbg) {
 #define R4D_CASE(D)                                                                                                  \
     case (D):                                                                                                        \
@@ -1837,6 +1838,7 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
         return 0;
     }
     if (const char* dbgs = getenv("DPVO_RC_DBG"); dbgs && f == DPVO_RG_RES && !gate) {   // timing experiments
+        if (atoi(dbgs)) warn_debug_knob("DPVO_RC_DBG");
         switch (atoi(dbgs)) {
 #define RCD_CASE(D)                                                                                               \
     case (D):                                                                                                     \

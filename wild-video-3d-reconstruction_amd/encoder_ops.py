@@ -16,6 +16,9 @@ import _dpvo_hot as H
 
 XPLAIN, XNORM_RELU, XBLOCK = 0, 1, 2
 _DBG_NOSTATS = os.environ.get("DPVO_ENC_DBG") == "nostats"   # timing experiments only: skips the IN statistics
+if _DBG_NOSTATS:
+    import warnings
+    warnings.warn("DPVO_ENC_DBG=nostats is set -- a timing experiment; encoder outputs are NOT valid")
 
 
 class ConvArgs(_ct.Structure):
