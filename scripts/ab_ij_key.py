@@ -19,7 +19,7 @@ def main():
             s.update()
         for _ in range(5):
             for on in (True, False):
-                s.cfg.WINDOW_IJ_KEY = on
+                s.cfg.WINDOW_IJ_KEY = on   # both window keys (kk and ii, jj)
                 s.update()
                 torch.cuda.synchronize()
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

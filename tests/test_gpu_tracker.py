@@ -360,8 +360,9 @@ def test_edge_construction_follows_reference_rules():
 @pytest.mark.parametrize("preset,buffer,n", [("fast", 96, 70), ("dpvo_2k", 2048, 2040)])
 def test_window_ij_groups_equal_the_operator_key(preset, buffer, n):
     """DPVO._ij_groups (12-bit window key, counting sort) == the update
-    operator's own group_by(ii * 12345 + jj) (net.py:88): same gid, CSR and
-    group count, so SoftAgg over frame pairs is bit-identical."""
+    operator's own group_by(ii * 12345 + jj) (net.py:88), and _kk_groups
+    (window-relative kk) == group_by(kk): same gid, CSR and group count, so
+    SoftAgg, the neighbours and BA's per-patch reduction are bit-identical."""
     import update_ops
     from dpvo.synthetic import steady_state_tracker
     with torch.no_grad():
@@ -369,7 +370,10 @@ def test_window_ij_groups_equal_the_operator_key(preset, buffer, n):
         got = s._ij_groups()
         key = s.pg.ii * 12345 + s.pg.jj
         want = update_ops.group_by(key, key_bits=update_ops.key_bits_for(s.N * 12345 + 12345))
+        got_kk = s._kk_groups()
+        want_kk = update_ops.group_by(s.pg.kk, key_bits=update_ops.key_bits_for(s.N * s.M))
     assert got is not None
-    G = int(want[3].item())
-    assert torch.equal(got[3], want[3]) and torch.equal(got[0], want[0]) and torch.equal(got[2], want[2])
-    assert torch.equal(got[1][:G + 1], want[1][:G + 1])   # offs past the group count is scratch
+    for g, w in ((got, want), (got_kk, want_kk)):
+        G = int(w[3].item())
+        assert torch.equal(g[3], w[3]) and torch.equal(g[0], w[0]) and torch.equal(g[2], w[2])
+        assert torch.equal(g[1][:G + 1], w[1][:G + 1])   # offs past the group count is scratch

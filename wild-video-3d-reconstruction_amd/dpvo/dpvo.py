@@ -281,7 +281,7 @@ class DPVO:
             # the edges grouped by patch once, on the device: the update
             # operator's SoftAgg over kk and temporal neighbours, and BA's
             # per-patch reduction all read this CSR
-            kk_groups = update_ops.group_by(self.pg.kk, key_bits=update_ops.key_bits_for(self.N * self.M))
+            kk_groups = self._kk_groups()
             ij_groups = self._ij_groups()
             with torch.autocast("cuda", enabled=True):
                 corr = self.corr(coords)
@@ -310,6 +310,22 @@ class DPVO:
             pops.point_cloud_centre(SE3(self.poses), self.patches[:, :m], self.intrinsics, self.ix[:m],
                                     out=self.pg.points_[:m])
 
+    def _window_keys(self):
+        """True when every edge of the sliding window has n - 64 <= ii, jj < n
+        (see _ij_groups) for this config."""
+        return (self.cfg.REMOVAL_WINDOW + self.cfg.PATCH_LIFETIME + 2 <= 64 and
+                getattr(self.cfg, "WINDOW_IJ_KEY", True))
+
+    def _kk_groups(self):
+        """The edges grouped by patch (the update operator's SoftAgg over kk,
+        its temporal neighbours and BA's per-patch reduction all read this
+        CSR).  Patch kk lives in frame kk // M = ii >= n - 64 (see _ij_groups),
+        so kk - M (n - 64) is a key below 64 M in the same order: the same
+        groups from a counting sort over 64 M bins instead of N M."""
+        if not self._window_keys():
+            return update_ops.group_by(self.pg.kk, key_bits=update_ops.key_bits_for(self.N * self.M))
+        return update_ops.group_by(self.pg.kk - self.M * (self.n - 64), key_bits=update_ops.key_bits_for(64 * self.M))
+
     def _ij_groups(self):
         """The update operator's SoftAgg over frame pairs groups the edges by
         ii * 12345 + jj (net.py:88), a key the device group-by must radix-sort
@@ -320,7 +336,7 @@ class DPVO:
         b = n - 64, is a 12-bit key in the same lexicographic order: the same
         groups in the same order (bit-identical results) by a counting sort.
         None (the operator's own key) when the config's windows could exceed it."""
-        if self.cfg.REMOVAL_WINDOW + self.cfg.PATCH_LIFETIME + 2 > 64 or not getattr(self.cfg, "WINDOW_IJ_KEY", True):
+        if not self._window_keys():
             return None
         b = self.n - 64
         key = (self.pg.ii - b) * 64 + (self.pg.jj - b)
