@@ -281,12 +281,18 @@ class DPVO:
             # the edges grouped by patch once, on the device: the update
             # operator's SoftAgg over kk and temporal neighbours, and BA's
             # per-patch reduction all read this CSR
-            kk_groups = self._kk_groups()
-            ij_groups = self._ij_groups()
+            if self._window_keys():
+                # both group keys and the context-row index in one launch
+                key_kk, key_ij, ctx_idx = update_ops.window_keys(self.pg.ii, self.pg.jj, self.pg.kk, self.M,
+                                                                 self.n - 64, self.M * self.pmem)
+                kk_groups = update_ops.group_by(key_kk, key_bits=update_ops.key_bits_for(64 * self.M))
+                ij_groups = update_ops.group_by(key_ij, key_bits=12)
+            else:
+                kk_groups, ij_groups = self._kk_groups(), self._ij_groups()
+                ctx_idx = self.pg.kk % (self.M * self.pmem)
             with torch.autocast("cuda", enabled=True):
                 corr = self.corr(coords)
                 # ctx = imap[:, kk % (M pmem)] (dpvo.py:718), gathered by the consumer
-                ctx_idx = self.pg.kk % (self.M * self.pmem)
                 self.pg.net, (delta, weight, _) = self.network.update(self.pg.net, self.imap, corr, None, self.pg.ii,
                                                                       self.pg.jj, self.pg.kk, inp_idx=ctx_idx,
                                                                       index_bounds=(self.N * self.M, self.N),
