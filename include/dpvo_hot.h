@@ -398,12 +398,13 @@ typedef struct dpvo_rowadd_args {
 } dpvo_rowadd_args;
 int dpvo_rowadd_ln(const dpvo_rowadd_args* args, void* stream);
 
-/* The tracker's per-update edge keys in one launch (DPVO.update, dpvo.py:718 and
- * the SoftAgg group keys of net.py:86-88): key_kk[e] = kk[e] - M base,
- * key_ij[e] = (ii[e] - base) * 64 + (jj[e] - base), ctx[e] = kk[e] mod ring.
- * All int64 [E]. */
+/* The tracker's per-update edge keys in one launch (DPVO.update / DPVO.corr,
+ * dpvo.py:326-327,718 and the SoftAgg group keys of net.py:86-88):
+ * key_kk[e] = kk[e] - M base, key_ij[e] = (ii[e] - base) * 64 + (jj[e] - base),
+ * ctx[e] = kk[e] mod ring, jslot[e] = jj[e] mod frames.  All int64 [E]. */
 int dpvo_window_keys(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t E, int64_t M, int64_t base,
-                     int64_t ring, int64_t* key_kk, int64_t* key_ij, int64_t* ctx, void* stream);
+                     int64_t ring, int64_t frames, int64_t* key_kk, int64_t* key_ij, int64_t* ctx, int64_t* jslot,
+                     void* stream);
 
 /* out[e][:] = idx[e] >= 0 ? x[idx[e]][:] : 0, converting in_dtype -> out_dtype
  * (the mask_ix * net[:, ix] of net.py:82-85; x rows at x + r*ldx, out

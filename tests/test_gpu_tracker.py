@@ -374,10 +374,11 @@ def test_window_ij_groups_equal_the_operator_key(preset, buffer, n):
         want_kk = update_ops.group_by(s.pg.kk, key_bits=update_ops.key_bits_for(s.N * s.M))
         # the one-launch keys update() uses == the torch compositions
         b, ring = s.n - 64, s.M * s.pmem
-        kk_key, ij_key, ctx = update_ops.window_keys(s.pg.ii, s.pg.jj, s.pg.kk, s.M, b, ring)
+        kk_key, ij_key, ctx, jslot = update_ops.window_keys(s.pg.ii, s.pg.jj, s.pg.kk, s.M, b, ring, s.pmem)
         assert torch.equal(kk_key, s.pg.kk - s.M * b)
         assert torch.equal(ij_key, (s.pg.ii - b) * 64 + (s.pg.jj - b))
         assert torch.equal(ctx, s.pg.kk % ring)
+        assert torch.equal(jslot, s.pg.jj % s.pmem)
     assert got is not None
     for g, w in ((got, want), (got_kk, want_kk)):
         G = int(w[3].item())

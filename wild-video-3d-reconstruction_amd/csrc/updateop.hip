@@ -520,19 +520,22 @@ extern "C" int dpvo_softagg_forward(int dtype, const void* f, int64_t ldf, const
 // The tracker's per-update edge keys in one pass (DPVO.update: _kk_groups,
 // _ij_groups and the context-row index of dpvo.py:718), instead of ~6 torch
 // elementwise launches: key_kk = kk - M base, key_ij = (ii - base) * 64 +
-// (jj - base), ctx = kk mod ring.
+// (jj - base), ctx = kk mod ring (the patch ring slot: DPVO.corr's and the
+// context gather's index), jslot = jj mod frames (the frame ring slot).
 __global__ __launch_bounds__(256) void window_keys_kernel(const int64_t* __restrict__ ii,
                                                           const int64_t* __restrict__ jj,
                                                           const int64_t* __restrict__ kk, int64_t E, int64_t M,
-                                                          int64_t base, int64_t ring, int64_t* __restrict__ key_kk,
-                                                          int64_t* __restrict__ key_ij, int64_t* __restrict__ ctx)
+                                                          int64_t base, int64_t ring, int64_t frames,
+                                                          int64_t* __restrict__ key_kk, int64_t* __restrict__ key_ij,
+                                                          int64_t* __restrict__ ctx, int64_t* __restrict__ jslot)
 {
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t k = kk[e];
         key_kk[e] = k - M * base;
         key_ij[e] = (ii[e] - base) * 64 + (jj[e] - base);
-        const int64_t r = k % ring;
-        ctx[e] = r < 0 ? r + ring : r;   // Python's modulo (kk >= 0 in the tracker)
+        const int64_t r = k % ring, f = jj[e] % frames;
+        ctx[e] = r < 0 ? r + ring : r;   // Python's modulo (kk, jj >= 0 in the tracker)
+        jslot[e] = f < 0 ? f + frames : f;
     }
 }
 
@@ -717,14 +720,14 @@ extern "C" int dpvo_softagg_csr(int dtype, const void* f, int64_t ldf, const voi
 }
 
 extern "C" int dpvo_window_keys(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t E, int64_t M,
-                                int64_t base, int64_t ring, int64_t* key_kk, int64_t* key_ij, int64_t* ctx,
-                                void* stream)
+                                int64_t base, int64_t ring, int64_t frames, int64_t* key_kk, int64_t* key_ij,
+                                int64_t* ctx, int64_t* jslot, void* stream)
 {
-    DPVO_CHECK_ARG(E >= 0 && M > 0 && ring > 0, "E >= 0, M > 0 and ring > 0 required");
+    DPVO_CHECK_ARG(E >= 0 && M > 0 && ring > 0 && frames > 0, "E >= 0, M > 0, ring > 0 and frames > 0 required");
     if (E == 0) return 0;
-    DPVO_CHECK_ARG(ii && jj && kk && key_kk && key_ij && ctx, "null operand");
+    DPVO_CHECK_ARG(ii && jj && kk && key_kk && key_ij && ctx && jslot, "null operand");
     hipLaunchKernelGGL(window_keys_kernel, dim3(grid_for(E, 256, 4096)), dim3(256), 0, as_stream(stream), ii, jj, kk,
-                       E, M, base, ring, key_kk, key_ij, ctx);
+                       E, M, base, ring, frames, key_kk, key_ij, ctx, jslot);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

@@ -177,12 +177,16 @@ class DPVO:
         return poses, torch.as_tensor([self.pg.tstamps_[i] for i in range(self.n)], dtype=torch.float64).numpy()
 
     # ------------------------------------------------------------------ hot path
-    def corr(self, coords, indicies=None):
-        """2-level local correlation -> [1, E, 882] (dpvo.py:326-333), one fused launch."""
-        ii, jj = indicies if indicies is not None else (self.pg.kk, self.pg.jj)
-        ii1 = ii % (self.M * self.pmem)
-        jj1 = jj % self.pmem
-        E = len(ii)
+    def corr(self, coords, indicies=None, slots=None):
+        """2-level local correlation -> [1, E, 882] (dpvo.py:326-333), one fused launch.
+        slots: the ring slots (kk mod M pmem, jj mod pmem) when the caller has them."""
+        if slots is not None:
+            ii1, jj1 = slots
+        else:
+            ii, jj = indicies if indicies is not None else (self.pg.kk, self.pg.jj)
+            ii1 = ii % (self.M * self.pmem)
+            jj1 = jj % self.pmem
+        E = len(ii1)
         out = table = None
         if self.gmap_.dtype == torch.float16:
             # rows padded to 896 (zeros past 882): the update operator's first
@@ -282,16 +286,18 @@ class DPVO:
             # operator's SoftAgg over kk and temporal neighbours, and BA's
             # per-patch reduction all read this CSR
             if self._window_keys():
-                # both group keys and the context-row index in one launch
-                key_kk, key_ij, ctx_idx = update_ops.window_keys(self.pg.ii, self.pg.jj, self.pg.kk, self.M,
-                                                                 self.n - 64, self.M * self.pmem)
+                # both group keys and the ring slots (context rows, corr) in one launch
+                key_kk, key_ij, ctx_idx, jslot = update_ops.window_keys(self.pg.ii, self.pg.jj, self.pg.kk, self.M,
+                                                                        self.n - 64, self.M * self.pmem, self.pmem)
                 kk_groups = update_ops.group_by(key_kk, key_bits=update_ops.key_bits_for(64 * self.M))
                 ij_groups = update_ops.group_by(key_ij, key_bits=12)
+                slots = (ctx_idx, jslot)
             else:
                 kk_groups, ij_groups = self._kk_groups(), self._ij_groups()
                 ctx_idx = self.pg.kk % (self.M * self.pmem)
+                slots = None
             with torch.autocast("cuda", enabled=True):
-                corr = self.corr(coords)
+                corr = self.corr(coords, slots=slots)
                 # ctx = imap[:, kk % (M pmem)] (dpvo.py:718), gathered by the consumer
                 self.pg.net, (delta, weight, _) = self.network.update(self.pg.net, self.imap, corr, None, self.pg.ii,
                                                                       self.pg.jj, self.pg.kk, inp_idx=ctx_idx,

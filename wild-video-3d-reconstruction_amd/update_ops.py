@@ -163,18 +163,18 @@ def neighbors_csr(jj, offs, perm, groups, max_groups):
     return ix, jx
 
 
-def window_keys(ii, jj, kk, M, base, ring):
-    """(kk - M base, (ii - base) * 64 + (jj - base), kk mod ring) as int64 [E]
-    each, in one launch (dpvo_window_keys)."""
+def window_keys(ii, jj, kk, M, base, ring, frames):
+    """(kk - M base, (ii - base) * 64 + (jj - base), kk mod ring, jj mod frames)
+    as int64 [E] each, in one launch (dpvo_window_keys)."""
     H.on_gpu(ii, jj, kk)
     ii, jj, kk = H.idx64(ii), H.idx64(jj), H.idx64(kk)
     E = kk.numel()
     if ii.numel() != E or jj.numel() != E:
         raise RuntimeError("window_keys: ii, jj and kk must have the same length")
-    out = torch.empty(3, E, dtype=torch.int64, device=kk.device)
-    H.check(H.lib().dpvo_window_keys(H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(M), int(base), int(ring), H.ptr(out[0]),
-                                     H.ptr(out[1]), H.ptr(out[2]), H.stream_of(kk)))
-    return out[0], out[1], out[2]
+    out = torch.empty(4, E, dtype=torch.int64, device=kk.device)
+    H.check(H.lib().dpvo_window_keys(H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(M), int(base), int(ring), int(frames),
+                                     H.ptr(out[0]), H.ptr(out[1]), H.ptr(out[2]), H.ptr(out[3]), H.stream_of(kk)))
+    return out[0], out[1], out[2], out[3]
 
 
 def gather_rows(x, idx, dtype=None):
