@@ -406,6 +406,14 @@ int dpvo_window_keys(const int64_t* ii, const int64_t* jj, const int64_t* kk, in
                      int64_t ring, int64_t frames, int64_t* key_kk, int64_t* key_ij, int64_t* ctx, int64_t* jslot,
                      void* stream);
 
+/* DPVO.update after the update operator (dpvo.py:724-727): target[e] =
+ * centre[e] + float(delta[e]), weight[e] = float(w[e]), both fp32 [E][2]
+ * contiguous.  delta, w: fp16, row e at delta + e * delta_stride (2 values);
+ * centre: fp32, x at centre + e * centre_stride, y at + centre_comp. */
+int dpvo_edge_targets(const void* delta, int64_t delta_stride, const void* w, int64_t w_stride, const float* centre,
+                      int64_t centre_stride, int64_t centre_comp, int64_t E, float* target, float* weight,
+                      void* stream);
+
 /* out[e][:] = idx[e] >= 0 ? x[idx[e]][:] : 0, converting in_dtype -> out_dtype
  * (the mask_ix * net[:, ix] of net.py:82-85; x rows at x + r*ldx, out
  * contiguous [n][D]). */

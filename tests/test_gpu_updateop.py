@@ -176,3 +176,17 @@ def test_rowgemm_device_row_count():
     _, ref, _ = U.rowgemm(A, W16, b16)
     assert torch.equal(out[:300], ref[:300])
     assert (out[300:] == 7.0).all()
+
+
+def test_edge_targets_equal_torch_composition():
+    """update_ops.edge_targets == coords[..., 1, 1] + delta.float(), weight.float()
+    (dpvo.py:724-727) bit for bit, on strided head views like the fused operator's."""
+    import update_ops
+    E = 5000
+    g = torch.Generator(device="cpu").manual_seed(0)
+    heads = (torch.randn(E, 4, generator=g) * 3).half().cuda()
+    coords = (torch.randn(1, E, 2, 3, 3, generator=g) * 100).cuda()
+    delta, weight = heads[None, :, :2], heads[None, :, 2:]
+    centre = coords[..., 1, 1]
+    t, w = update_ops.edge_targets(centre, delta, weight)
+    assert torch.equal(t, centre + delta.float()) and torch.equal(w, weight.float())

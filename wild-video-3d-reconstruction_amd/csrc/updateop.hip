@@ -539,6 +539,25 @@ __global__ __launch_bounds__(256) void window_keys_kernel(const int64_t* __restr
     }
 }
 
+// target = coords[..., P/2, P/2] + float(delta), weight = float(w) for every
+// edge (DPVO.update after the update operator, dpvo.py:724-727), one launch
+// instead of three.  delta / w: fp16 rows with their own strides (the fused
+// operator's [E][4] head rows); c: the patch centre's x at c + e * cs, y at
+// c + e * cs + cc.
+__global__ __launch_bounds__(256) void edge_targets_kernel(const half_t* __restrict__ delta, int64_t ds,
+                                                           const half_t* __restrict__ w, int64_t ws,
+                                                           const float* __restrict__ c, int64_t cs, int64_t cc,
+                                                           int64_t E, float* __restrict__ target,
+                                                           float* __restrict__ weight)
+{
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+        target[2 * e] = c[e * cs] + (float)delta[e * ds];
+        target[2 * e + 1] = c[e * cs + cc] + (float)delta[e * ds + 1];
+        weight[2 * e] = (float)w[e * ws];
+        weight[2 * e + 1] = (float)w[e * ws + 1];
+    }
+}
+
 extern "C" int dpvo_gather_rows(int in_dtype, const void* x, int64_t ldx, int64_t rows, const int64_t* idx, int64_t n,
                                 int D, int out_dtype, void* out, void* stream)
 {
@@ -728,6 +747,20 @@ extern "C" int dpvo_window_keys(const int64_t* ii, const int64_t* jj, const int6
     DPVO_CHECK_ARG(ii && jj && kk && key_kk && key_ij && ctx && jslot, "null operand");
     hipLaunchKernelGGL(window_keys_kernel, dim3(grid_for(E, 256, 4096)), dim3(256), 0, as_stream(stream), ii, jj, kk,
                        E, M, base, ring, frames, key_kk, key_ij, ctx, jslot);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_edge_targets(const void* delta, int64_t delta_stride, const void* w, int64_t w_stride,
+                                 const float* centre, int64_t centre_stride, int64_t centre_comp, int64_t E,
+                                 float* target, float* weight, void* stream)
+{
+    DPVO_CHECK_ARG(E >= 0, "E >= 0 required");
+    if (E == 0) return 0;
+    DPVO_CHECK_ARG(delta && w && centre && target && weight, "null operand");
+    hipLaunchKernelGGL(edge_targets_kernel, dim3(grid_for(E, 256, 4096)), dim3(256), 0, as_stream(stream),
+                       (const half_t*)delta, delta_stride, (const half_t*)w, w_stride, centre, centre_stride,
+                       centre_comp, E, target, weight);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

@@ -303,8 +303,12 @@ class DPVO:
                                                                       self.pg.jj, self.pg.kk, inp_idx=ctx_idx,
                                                                       index_bounds=(self.N * self.M, self.N),
                                                                       kk_groups=kk_groups, ij_groups=ij_groups)
-            weight = weight.float()
-            target = coords[..., self.P // 2, self.P // 2] + delta.float()
+            centre = coords[..., self.P // 2, self.P // 2]
+            if delta.dtype == torch.float16 and weight.dtype == torch.float16 and delta.stride(2) == 1:
+                target, weight = update_ops.edge_targets(centre, delta, weight)   # one launch
+            else:
+                weight = weight.float()
+                target = centre + delta.float()
         self.pg.target = target
         self.pg.weight = weight
         with Timer("BA", enabled=self.enable_timing):

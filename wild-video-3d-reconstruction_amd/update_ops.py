@@ -177,6 +177,23 @@ def window_keys(ii, jj, kk, M, base, ring, frames):
     return out[0], out[1], out[2], out[3]
 
 
+def edge_targets(centre, delta, weight):
+    """(centre + delta.float(), weight.float()) for [1, E, 2] views (fp32 centre,
+    fp16 delta / weight with unit component stride) in one launch."""
+    H.on_gpu(centre, delta, weight)
+    E = delta.shape[1]
+    if (delta.dtype != torch.float16 or weight.dtype != torch.float16 or centre.dtype != torch.float32 or
+            delta.shape != (1, E, 2) or weight.shape != (1, E, 2) or centre.shape != (1, E, 2) or
+            delta.stride(2) != 1 or weight.stride(2) != 1):
+        raise RuntimeError("edge_targets: centre fp32, delta / weight fp16 [1, E, 2] with unit component stride")
+    target = torch.empty(1, E, 2, dtype=torch.float32, device=delta.device)
+    w32 = torch.empty(1, E, 2, dtype=torch.float32, device=delta.device)
+    H.check(H.lib().dpvo_edge_targets(H.ptr(delta), delta.stride(1), H.ptr(weight), weight.stride(1), H.ptr(centre),
+                                      centre.stride(1), centre.stride(2), E, H.ptr(target), H.ptr(w32),
+                                      H.stream_of(delta)))
+    return target, w32
+
+
 def gather_rows(x, idx, dtype=None):
     """out[e] = x[idx[e]] if idx[e] >= 0 else 0, cast to ``dtype`` (default x's).
     x: [R, D] with unit channel stride; idx: [n] int64."""
