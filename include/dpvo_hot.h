@@ -401,10 +401,12 @@ int dpvo_rowadd_ln(const dpvo_rowadd_args* args, void* stream);
 /* The tracker's per-update edge keys in one launch (DPVO.update / DPVO.corr,
  * dpvo.py:326-327,718 and the SoftAgg group keys of net.py:86-88):
  * key_kk[e] = kk[e] - M base, key_ij[e] = (ii[e] - base) * 64 + (jj[e] - base),
- * ctx[e] = kk[e] mod ring, jslot[e] = jj[e] mod frames.  All int64 [E]. */
+ * ctx[e] = kk[e] mod ring, jslot[e] = jj[e] mod frames.  All int64 [E].
+ * flag (optional int32): set to -2 if still 0 when an edge falls outside the
+ * window (ii - base, jj - base not in [0, 64) or key_kk not in [0, 64 M)). */
 int dpvo_window_keys(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t E, int64_t M, int64_t base,
                      int64_t ring, int64_t frames, int64_t* key_kk, int64_t* key_ij, int64_t* ctx, int64_t* jslot,
-                     void* stream);
+                     int* flag, void* stream);
 
 /* DPVO.update after the update operator (dpvo.py:724-727): target[e] =
  * centre[e] + float(delta[e]), weight[e] = float(w[e]), both fp32 [E][2]

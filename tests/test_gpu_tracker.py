@@ -384,3 +384,26 @@ def test_window_ij_groups_equal_the_operator_key(preset, buffer, n):
         G = int(w[3].item())
         assert torch.equal(g[3], w[3]) and torch.equal(g[0], w[0]) and torch.equal(g[2], w[2])
         assert torch.equal(g[1][:G + 1], w[1][:G + 1])   # offs past the group count is scratch
+
+
+def test_window_keys_flag_out_of_window_edges():
+    """An edge outside the 64-frame key window sets the deferred failure word
+    (-2, first failure kept), which check_ba() turns into an error; in-window
+    edges leave it alone."""
+    import cuda_ba
+    import update_ops
+    n, M = 100, 8
+    ii = torch.tensor([n - 1, n - 5, n - 40], device="cuda")
+    jj = torch.tensor([n - 2, n - 1, n - 50], device="cuda")
+    kk = ii * M + 3
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    update_ops.window_keys(ii, jj, kk, M, n - 64, M * 36, 36, flag=flag)
+    assert int(flag.item()) == 0
+    jj[2] = n - 70   # outside [n - 64, n)
+    update_ops.window_keys(ii, jj, kk, M, n - 64, M * 36, 36, flag=flag)
+    assert int(flag.item()) == -2
+    flag.fill_(7)    # an earlier failure is kept
+    update_ops.window_keys(ii, jj, kk, M, n - 64, M * 36, 36, flag=flag)
+    assert int(flag.item()) == 7
+    with pytest.raises(RuntimeError, match="key window"):
+        cuda_ba.raise_for_status(-2)

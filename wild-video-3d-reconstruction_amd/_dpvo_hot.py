@@ -78,7 +78,7 @@ _SIGNATURES = {
     "dpvo_rowchain_gated": (_ip, [_vp, _vp, _vp, _vp]),
     "dpvo_rowadd_ln": (_ip, [_vp, _vp]),
     "dpvo_edge_targets": (_ip, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp]),
-    "dpvo_window_keys": (_ip, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp]),
+    "dpvo_window_keys": (_ip, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dpvo_encoder_tiles": (_i64, [_ip, _ip, _ip, _ip]),
     "dpvo_encoder_stem": (_ip, [_vp, _ip, _ip, _vp, _ip, _vp]),
     "dpvo_encoder_conv": (_ip, [_ip] * 7 + [_vp, _ip, _vp]),

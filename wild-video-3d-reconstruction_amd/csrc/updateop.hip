@@ -522,17 +522,23 @@ extern "C" int dpvo_softagg_forward(int dtype, const void* f, int64_t ldf, const
 // elementwise launches: key_kk = kk - M base, key_ij = (ii - base) * 64 +
 // (jj - base), ctx = kk mod ring (the patch ring slot: DPVO.corr's and the
 // context gather's index), jslot = jj mod frames (the frame ring slot).
+// flag (optional): set to -2 (unless already non-zero) when an edge lies
+// outside the 64-frame key window, so a violated invariant fails loudly at the
+// tracker's next status read instead of mis-grouping silently.
 __global__ __launch_bounds__(256) void window_keys_kernel(const int64_t* __restrict__ ii,
                                                           const int64_t* __restrict__ jj,
                                                           const int64_t* __restrict__ kk, int64_t E, int64_t M,
                                                           int64_t base, int64_t ring, int64_t frames,
                                                           int64_t* __restrict__ key_kk, int64_t* __restrict__ key_ij,
-                                                          int64_t* __restrict__ ctx, int64_t* __restrict__ jslot)
+                                                          int64_t* __restrict__ ctx, int64_t* __restrict__ jslot,
+                                                          int* __restrict__ flag)
 {
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t k = kk[e];
-        key_kk[e] = k - M * base;
-        key_ij[e] = (ii[e] - base) * 64 + (jj[e] - base);
+        const int64_t a = ii[e] - base, b = jj[e] - base, kr = k - M * base;
+        key_kk[e] = kr;
+        key_ij[e] = a * 64 + b;
+        if (flag && (a < 0 || a >= 64 || b < 0 || b >= 64 || kr < 0 || kr >= 64 * M)) atomicCAS(flag, 0, -2);
         const int64_t r = k % ring, f = jj[e] % frames;
         ctx[e] = r < 0 ? r + ring : r;   // Python's modulo (kk, jj >= 0 in the tracker)
         jslot[e] = f < 0 ? f + frames : f;
@@ -740,13 +746,13 @@ extern "C" int dpvo_softagg_csr(int dtype, const void* f, int64_t ldf, const voi
 
 extern "C" int dpvo_window_keys(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t E, int64_t M,
                                 int64_t base, int64_t ring, int64_t frames, int64_t* key_kk, int64_t* key_ij,
-                                int64_t* ctx, int64_t* jslot, void* stream)
+                                int64_t* ctx, int64_t* jslot, int* flag, void* stream)
 {
     DPVO_CHECK_ARG(E >= 0 && M > 0 && ring > 0 && frames > 0, "E >= 0, M > 0, ring > 0 and frames > 0 required");
     if (E == 0) return 0;
     DPVO_CHECK_ARG(ii && jj && kk && key_kk && key_ij && ctx && jslot, "null operand");
     hipLaunchKernelGGL(window_keys_kernel, dim3(grid_for(E, 256, 4096)), dim3(256), 0, as_stream(stream), ii, jj, kk,
-                       E, M, base, ring, frames, key_kk, key_ij, ctx, jslot);
+                       E, M, base, ring, frames, key_kk, key_ij, ctx, jslot, flag);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

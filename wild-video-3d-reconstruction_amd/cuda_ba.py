@@ -41,6 +41,9 @@ def raise_for_status(s):
         raise RuntimeError(
             "linalg.cholesky: The factorization could not be completed because the input is not positive-"
             f"definite (the leading minor of order {s} is not positive-definite).")
+    if s == -2:
+        raise RuntimeError("DPVO.update: an edge lies outside the 64-frame key window "
+                           "(REMOVAL_WINDOW / PATCH_LIFETIME invariant; set cfg.WINDOW_IJ_KEY = False)")
     if s < 0:
         raise RuntimeError("cuda_ba.forward: patch index out of range")
 

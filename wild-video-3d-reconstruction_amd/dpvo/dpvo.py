@@ -287,8 +287,11 @@ class DPVO:
             # per-patch reduction all read this CSR
             if self._window_keys():
                 # both group keys and the ring slots (context rows, corr) in one launch
+                # (an edge outside the window sets the deferred failure word: the
+                # next keyframe() / check_ba() raises)
                 key_kk, key_ij, ctx_idx, jslot = update_ops.window_keys(self.pg.ii, self.pg.jj, self.pg.kk, self.M,
-                                                                        self.n - 64, self.M * self.pmem, self.pmem)
+                                                                        self.n - 64, self.M * self.pmem, self.pmem,
+                                                                        flag=self._ba_fail)
                 kk_groups = update_ops.group_by(key_kk, key_bits=update_ops.key_bits_for(64 * self.M))
                 ij_groups = update_ops.group_by(key_ij, key_bits=12)
                 slots = (ctx_idx, jslot)

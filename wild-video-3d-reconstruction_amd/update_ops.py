@@ -163,9 +163,10 @@ def neighbors_csr(jj, offs, perm, groups, max_groups):
     return ix, jx
 
 
-def window_keys(ii, jj, kk, M, base, ring, frames):
+def window_keys(ii, jj, kk, M, base, ring, frames, flag=None):
     """(kk - M base, (ii - base) * 64 + (jj - base), kk mod ring, jj mod frames)
-    as int64 [E] each, in one launch (dpvo_window_keys)."""
+    as int64 [E] each, in one launch (dpvo_window_keys).  flag: optional int32
+    device word set to -2 (if 0) when an edge falls outside the key window."""
     H.on_gpu(ii, jj, kk)
     ii, jj, kk = H.idx64(ii), H.idx64(jj), H.idx64(kk)
     E = kk.numel()
@@ -173,7 +174,8 @@ def window_keys(ii, jj, kk, M, base, ring, frames):
         raise RuntimeError("window_keys: ii, jj and kk must have the same length")
     out = torch.empty(4, E, dtype=torch.int64, device=kk.device)
     H.check(H.lib().dpvo_window_keys(H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(M), int(base), int(ring), int(frames),
-                                     H.ptr(out[0]), H.ptr(out[1]), H.ptr(out[2]), H.ptr(out[3]), H.stream_of(kk)))
+                                     H.ptr(out[0]), H.ptr(out[1]), H.ptr(out[2]), H.ptr(out[3]), H.ptr(flag),
+                                     H.stream_of(kk)))
     return out[0], out[1], out[2], out[3]
 
 
