@@ -324,6 +324,14 @@ int dpvo_neighbors_csr(const int64_t* jj, const int* offs, const int* perm, cons
 int dpvo_softagg_csr(int dtype, const void* f, int64_t ldf, const void* s, int64_t lds, const int* offs,
                      const int* perm, const int64_t* groups, int64_t max_groups, int D, float eps, void* y,
                      void* stream);
+/* dpvo_softagg_csr for a few long groups (the update operator's frame-pair
+ * SoftAgg, ~190 edges per group at C3): groups of >= 64 edges are split over
+ * four waves whose online-softmax states are merged in a fixed order
+ * (deterministic; not bit-identical to dpvo_softagg_csr for those groups,
+ * identical for shorter ones).  fp16 or fp32. */
+int dpvo_softagg_csr_long(int dtype, const void* f, int64_t ldf, const void* s, int64_t lds, const int* offs,
+                          const int* perm, const int64_t* groups, int64_t max_groups, int D, float eps, void* y,
+                          void* stream);
 
 /* Full-row fused GEMM of the update operator (dpvo/net.py:75-93 and
  * blocks.py GatedResidual under autocast), N = 384 output columns per row:

@@ -190,3 +190,23 @@ def test_edge_targets_equal_torch_composition():
     centre = coords[..., 1, 1]
     t, w = update_ops.edge_targets(centre, delta, weight)
     assert torch.equal(t, centre + delta.float()) and torch.equal(w, weight.float())
+
+
+@pytest.mark.parametrize("ngroups", [50, 3000])
+def test_softagg_csr_long_groups(ngroups):
+    """softagg_csr(long_groups=True) (groups >= 64 edges split over four waves,
+    states merged in a fixed order): within the fp16 bar of the oracle,
+    repeatable bit for bit, and equal to the default kernel for short groups."""
+    import update_ops
+    E, D = 20000, 384
+    fs = torch.randn(E, 2 * D, device="cuda").half()
+    key = torch.randint(0, ngroups, (E,), device="cuda") * 12345 + 11
+    gid, offs, perm, G = update_ops.group_by(key)
+    g = int(G.item())
+    y = update_ops.softagg_csr(fs[:, :D], fs[:, D:], offs, perm, G, E, long_groups=True)[:g]
+    y2 = update_ops.softagg_csr(fs[:, :D], fs[:, D:], offs, perm, G, E, long_groups=True)[:g]
+    assert torch.equal(y, y2)
+    want = oracle.softagg(fs[:, :D].double().cpu().numpy(), fs[:, D:].double().cpu().numpy(), gid.cpu().numpy(), g)
+    np.testing.assert_allclose(y.double().cpu().numpy(), want, rtol=2e-3, atol=2e-3)
+    if ngroups == 3000:   # ~7 edges per group: the unsplit arithmetic
+        assert torch.equal(y, update_ops.softagg_csr(fs[:, :D], fs[:, D:], offs, perm, G, E)[:g])

@@ -71,6 +71,7 @@ _SIGNATURES = {
     "dpvo_group_by_workspace_bytes_for": (_sz, [_i64, _ip]),
     "dpvo_group_by": (_ip, [_vp, _i64, _ip, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dpvo_softagg_csr": (_ip, [_ip, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _ip, _fp, _vp, _vp]),
+    "dpvo_softagg_csr_long": (_ip, [_ip, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _ip, _fp, _vp, _vp]),
     "dpvo_neighbors_csr": (_ip, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),
     "dpvo_rowgemm": (_ip, [_vp, _vp]),
     "dpvo_rowgemm_pair": (_ip, [_vp, _vp, _vp]),

@@ -19,6 +19,8 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace dpvo {
@@ -465,6 +467,108 @@ __global__ __launch_bounds__(256) void sa_reduce_csr_kernel(const T* __restrict_
     }
 }
 
+// Online softmax-weighted sum over rows order[i0 .. i1) for the lane's two
+// channels, in SA_UNROLL batches from i0 (sa_reduce_csr_kernel's arithmetic).
+template <typename T>
+__device__ __forceinline__ void sa_online(const T* __restrict__ f, int64_t ldf, const T* __restrict__ s, int64_t lds,
+                                          const int* order, int i0b, int i1, int cc, float2_t& m, float2_t& l,
+                                          float2_t& acc)
+{
+    for (int i0 = i0b; i0 < i1; i0 += SA_UNROLL) {
+        float2_t sv[SA_UNROLL], fv[SA_UNROLL];
+#pragma unroll
+        for (int u = 0; u < SA_UNROLL; u++) {
+            const int64_t e = order[min(i0 + u, i1 - 1)];
+            sv[u] = Pair<T>::load(s + e * lds + cc);
+            fv[u] = Pair<T>::load(f + e * ldf + cc);
+        }
+        float2_t mb = m;
+#pragma unroll
+        for (int u = 0; u < SA_UNROLL; u++)
+            if (i0 + u < i1) {
+                mb.x = fmaxf(mb.x, sv[u].x);
+                mb.y = fmaxf(mb.y, sv[u].y);
+            }
+        const float ax = __expf(m.x - mb.x), ay = __expf(m.y - mb.y);
+        l.x *= ax; l.y *= ay; acc.x *= ax; acc.y *= ay;
+#pragma unroll
+        for (int u = 0; u < SA_UNROLL; u++)
+            if (i0 + u < i1) {
+                const float px = __expf(sv[u].x - mb.x), py = __expf(sv[u].y - mb.y);
+                l.x += px; l.y += py;
+                acc.x += px * fv[u].x; acc.y += py * fv[u].y;
+            }
+        m = mb;
+    }
+}
+
+// sa_reduce_csr_kernel with a workgroup per (group, 128-channel slice): groups
+// of at least SA_SPLIT rows are cut into four contiguous row ranges, one per
+// wave, whose (max, sum, weighted sum) states are merged in wave order -- the
+// long frame-pair groups (~190 rows at C3) run four times shorter chains of
+// dependent loads.  Shorter groups run on wave 0 alone with exactly
+// sa_reduce_csr_kernel's arithmetic (same bits).  Deterministic either way.
+constexpr int SA_SPLIT = 64;
+template <typename T>
+__global__ __launch_bounds__(256) void sa_reduce_csr_split_kernel(const T* __restrict__ f, int64_t ldf,
+                                                                  const T* __restrict__ s, int64_t lds,
+                                                                  const int* __restrict__ offs,
+                                                                  const int* __restrict__ perm,
+                                                                  const int64_t* __restrict__ groups, int D,
+                                                                  int slices, float eps, T* __restrict__ y)
+{
+    __shared__ float2_t st[4][3][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t ntask = *groups * slices;
+    for (int64_t task = blockIdx.x; task < ntask; task += gridDim.x) {
+        const int64_t g = task / slices;
+        const int c = (int)(task % slices) * 128 + 2 * lane;
+        const int b = offs[g], S = offs[g + 1] - b;
+        const int* order = perm + b;
+        const bool act = c < D;
+        const int cc = act ? c : 0;
+        float2_t m = {-INFINITY, -INFINITY}, l = {0.f, 0.f}, acc = {0.f, 0.f};
+        if (S < SA_SPLIT) {
+            if (wave == 0) {
+                sa_online<T>(f, ldf, s, lds, order, 0, S, cc, m, l, acc);
+                if (act) Pair<T>::store(y + g * (int64_t)D + c, float2_t{acc.x / (l.x + eps), acc.y / (l.y + eps)});
+            }
+            continue;   // S is uniform over the workgroup: every wave skips the barriers below together
+        }
+        const int q = (S + 3) / 4, r0 = min(S, wave * q), r1 = min(S, r0 + q);
+        sa_online<T>(f, ldf, s, lds, order, r0, r1, cc, m, l, acc);
+        st[wave][0][lane] = m;
+        st[wave][1][lane] = l;
+        st[wave][2][lane] = acc;
+        __syncthreads();
+        if (wave == 0) {
+            float2_t M = st[0][0][lane];
+#pragma unroll
+            for (int w = 1; w < 4; w++) {
+                M.x = fmaxf(M.x, st[w][0][lane].x);
+                M.y = fmaxf(M.y, st[w][0][lane].y);
+            }
+            float2_t L = {0.f, 0.f}, A = {0.f, 0.f};
+#pragma unroll
+            for (int w = 0; w < 4; w++) {
+                const float2_t mw = st[w][0][lane];
+                if (mw.x != -INFINITY) {
+                    const float a = __expf(mw.x - M.x);
+                    L.x += st[w][1][lane].x * a;
+                    A.x += st[w][2][lane].x * a;
+                }
+                if (mw.y != -INFINITY) {
+                    const float a = __expf(mw.y - M.y);
+                    L.y += st[w][1][lane].y * a;
+                    A.y += st[w][2][lane].y * a;
+                }
+            }
+            if (act) Pair<T>::store(y + g * (int64_t)D + c, float2_t{A.x / (L.x + eps), A.y / (L.y + eps)});
+        }
+        __syncthreads();   // the states are read before the next task overwrites them
+    }
+}
+
 }  // namespace
 }  // namespace dpvo
 
@@ -767,6 +871,28 @@ extern "C" int dpvo_edge_targets(const void* delta, int64_t delta_stride, const 
     hipLaunchKernelGGL(edge_targets_kernel, dim3(grid_for(E, 256, 4096)), dim3(256), 0, as_stream(stream),
                        (const half_t*)delta, delta_stride, (const half_t*)w, w_stride, centre, centre_stride,
                        centre_comp, E, target, weight);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_softagg_csr_long(int dtype, const void* f, int64_t ldf, const void* s, int64_t lds,
+                                     const int* offs, const int* perm, const int64_t* groups, int64_t max_groups,
+                                     int D, float eps, void* y, void* stream)
+{
+    DPVO_CHECK_ARG(D > 0 && D % 2 == 0, "feature dim must be even and positive");
+    DPVO_CHECK_ARG(ldf >= D && lds >= D && ldf % 2 == 0 && lds % 2 == 0, "row strides must be even and >= D");
+    DPVO_CHECK_ARG(groups != nullptr && offs != nullptr && perm != nullptr, "CSR missing");
+    DPVO_CHECK_ARG(dtype == DPVO_F16 || dtype == DPVO_F32, "dtype must be fp16 or fp32");
+    if (max_groups <= 0) return 0;
+    const int slices = (D + 127) / 128;
+    const unsigned grid = grid_for(max_groups * slices, 1, 8192);
+    if (dtype == DPVO_F16)
+        hipLaunchKernelGGL(sa_reduce_csr_split_kernel<half_t>, dim3(grid), dim3(256), 0, as_stream(stream),
+                           (const half_t*)f, ldf, (const half_t*)s, lds, offs, perm, groups, D, slices, eps,
+                           (half_t*)y);
+    else
+        hipLaunchKernelGGL(sa_reduce_csr_split_kernel<float>, dim3(grid), dim3(256), 0, as_stream(stream),
+                           (const float*)f, ldf, (const float*)s, lds, offs, perm, groups, D, slices, eps, (float*)y);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

@@ -117,7 +117,8 @@ class Update(nn.Module):
             else:
                 gid, offs, perm, G = ij_groups if ij_groups is not None else U.group_by(key, key_bits=ij_bits)
             f16, g16 = U.rowgemm_pair(n16, *pf, *pg_)
-            y = U.softagg_csr(f16, g16, offs, perm, G, E)
+            # frame-pair groups are few and long (~190 edges at C3): split over waves
+            y = U.softagg_csr(f16, g16, offs, perm, G, E, long_groups=key is not None)
             _, hy, _ = U.rowgemm(y, *ph, M_dev=G)
             n32, n16 = U.rowadd_ln(n32, hy, gid, ln=ln)
         # gru = LN0 (fused above), GatedResidual, LN1, GatedResidual; then the d / w heads

@@ -66,16 +66,17 @@ def group_by(key, key_bits=64, radix=False):
     return gid, offs, perm, groups
 
 
-def softagg_csr(f, s, offs, perm, groups, max_groups, eps=1e-12):
-    """softagg over group_by's CSR; y [max_groups, D], rows >= groups untouched."""
+def softagg_csr(f, s, offs, perm, groups, max_groups, eps=1e-12, long_groups=False):
+    """softagg over group_by's CSR; y [max_groups, D], rows >= groups untouched.
+    long_groups: split groups of >= 64 edges over four waves (dpvo_softagg_csr_long)."""
     H.on_gpu(f, s, offs, perm, groups)
     if f.dim() != 2 or s.shape != f.shape or f.dtype != s.dtype or f.stride(1) != 1 or s.stride(1) != 1:
         raise RuntimeError("softagg_csr: f and s must be [E, D] with channel-contiguous rows, same dtype")
     D = f.shape[1]
     y = torch.empty(max_groups, D, dtype=f.dtype, device=f.device)
-    H.check(H.lib().dpvo_softagg_csr(H.dtype_code(f), H.ptr(f), f.stride(0), H.ptr(s), s.stride(0), H.ptr(offs),
-                                     H.ptr(perm), H.ptr(groups), int(max_groups), D, float(eps), H.ptr(y),
-                                     H.stream_of(f)))
+    fn = H.lib().dpvo_softagg_csr_long if long_groups else H.lib().dpvo_softagg_csr
+    H.check(fn(H.dtype_code(f), H.ptr(f), f.stride(0), H.ptr(s), s.stride(0), H.ptr(offs), H.ptr(perm), H.ptr(groups),
+               int(max_groups), D, float(eps), H.ptr(y), H.stream_of(f)))
     return y
 
 
