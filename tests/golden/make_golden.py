@@ -27,6 +27,7 @@ Usage:  python tests/golden/make_golden.py
 """
 from __future__ import annotations
 
+import copy
 import importlib
 import os
 import sys
@@ -39,8 +40,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 REF = "/root/reference"
 sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
 
 from oracle import oracle  # noqa: E402
+import net_inputs as NI  # noqa: E402
 
 
 # ----------------------------------------------------------------------------
@@ -83,9 +86,35 @@ def _torch_scatter_module():
         out = torch.zeros(shape, dtype=src.dtype)
         return out.index_add_(dim, index, src)
 
+    def _bcast(index, src, dim):
+        # torch_scatter.utils.broadcast: a 1-D index along `dim`, expanded to src
+        view = [1] * src.dim()
+        view[dim] = -1
+        return index.view(view).expand_as(src)
+
+    def scatter_softmax(src, index, dim=-1, eps=1e-12, dim_size=None):
+        # torch-scatter 2.1.2 composite/softmax.py: recentre on the group max,
+        # exp, divide by (group sum + eps)
+        dim = dim % src.dim()
+        if dim_size is None:
+            dim_size = int(index.max()) + 1 if index.numel() else 0
+        idx = _bcast(index, src, dim)
+        shape = list(src.shape)
+        shape[dim] = dim_size
+        gmax = torch.zeros(shape, dtype=src.dtype).scatter_reduce(dim, idx, src, "amax", include_self=False)
+        ex = (src - gmax.gather(dim, idx)).exp()
+        den = scatter_sum(ex, index, dim, dim_size) + eps
+        return ex / den.gather(dim, idx)
+
     m.scatter_sum = scatter_sum
-    m.scatter_softmax = None
+    m.scatter_softmax = scatter_softmax
     return m
+
+
+def _neighbors_stub(ii, jj):
+    """cuda_ba.neighbors (ba.cpp:106-151) := the Python restatement below"""
+    ix, jx = neighbors_py(ii.cpu().numpy(), jj.cpu().numpy())
+    return [torch.from_numpy(ix), torch.from_numpy(jx)]
 
 
 def import_reference():
@@ -99,6 +128,7 @@ def import_reference():
         for attr in ["neighbors", "reproject", "forward", "backward", "patchify_forward", "patchify_backward"]:
             setattr(mod, attr, None)
         sys.modules[stub] = mod
+    sys.modules["cuda_ba"].neighbors = _neighbors_stub
     sys.path.insert(0, REF)
     pops = importlib.import_module("dpvo.projective_ops")
     ba = importlib.import_module("dpvo.ba")
@@ -351,10 +381,94 @@ def neighbors_fixtures():
     print("neighbors: vectors saved")
 
 
+# ----------------------------------------------------------------------------
+# the learned modules: reference Update (net.py:28-93) and BasicEncoder4
+# (extractor.py:200-264) executed as imported code
+# ----------------------------------------------------------------------------
+def _load(module, spec, seed):
+    params = NI.make_params(spec, seed)
+    sd = {k: torch.from_numpy(v) for k, v in params.items()}
+    module.load_state_dict(sd, strict=True)
+    return params
+
+
+def _err_stats(a, ref):
+    d = (np.asarray(a, np.float64) - np.asarray(ref, np.float64))
+    return np.array([np.sqrt((d ** 2).mean()), np.abs(d).max()])
+
+
+def update_fixtures():
+    """Update.forward (net.py:75-93) of the reference module on seeded
+    weights / inputs: in float64 (the exact answer) and under CPU fp16
+    autocast (the reference's own fp16 execution; its error against float64
+    is the scale the native fp16 path is held to)."""
+    net_mod = importlib.import_module("dpvo.net")
+    torch.manual_seed(0)
+    upd = net_mod.Update(3)
+    spec = NI.spec_json(upd.state_dict())
+    params = _load(upd, spec, NI.UPDATE_SEED)
+    ii, jj, kk = NI.update_edges()
+    E = len(ii)
+    net, inp, corr = NI.update_inputs(E)
+    T = torch.from_numpy
+    with torch.no_grad():
+        u64 = copy.deepcopy(upd).double()
+        n64, (d64, w64, _) = u64(T(net).double()[None], T(inp).double()[None], T(corr).double()[None], None,
+                                 T(ii), T(jj), T(kk))
+        with torch.autocast("cpu", dtype=torch.float16):
+            n16, (d16, w16, _) = upd(T(net)[None], T(inp)[None], T(corr)[None], None, T(ii), T(jj), T(kk))
+    rows = NI.update_rows(E)
+    n64, d64, w64 = n64[0].numpy(), d64[0].numpy(), w64[0].numpy()
+    n16, d16, w16 = n16[0].float().numpy(), d16[0].float().numpy(), w16[0].float().numpy()
+    ix, jx = neighbors_py(kk, jj)
+    np.savez_compressed(
+        os.path.join(HERE, "update_ref.npz"), spec=np.array(spec), seed=np.int64(NI.UPDATE_SEED),
+        param_checksum=np.stack([NI.checksum(params[k]) for k in sorted(params)]),
+        ii=ii, jj=jj, kk=kk, input_checksum=np.stack([NI.checksum(x) for x in (net, inp, corr)]),
+        rows=rows, net_out=n64[rows].astype(np.float32), delta=d64.astype(np.float32), weight=w64.astype(np.float32),
+        net_out64_rows_sum=n64[rows].sum(1), n_ix_neg=np.int64((ix < 0).sum()), n_jx_neg=np.int64((jx < 0).sum()),
+        amp_err_net=_err_stats(n16[rows], n64[rows]), amp_err_delta=_err_stats(d16, d64),
+        amp_err_weight=_err_stats(w16, w64))
+    print(f"update: reference Update.forward vectors saved, E = {E}; CPU-amp error rms/max net "
+          f"{_err_stats(n16, n64)}, delta {_err_stats(d16, d64)}, weight {_err_stats(w16, w64)}")
+
+
+def encoder_fixtures():
+    """fnet = BasicEncoder4(128, 'instance') and inet = BasicEncoder4(384,
+    'none') (net.py:100-101) of the reference on seeded weights, in float64,
+    on the Patchifier's input 2 (img / 255) - 0.5 and its /4 scale
+    (net.py:119-122): fmap (stored rows) and imap at the patch centres."""
+    ext = importlib.import_module("dpvo.extractor")
+    torch.manual_seed(0)
+    fnet = ext.BasicEncoder4(output_dim=128, norm_fn="instance")
+    inet = ext.BasicEncoder4(output_dim=384, norm_fn="none")
+    fspec, ispec = NI.spec_json(fnet.state_dict()), NI.spec_json(inet.state_dict())
+    fp = _load(fnet, fspec, NI.ENCODER_SEED)
+    ip = _load(inet, ispec, NI.ENCODER_SEED + 1)
+    out = dict(fspec=np.array(fspec), ispec=np.array(ispec),
+               param_checksum=np.stack([NI.checksum(d[k]) for d in (fp, ip) for k in sorted(d)]))
+    fnet, inet = fnet.double().eval(), inet.double().eval()
+    for f, (H, W, kind) in enumerate(NI.ENCODER_FRAMES):
+        img = NI.encoder_image(H, W, kind)
+        x = 2 * (torch.from_numpy(img).double()[None, None] / 255.0) - 0.5
+        with torch.no_grad():
+            fmap = (fnet(x) / 4.0)[0, 0].numpy()
+            imap = (inet(x) / 4.0)[0, 0].numpy()
+        h, w = fmap.shape[-2:]
+        xs, ys = NI.encoder_centres(h, w)
+        rows = NI.encoder_rows(h)
+        out.update({f"f{f}_image_checksum": NI.checksum(img), f"f{f}_hw": np.array([h, w]), f"f{f}_rows": rows,
+                    f"f{f}_fmap": fmap[:, rows].astype(np.float32), f"f{f}_xs": xs, f"f{f}_ys": ys,
+                    f"f{f}_imap": imap[:, ys, xs].T.astype(np.float32)})
+        print(f"encoders: frame {H}x{W} ({kind}) -> fmap {fmap.shape}, |fmap| max {np.abs(fmap).max():.3g}")
+    np.savez_compressed(os.path.join(HERE, "encoder_ref.npz"), **out)
+    print("encoders: reference BasicEncoder4 vectors saved")
+
+
 if __name__ == "__main__":
-    # python make_golden.py [part ...]: parts lietorch, pops, ba, altcorr, neighbors (default: all)
+    # python make_golden.py [part ...]: parts lietorch, pops, ba, altcorr, neighbors, update, encoder
     torch.set_num_threads(8)
-    parts = set(sys.argv[1:]) or {"lietorch", "pops", "ba", "altcorr", "neighbors"}
+    parts = set(sys.argv[1:]) or {"lietorch", "pops", "ba", "altcorr", "neighbors", "update", "encoder"}
     pops, ba, lie = import_reference()
     if "lietorch" in parts:
         lietorch_fixtures(lie)
@@ -366,3 +480,7 @@ if __name__ == "__main__":
         altcorr_fixtures()
     if "neighbors" in parts:
         neighbors_fixtures()
+    if "update" in parts:
+        update_fixtures()
+    if "encoder" in parts:
+        encoder_fixtures()

@@ -1,0 +1,123 @@
+"""Deterministic inputs and weights for the learned-module fixtures
+(update_ref.npz, encoder_ref.npz).
+
+Shared by tests/golden/make_golden.py (which runs the REFERENCE's own modules,
+dpvo/net.py:28-93 Update and dpvo/extractor.py:200-264 BasicEncoder4, on them
+in this container) and by the tests (which load the same weights into this
+repo's mirror modules and run the native HIP path).  Weights and inputs are
+regenerated from seeds with numpy's PCG64 instead of being stored: the
+fixtures then hold only the parameter spec (names + shapes, i.e. the
+reference's state_dict layout), checksums of what was generated, and the
+reference outputs.  Test infrastructure only.
+"""
+import json
+
+import numpy as np
+
+UPDATE_SEED = 31
+ENCODER_SEED = 41
+
+
+def spec_json(state_dict):
+    """the (name, shape) list of a torch state_dict, in its own order"""
+    return json.dumps([[k, list(v.shape)] for k, v in state_dict.items()])
+
+
+def make_params(spec, seed):
+    """name -> float32 array for every entry of `spec` (a spec_json string).
+
+    Linear / conv weights: U(-a, a) with a = 2 / sqrt(fan_in) (twice torch's
+    default bound, so LayerNorms, gates and ReLUs see O(1) activations);
+    1-D weights (LayerNorm gamma): U(0.5, 1.5); biases: U(-0.1, 0.1)
+    (LayerNorm beta included) -- non-trivial values everywhere, so a swapped
+    gamma / beta or a missing bias shows up in the outputs."""
+    g = np.random.default_rng(seed)
+    out = {}
+    for name, shape in json.loads(str(spec)):
+        shape = tuple(shape)
+        if name.endswith("weight") and len(shape) >= 2:
+            fan_in = int(np.prod(shape[1:]))
+            a = 2.0 / np.sqrt(fan_in)
+            out[name] = g.uniform(-a, a, size=shape).astype(np.float32)
+        elif name.endswith("weight"):
+            out[name] = g.uniform(0.5, 1.5, size=shape).astype(np.float32)
+        else:
+            out[name] = g.uniform(-0.1, 0.1, size=shape).astype(np.float32)
+    return out
+
+
+def update_edges(n=12, M=72, seed=UPDATE_SEED):
+    """Edge lists of the tracker's rules (dpvo.py:756-769) over n frames of M
+    patches, with ~8 % of the edges dropped at random (ragged groups, -1
+    neighbours inside a patch's run, frame-pair groups both >= 64 and < 64
+    edges long)."""
+    ii, jj, kk = [], [], []
+    for t in range(1, n + 1):
+        for k in range(M * max(t - 13, 0), M * max(t - 1, 0)):
+            kk.append(k); jj.append(t - 1); ii.append(k // M)
+        for k in range(M * (t - 1), M * t):
+            for j in range(max(t - 13, 0), t):
+                kk.append(k); jj.append(j); ii.append(k // M)
+    ii, jj, kk = (np.asarray(a, np.int64) for a in (ii, jj, kk))
+    g = np.random.default_rng(seed + 1)
+    keep = g.uniform(size=len(ii)) > 0.08
+    return ii[keep], jj[keep], kk[keep]
+
+
+def update_inputs(E, seed=UPDATE_SEED):
+    """net (fp32, the tracker's edge state dtype), inp (fp16, the context
+    rows) and corr (fp16, altcorr's 882-wide rows) for E edges."""
+    g = np.random.default_rng(seed + 2)
+    net = g.standard_normal((E, 384)).astype(np.float32)
+    inp = (0.5 * g.standard_normal((E, 384))).astype(np.float16)
+    corr = g.standard_normal((E, 882)).astype(np.float16)
+    return net, inp, corr
+
+
+def update_rows(E):
+    """the rows whose 384-wide outputs are stored (all rows' delta / weight are)"""
+    return np.unique(np.concatenate([np.arange(0, E, max(E // 1536, 1)), [E - 1]])).astype(np.int64)
+
+
+def texture_image(H, W, seed):
+    """uint8 [3, H, W]: smooth value noise (bilinear upsampled 1/16 grid) plus
+    pixel noise, the synthetic frame of SURVEY.md 8(d)"""
+    g = np.random.default_rng(seed)
+    gh, gw = H // 16 + 2, W // 16 + 2
+    coarse = g.uniform(0, 255, size=(3, gh, gw))
+    ys = np.linspace(0, gh - 1.001, H)
+    xs = np.linspace(0, gw - 1.001, W)
+    y0, x0 = ys.astype(int), xs.astype(int)
+    fy, fx = (ys - y0)[None, :, None], (xs - x0)[None, None, :]
+    c = coarse
+    img = ((1 - fy) * (1 - fx) * c[:, y0][:, :, x0] + (1 - fy) * fx * c[:, y0][:, :, x0 + 1] +
+           fy * (1 - fx) * c[:, y0 + 1][:, :, x0] + fy * fx * c[:, y0 + 1][:, :, x0 + 1])
+    img = img + g.normal(0, 12.0, size=img.shape)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+ENCODER_FRAMES = ((384, 512, "texture"), (100, 134, "noise"))
+
+
+def encoder_image(H, W, kind, seed=ENCODER_SEED):
+    if kind == "noise":
+        return np.random.default_rng(seed + H).integers(0, 256, size=(3, H, W)).astype(np.uint8)
+    return texture_image(H, W, seed + H)
+
+
+def encoder_centres(h, w, M=96, seed=ENCODER_SEED):
+    """patch centres as drawn by the Patchifier (net.py:151-152): x in [1, w-1), y in [1, h-1)"""
+    g = np.random.default_rng(seed + 7)
+    return g.integers(1, w - 1, size=M).astype(np.int64), g.integers(1, h - 1, size=M).astype(np.int64)
+
+
+def encoder_rows(h):
+    """fmap rows stored for the full-size frame (all rows for small frames)"""
+    if h <= 32:
+        return np.arange(h, dtype=np.int64)
+    return np.unique(np.concatenate([[0, 1, 2], np.arange(3, h - 3, 7), [h - 3, h - 2, h - 1]])).astype(np.int64)
+
+
+def checksum(a):
+    a = np.asarray(a, np.float64)
+    return np.array([a.sum(), np.abs(a).sum(), (a * np.arange(a.size).reshape(a.shape) % 7).sum()])

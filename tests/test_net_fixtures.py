@@ -1,0 +1,124 @@
+"""The mirror's learned modules against fixtures produced by the REFERENCE's
+own modules (tests/golden/make_golden.py: dpvo/net.py:28-93 ``Update`` and
+dpvo/extractor.py:200-264 ``BasicEncoder4`` imported and run in float64).
+
+CPU tests: the mirror modules (dpvo/net.py, dpvo/blocks.py, dpvo/extractor.py)
+take the reference's state_dict layout unchanged and, in float64 on the CPU,
+reproduce the reference outputs to rounding.  This pins the module structure
+(layer order, LayerNorm eps, residual order, gating, SoftAgg) that the native
+GPU path is built from; tests/test_gpu_net_fixtures.py then holds the native
+path itself to the same fixtures.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+sys.path.insert(0, GOLDEN)
+import net_inputs as NI  # noqa: E402
+
+
+def _fix(name):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+def _spec(model):
+    return [[k, list(v.shape)] for k, v in model.state_dict().items()]
+
+
+def _load(model, spec, seed):
+    params = NI.make_params(spec, seed)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=True)
+    return params
+
+
+def _neighbors_cpu(kk, jj):
+    """fastba.neighbors (ba.cpp:106-151) on the host: previous / next edge of
+    the same patch in stable jj order, -1 at the ends (test stand-in for the
+    device kernel, which tests/test_gpu_updateop.py checks separately)."""
+    kk_n, jj_n = kk.numpy(), jj.numpy()
+    order = np.lexsort((np.arange(len(kk_n)), jj_n, kk_n))
+    ix = np.full(len(kk_n), -1, np.int64)
+    jx = np.full(len(kk_n), -1, np.int64)
+    same = kk_n[order[1:]] == kk_n[order[:-1]]
+    ix[order[1:][same]] = order[:-1][same]
+    jx[order[:-1][same]] = order[1:][same]
+    return torch.from_numpy(ix), torch.from_numpy(jx)
+
+
+def test_update_fixture_spec_and_inputs():
+    """the mirror Update has the reference's state_dict layout (so dpvo.pth
+    loads), and the seeded weights / inputs regenerate bit for bit"""
+    from dpvo.net import Update
+    f = _fix("update_ref.npz")
+    spec = str(f["spec"])
+    assert _spec(Update(3)) == json.loads(spec)
+    params = NI.make_params(spec, int(f["seed"]))
+    np.testing.assert_array_equal(np.stack([NI.checksum(params[k]) for k in sorted(params)]), f["param_checksum"])
+    E = len(f["ii"])
+    ii, jj, kk = NI.update_edges()
+    assert np.array_equal(ii, f["ii"]) and np.array_equal(jj, f["jj"]) and np.array_equal(kk, f["kk"])
+    np.testing.assert_array_equal(np.stack([NI.checksum(x) for x in NI.update_inputs(E)]), f["input_checksum"])
+    # the edge set exercises what the operator's kernels special-case
+    _, counts = np.unique(ii * 12345 + jj, return_counts=True)
+    assert counts.max() >= 64 and counts.min() < 64          # long and short frame-pair groups
+    assert int(f["n_ix_neg"]) > 0 and int(f["n_jx_neg"]) > 0  # -1 neighbours
+
+
+def test_update_mirror_float64_matches_reference(monkeypatch):
+    """Update.forward of the mirror (torch path, float64, CPU) == the
+    reference module's float64 outputs"""
+    from dpvo import fastba
+    from dpvo.net import Update
+    f = _fix("update_ref.npz")
+    upd = Update(3)
+    _load(upd, str(f["spec"]), int(f["seed"]))
+    upd = upd.double()
+    monkeypatch.setattr(fastba, "neighbors", _neighbors_cpu)
+    ii, jj, kk = (torch.from_numpy(f[k]) for k in ("ii", "jj", "kk"))
+    net, inp, corr = (torch.from_numpy(x).double()[None] for x in NI.update_inputs(len(ii)))
+    # the torch path with autograd on (the inference path's SoftAgg is the HIP kernel)
+    net.requires_grad_(True)
+    out, (d, w, _) = upd(net, inp, corr, None, ii, jj, kk)
+    rows = torch.from_numpy(f["rows"])
+    np.testing.assert_allclose(out[0, rows].detach().numpy(), f["net_out"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(d[0].detach().numpy(), f["delta"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(w[0].detach().numpy(), f["weight"], rtol=1e-5, atol=1e-6)
+
+
+def test_encoder_fixture_spec():
+    from dpvo.extractor import BasicEncoder4
+    f = _fix("encoder_ref.npz")
+    assert _spec(BasicEncoder4(128, "instance")) == json.loads(str(f["fspec"]))
+    assert _spec(BasicEncoder4(384, "none")) == json.loads(str(f["ispec"]))
+    fp = NI.make_params(str(f["fspec"]), NI.ENCODER_SEED)
+    ip = NI.make_params(str(f["ispec"]), NI.ENCODER_SEED + 1)
+    np.testing.assert_array_equal(np.stack([NI.checksum(d[k]) for d in (fp, ip) for k in sorted(d)]),
+                                  f["param_checksum"])
+
+
+@pytest.mark.parametrize("frame", range(len(NI.ENCODER_FRAMES)))
+def test_encoder_mirror_float64_matches_reference(frame):
+    """fnet / inet of the mirror in float64 == the reference's (net.py:119-122
+    input scaling and /4 output scale included)"""
+    from dpvo.extractor import BasicEncoder4
+    f = _fix("encoder_ref.npz")
+    fnet, inet = BasicEncoder4(128, "instance"), BasicEncoder4(384, "none")
+    _load(fnet, str(f["fspec"]), NI.ENCODER_SEED)
+    _load(inet, str(f["ispec"]), NI.ENCODER_SEED + 1)
+    H, W, kind = NI.ENCODER_FRAMES[frame]
+    img = NI.encoder_image(H, W, kind)
+    np.testing.assert_array_equal(NI.checksum(img), f[f"f{frame}_image_checksum"])
+    x = 2 * (torch.from_numpy(img).double()[None, None] / 255.0) - 0.5
+    with torch.no_grad():
+        fmap = (fnet.double()(x) / 4.0)[0, 0].numpy()
+        imap = (inet.double()(x) / 4.0)[0, 0].numpy()
+    assert tuple(fmap.shape[-2:]) == tuple(f[f"f{frame}_hw"])
+    np.testing.assert_allclose(fmap[:, f[f"f{frame}_rows"]], f[f"f{frame}_fmap"], rtol=1e-5, atol=1e-6)
+    xs, ys = f[f"f{frame}_xs"], f[f"f{frame}_ys"]
+    np.testing.assert_allclose(imap[:, ys, xs].T, f[f"f{frame}_imap"], rtol=1e-5, atol=1e-6)
