@@ -10,6 +10,7 @@ the timed region (weak scaling); poses/points are gathered over RCCL after.
   python bench.py [--gpus N --steps K --warmup W]
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -25,11 +26,42 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "keyframes/s (altcorr+BA update loop), 512×384, 2048-KF buffer, 1/2/4/8 GPU"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA peak (MI355X_MICROARCH.md; no sparsity)
 C, P, LEVELS = 128, 3, 2
 # algorithmic bytes per edge of the fused 2-level altcorr launch:
 # gmap patch + 10x10 level-1 window + 9x9 level-2 window (fp16) + fp16 output + coords + ii/jj
 CORR_BYTES_PER_EDGE = 2 * C * (P * P + 10 * 10 + 9 * 9) + 2 * 2 * 49 * P * P + 4 * 2 * P * P + 8 * 2
+# the update operator per edge (net.py:75-93): multiply-adds of
+# its Linear layers (corr 882 -> 384, then 16 Linear(384, 384): corr x2, c1 x2, c2 x2,
+# SoftAgg f, g x2, GatedResidual gate + res x2 twice; d / w heads), and the bytes the
+# fused launches move per edge row (inputs read + outputs written, fp16 / fp32 as stored)
+UPD_MACS_PER_EDGE = 882 * 384 + 16 * 384 * 384 + 384 * 4
+UPD_MACS_PER_GROUP = 384 * 384   # SoftAgg's h Linear runs on the G groups only
+UPD_BYTES_PER_EDGE = (
+    (1792 + 768)                      # corr chain: corr rows in (896 fp16), h out (fp16)
+    + (768 + 1536 + 768 + 1536 + 768)  # corr Linear 3 + RES|LN: h, net32, ctx row in; net32, net16 out
+    + 2 * (768 + 1536 + 1536 + 768)    # c1, c2 chains: gathered row, net32 in; net32, net16 out
+    + 2 * (768 + 1536)                 # SoftAgg f|g pair GEMMs: net16 in, f16 | g16 out
+    + 2 * 1536                         # SoftAgg reduce: f, g rows in
+    + 2 * (1536 + 1536 + 768)          # rowadd_ln: net32 in; net32, net16 out
+    + (768 + 1536 + 1536 + 768)        # gated chain 1: net16, net32 in; net32, net16 out
+    + (768 + 1536 + 1536 + 8))         # gated chain 2: net16, net32 in; net32, heads out
+COUNTERS_JSON = os.path.join(REPO, "profiles", "counters_c3.json")
+
+
+def source_sha(*names):
+    """hash of the HIP sources a counter record was taken with (the record is
+    used only for the same kernel version)"""
+    h = hashlib.sha256()
+    for n in names:
+        with open(os.path.join(PKG, "csrc", n), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+CORR_SOURCES = ("corrmfma.hip", "altcorr.hip")
+UPD_SOURCES = ("rowgemm.hip", "updateop.hip")
 
 
 # BASELINE.json configs that fit one GPU (SURVEY 8d): preset, overrides, buffer, BA iterations
@@ -56,14 +88,36 @@ def parse():
                     help="replay update() from a HIP graph (captured in the warmup) instead of launching it eagerly")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-edges", type=int, default=1500)
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "altcorr_traffic.json"))
+    ap.add_argument("--counters-json", default=COUNTERS_JSON,
+                    help="rocprofv3 counter record of the same kernel versions (scripts/counters_json.py)")
+    ap.add_argument("--no-affinity", action="store_true", help="do not pin this rank's host threads")
     return ap.parse_args()
+
+
+def pin_host_cores(local, local_world):
+    """One process per GPU with its own host cores: the CPUs this
+    process may use are split into local_world contiguous blocks and rank
+    `local` keeps block `local` -- before any GPU call, so the HIP runtime's
+    threads inherit it.  Returns the core list (None if not pinned)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+    if local_world <= 1 or len(cpus) < local_world:
+        return cpus
+    per = len(cpus) // local_world
+    mine = cpus[local * per:(local + 1) * per]
+    os.sched_setaffinity(0, mine)
+    torch.set_num_threads(max(1, min(len(mine), torch.get_num_threads())))
+    return mine
 
 
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    args.cores = None if args.no_affinity else pin_host_cores(local, local_world)
     # one process per GPU; DPVO_BENCH_BACKEND=gloo (collectives through host
     # copies) lets the multi-rank path run with several ranks on one GPU (tests)
     local = local % max(torch.cuda.device_count(), 1)
@@ -114,18 +168,19 @@ def gather_to_rank0(tensors, rank, world):
 
 
 class CorrProbe:
-    """HIP events around every fused-altcorr launch, on the stream it runs on."""
+    """HIP events around every altcorr launch on the stream it runs on: the
+    fused 2-level kernel (dpvo.altcorr.corr_pyramid / corr_pyramid_mfma, called
+    by DPVO.corr) and the matrix-core path's edge ordering (cuda_corr.edge_order,
+    a counting sort of the edges by target frame that DPVO.corr runs first)."""
 
     def __init__(self):
-        self.pairs = []
+        self.pairs = {"corr": [], "order": []}
 
     def wrap(self, slam):
-        """Events bracket exactly the fused-altcorr launch (dpvo.altcorr.corr_pyramid
-        or corr_pyramid_mfma, called by DPVO.corr), on the current stream -- the
-        stream it runs on."""
+        import cuda_corr
         from dpvo import altcorr
 
-        def timed(inner):
+        def timed(inner, kind):
             def f(*a, **k):
                 # (ROCm torch refuses event-record nodes in a graph capture:
                 # a captured update() is timed per step only)
@@ -136,44 +191,60 @@ class CorrProbe:
                 s.record()
                 out = inner(*a, **k)
                 e.record()
-                self.pairs.append((s, e))
+                self.pairs[kind].append((s, e))
                 return out
             return f
-        altcorr.corr_pyramid = timed(altcorr.corr_pyramid)
-        altcorr.corr_pyramid_mfma = timed(altcorr.corr_pyramid_mfma)
+        altcorr.corr_pyramid = timed(altcorr.corr_pyramid, "corr")
+        altcorr.corr_pyramid_mfma = timed(altcorr.corr_pyramid_mfma, "corr")
+        cuda_corr.edge_order = timed(cuda_corr.edge_order, "order")
 
-    def mean_ms(self):
-        ts = [s.elapsed_time(e) for s, e in self.pairs]
-        return float(np.mean(ts)) if ts else float("nan")
+    def clear(self):
+        for v in self.pairs.values():
+            v.clear()
+
+    def mean_ms(self, kind="corr"):
+        ts = [s.elapsed_time(e) for s, e in self.pairs[kind]]
+        return float(np.mean(ts)) if ts else 0.0
 
 
 def phase_breakdown(slam, reps=5):
-    """Per-operator device time of one update, measured with events (outside the timed loop)."""
+    """Per-phase device time of one update, measured with events outside the
+    timed loop.  The phases follow DPVO.update() (dpvo/dpvo.py) step by step,
+    with the same arguments: reproject; the window keys and both group-bys;
+    altcorr (edge ordering + the fused kernel); the update operator; the BA
+    targets + fastba; the point cloud."""
+    import update_ops
     from dpvo import fastba
     from dpvo import projective_ops as pops
     from dpvo.lietorch import SE3
     ev = lambda: torch.cuda.Event(enable_timing=True)
-    import update_ops
-    acc = {k: [] for k in ("reproject", "group_by", "altcorr", "update_op", "fastba", "point_cloud")}
+    names = ("reproject", "group_by", "altcorr", "update_op", "fastba", "point_cloud")
+    acc = {k: [] for k in names}
+    assert slam._window_keys(), "phase_breakdown follows the window-key path of DPVO.update"
     for _ in range(reps):
-        e = [ev() for _ in range(7)]
+        slam._ba_status.zero_()
+        e = [ev() for _ in range(len(names) + 1)]
         e[0].record()
         coords = slam.reproject()
         e[1].record()
-        kk_groups = update_ops.group_by(slam.pg.kk, key_bits=update_ops.key_bits_for(slam.N * slam.M))
+        key_kk, key_ij, ctx_idx, jslot = update_ops.window_keys(slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M,
+                                                                slam.n - 64, slam.M * slam.pmem, slam.pmem,
+                                                                flag=slam._ba_status)
+        kk_groups = update_ops.group_by(key_kk, key_bits=update_ops.key_bits_for(64 * slam.M))
+        ij_groups = update_ops.group_by(key_ij, key_bits=12)
         e[2].record()
         with torch.autocast("cuda", enabled=True):
-            corr = slam.corr(coords)
+            corr = slam.corr(coords, slots=(ctx_idx, jslot))
             e[3].record()
-            ctx_idx = slam.pg.kk % (slam.M * slam.pmem)
             net, (delta, weight, _) = slam.network.update(slam.pg.net, slam.imap, corr, None, slam.pg.ii, slam.pg.jj,
                                                           slam.pg.kk, inp_idx=ctx_idx,
-                                                          index_bounds=(slam.N * slam.M, slam.N), kk_groups=kk_groups)
-        target = coords[..., 1, 1] + delta.float()
+                                                          index_bounds=(slam.N * slam.M, slam.N),
+                                                          kk_groups=kk_groups, ij_groups=ij_groups)
         e[4].record()
-        fastba.BA(slam.poses, slam.patches, slam.intrinsics, target, weight.float(), slam._lmbda, slam.pg.ii,
+        target, weight = update_ops.edge_targets(coords[..., P // 2, P // 2], delta, weight)
+        fastba.BA(slam.poses, slam.patches, slam.intrinsics, target, weight, slam._lmbda, slam.pg.ii,
                   slam.pg.jj, slam.pg.kk, max(slam.n - slam.cfg.OPTIMIZATION_WINDOW, 1), slam.n,
-                  slam.cfg.BA_ITERATIONS, csr=kk_groups[1:])
+                  slam.cfg.BA_ITERATIONS, csr=kk_groups[1:], status=slam._ba_status, keep_status=True)
         e[5].record()
         m = slam.pg.m
         pops.point_cloud_centre(SE3(slam.poses), slam.patches[:, :m], slam.intrinsics, slam.ix[:m],
@@ -182,7 +253,96 @@ def phase_breakdown(slam, reps=5):
         torch.cuda.synchronize()
         for k, (a, b) in zip(acc, zip(e[:-1], e[1:])):
             acc[k].append(a.elapsed_time(b))
+    slam.check_ba(int(slam._ba_status.item()))
     return {k: round(float(np.median(v)), 4) for k, v in acc.items()}
+
+
+def load_counters(path, edges):
+    """the rocprofv3 counter record (scripts/counters_json.py) if it was
+    taken on this workload with the current kernel sources, else None"""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as f:
+        rec = json.load(f)
+    if rec.get("edges") != edges:
+        return None
+    ok = {"corr": rec.get("sha", {}).get("corr") == source_sha(*CORR_SOURCES),
+          "update_op": rec.get("sha", {}).get("update_op") == source_sha(*UPD_SOURCES)}
+    return rec, ok
+
+
+def roofline_lines(slam, corr_ms, order_ms, breakdown, counters, path):
+    """The two roofline objects of the bench line.
+
+    altcorr (the matrix-core kernel + its edge ordering): HBM bytes measured
+    by rocprofv3 (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md's gfx950
+    correction) for the same kernel sources, divided by the phase time
+    measured here; the PMC shows the kernel bound by its vector-memory address
+    path (TA), so `bound` says so and `ta` reports that unit's busy fraction
+    from the same record.  The algorithmic bytes (no cross-edge
+    reuse) are reported beside it: the edge-grouped kernel reads each target
+    frame's window pixels once per XCD L2, so HBM sees ~30 % of them.
+
+    update operator: its fused launches' bytes (counter record when current,
+    else the per-launch model UPD_BYTES_PER_EDGE) over the phase time vs HBM
+    peak, and its Linear layers' flops vs the dense fp16 MFMA peak."""
+    E = slam.pg.ii.numel()
+    rec, ok = counters if counters else (None, {"corr": False, "update_op": False})
+    phase_ms = corr_ms + order_ms
+    alg = CORR_BYTES_PER_EDGE * E
+    corr = {"kernel": ("corr_sfast_kernel<2,16> (bit-exact fp16-chain altcorr)" if slam.cfg.EXACT_CORR
+                       else "corr_mfma_kernel (2-level altcorr on the matrix cores) + edge_order"),
+            "unit": "GB/s", "peak": HBM_PEAK_GBS, "avg_launch_ms": round(phase_ms, 5),
+            "kernel_ms": round(corr_ms, 5), "edge_order_ms": round(order_ms, 5),
+            "algorithmic_bytes": alg, "algorithmic_GBs": round(alg / (phase_ms * 1e-3) / 1e9, 1),
+            "bytes_per_edge": CORR_BYTES_PER_EDGE}
+    if ok["corr"] and not slam.cfg.EXACT_CORR:
+        c = rec["corr"]
+        traffic = c["hbm_bytes_per_launch"]
+        achieved = traffic / (phase_ms * 1e-3) / 1e9
+        corr.update({"bound": "ta", "achieved": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "basis": "HBM counter bytes (same kernel sources) / phase time",
+                     "ta": {"busy_frac": c.get("ta_busy_frac"),
+                            "note": "TA_BUSY_avr / kernel cycles per XCD: the address path is the binding unit"},
+                     "counters": os.path.relpath(path, REPO)})
+    else:
+        achieved = alg / (phase_ms * 1e-3) / 1e9
+        corr.update({"bound": "ta", "achieved": round(achieved, 1), "frac": None, "traffic": None,
+                     "basis": "no counter record for these kernel sources: algorithmic bytes only (no reuse "
+                              "model; not a utilisation)"})
+    upd_ms = breakdown["update_op"]
+    G = E // 22 + E // slam.M   # SoftAgg groups: ~E / 21.6 patches (SURVEY 8d: 497 M edges, 23 M patches) + ~E / M frame pairs
+    flops = 2.0 * (UPD_MACS_PER_EDGE * E + UPD_MACS_PER_GROUP * G)
+    upd_bytes = UPD_BYTES_PER_EDGE * E
+    upd = {"kernel": "update operator (rowchain / rowgemm3 / rowadd_ln / sa_reduce_csr launches)",
+           "bound": "latency (k-loop + row epilogue; see DESIGN.md)", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+           "phase_ms": upd_ms, "algorithmic_bytes": upd_bytes, "flops": flops,
+           "tflops": round(flops / (upd_ms * 1e-3) / 1e12, 1), "mfma_peak_tflops": MFMA_PEAK_TFLOPS,
+           "mfma_frac": round(flops / (upd_ms * 1e-3) / 1e12 / MFMA_PEAK_TFLOPS, 4)}
+    if ok["update_op"]:
+        traffic = rec["update_op"]["hbm_bytes_per_update"]
+        upd.update({"traffic": traffic, "basis": "HBM counter bytes of the operator's launches / phase time"})
+    else:
+        traffic = upd_bytes
+        upd.update({"traffic": None, "basis": "per-launch byte model (no counter record for these sources)"})
+    a = traffic / (upd_ms * 1e-3) / 1e9
+    upd.update({"achieved": round(a, 1), "frac": round(a / HBM_PEAK_GBS, 4)})
+    return corr, upd
+
+
+def _core_str(cores):
+    """compact core list: '0-15' / '0-3,8-11'"""
+    if not cores:
+        return None
+    runs, start, prev = [], cores[0], cores[0]
+    for c in cores[1:] + [None]:
+        if c is not None and c == prev + 1:
+            prev = c
+            continue
+        runs.append(f"{start}-{prev}" if prev != start else f"{start}")
+        if c is not None:
+            start = prev = c
+    return ",".join(runs)
 
 
 def _cpu_model():
@@ -374,7 +534,7 @@ def main():
     with torch.no_grad():
         for _ in range(max(args.warmup, 2 if args.graph else 0)):
             upd()
-        probe.pairs.clear()
+        probe.clear()
         barrier(world)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -386,12 +546,12 @@ def main():
         # every timed launch (eager); with --graph the captured launches are
         # not evented (ROCm torch has no event-record nodes), so the probe
         # falls back to a short eager pass after the loop
-        corr_ms = probe.mean_ms()
+        corr_ms, order_ms = probe.mean_ms("corr"), probe.mean_ms("order")
         if args.graph:
             for _ in range(3):
                 slam.update()
             torch.cuda.synchronize()
-            corr_ms = probe.mean_ms()
+            corr_ms, order_ms = probe.mean_ms("corr"), probe.mean_ms("order")
         slam.check_ba()
         breakdown = phase_breakdown(slam)
 
@@ -407,15 +567,11 @@ def main():
 
     if rank == 0:
         value = world * args.steps / elapsed
-        achieved = CORR_BYTES_PER_EDGE * E / (corr_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(args.traffic_json):
-            with open(args.traffic_json) as f:
-                tj = json.load(f)
-            if tj.get("edges") == E:
-                traffic = tj.get("hbm_bytes_per_launch")
+        counters = load_counters(args.counters_json, E)
+        roof, roof_upd = roofline_lines(slam, corr_ms, order_ms, breakdown, counters, args.counters_json)
+        metric = METRIC if args.buffer == 2048 else METRIC.replace("2048-KF buffer", f"{args.buffer}-KF buffer")
         line = {
-            "metric": METRIC, "value": round(value, 3), "unit": "keyframes/s", "n_gpus": world,
+            "metric": metric, "value": round(value, 3), "unit": "keyframes/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f16+f32",
             "launch": "hip-graph replay of update()" if args.graph else "eager",
@@ -425,13 +581,11 @@ def main():
                        "patches_per_frame": slam.M, "buffer": args.buffer, "n_keyframes": slam.n, "edges": E,
                        "ba_iterations": slam.cfg.BA_ITERATIONS, "image": "512x384",
                        "parallelism": f"replicas{world}"},
-            "roofline": {"kernel": ("corr_sfast_kernel<2,16> (bit-exact fp16-chain altcorr)" if slam.cfg.EXACT_CORR
-                                    else "corr_mfma_kernel (2-level altcorr on the matrix cores)"), "bound": "hbm",
-                         "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "bytes_per_edge": CORR_BYTES_PER_EDGE, "avg_launch_ms": round(corr_ms, 5)},
+            "roofline": roof,
+            "roofline_update_op": roof_upd,
             "breakdown_ms": breakdown,
             "fastba_us_per_iteration": round(breakdown["fastba"] * 1e3 / slam.cfg.BA_ITERATIONS, 2),
+            "host_cores": {"rank0": _core_str(args.cores), "cpu_model": _cpu_model()},
         }
         if gather_ms is not None:
             line["gather_ms"] = gather_ms

@@ -168,7 +168,10 @@ int dpvo_ba_forward(float* poses, float* patches, int64_t num_patches, int P, co
  * 32767 poses.  The sparse path reads the pose-graph bandwidth back to the
  * host once per call (one stream synchronisation); its status is the failing
  * leading-minor order as above. */
-enum { DPVO_BA_AUTO = 0, DPVO_BA_SPARSE = 1, DPVO_BA_ATOMIC = 2 };
+enum { DPVO_BA_AUTO = 0, DPVO_BA_SPARSE = 1, DPVO_BA_ATOMIC = 2, DPVO_BA_KEEP_STATUS = 4 };
+/* DPVO_BA_KEEP_STATUS (deterministic sliding-window path): *status is not
+ * cleared on entry; when it already holds a failure the call changes nothing
+ * (every kernel returns on entry) and the word keeps the earlier failure. */
 size_t dpvo_ba_workspace_bytes_ex(int64_t num_edges, int64_t num_patches, int num_opt_poses, int flags);
 int dpvo_ba_forward_ex(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
                        const float* target, const float* weight, const float* lmbda, const int64_t* ii,
@@ -333,6 +336,23 @@ int dpvo_softagg_csr_long(int dtype, const void* f, int64_t ldf, const void* s, 
                           const int* perm, const int64_t* groups, int64_t max_groups, int D, float eps, void* y,
                           void* stream);
 
+/* torch_scatter 2.1.2 over the CSR of dpvo_group_by(index) -- replaces the
+ * third-party scatter_sum / scatter_mean / scatter_max / scatter_softmax the
+ * reference calls (blocks.py:42-43, ba.py:40-56, long_term.py:134).
+ * src: [outer][E][inner] contiguous (scatter dim in the middle), index [E]
+ * int64 (1-D along the scatter dim).  op:
+ *   0 sum     out[o][index[e]][c] += sum over e           (out [outer][out_rows][inner])
+ *   1 mean    out[o][k][c] = (out + sum) / count           (keys with members)
+ *   2 max     out[o][k][c] = max, argmax[o][k][c] = e      (first maximum in edge order)
+ *   3 softmax out[o][e][c] = exp(src - gmax) / (gsum + eps) (out shaped like src)
+ * Rows of out whose key has no members are not written (the caller fills them:
+ * zeros, and argmax = E, as torch_scatter does).  Keys outside [0, out_rows)
+ * are skipped.  Sums run in fp32 (fp64 for fp64) in ascending edge order:
+ * deterministic.  dtype DPVO_F16 / F32 / F64. */
+int dpvo_scatter_csr(int op, int dtype, const void* src, int64_t outer, int64_t E, int64_t inner, const int64_t* index,
+                     const int* offs, const int* perm, const int64_t* groups, int64_t max_groups, float eps, void* out,
+                     int64_t out_rows, int64_t* argmax, void* stream);
+
 /* Full-row fused GEMM of the update operator (dpvo/net.py:75-93 and
  * blocks.py GatedResidual under autocast), N = 384 output columns per row:
  *   y16  = fp16(A W^T + bias)            A fp16 [M][K] rows at A + r*lda, or
@@ -382,6 +402,18 @@ int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_args* b, vo
  * written.  g2: W ([384][384]), bias, flags and every epilogue input / output
  * of dpvo_rowgemm (its A, M and M_dev are taken from g1). */
 int dpvo_rowchain(const dpvo_rowgemm_args* first, const dpvo_rowgemm_args* second, void* stream);
+
+/* Three chained rowgemms: the update operator's corr MLP and the first
+ * LayerNorm (net.py:54-61,78-79) in one launch,
+ *   h1 = act1(A W1^T + b1);  h2 = fp16(relu(LN2(fp16(h1 W2^T + b2))));
+ *   Y  = epi3(h2 W3^T + b3)
+ * with h1 and h2 kept on chip.  first: as dpvo_rowchain's; middle: W, bias,
+ * flags == DPVO_RG_LN | DPVO_RG_LN_RELU and ln_g / ln_b / ln_eps; last: W,
+ * bias, flags == DPVO_RG_RES | DPVO_RG_LN and every epilogue input / output
+ * of dpvo_rowgemm.  Bit-identical to dpvo_rowchain(first, middle) writing
+ * fp16 rows followed by dpvo_rowgemm(those rows, last). */
+int dpvo_rowchain3(const dpvo_rowgemm_args* first, const dpvo_rowgemm_args* middle, const dpvo_rowgemm_args* last,
+                   void* stream);
 
 /* The GRU's GatedResidual (blocks.py:27-30) in one launch:
  *   gate = sigmoid(fp16(A Wg^T + bg)),  Y = epi2(act1(A W1^T + b1) W2^T + b2)

@@ -133,3 +133,21 @@ def test_native_encoder_rejects_bad_inputs():
         enc.run(torch.zeros(3, 64, 64, device="cuda"), xs, xs)
     with pytest.raises(RuntimeError, match="GPU"):
         enc.run(torch.zeros(3, 64, 64, dtype=torch.uint8), xs.cpu(), xs.cpu())
+
+
+def test_patchifier_float_frames_take_the_torch_encoders():
+    """float frames (the reference accepts any dtype) run the torch encoders,
+    eagerly and from the captured graph, instead of failing the native gate
+    """
+    pf = _nets()
+    img = _image(96, 128, "texture")
+    with torch.no_grad(), torch.autocast("cuda", enabled=True):
+        for graphed in (False, True):
+            pf.graphed = graphed
+            torch.manual_seed(3)
+            a = pf(img.float(), patches_per_image=16)
+            torch.manual_seed(3)
+            b = pf(img, patches_per_image=16)
+            assert a[0].shape == b[0].shape and torch.isfinite(a[0]).all()
+            d = (a[0].float() - b[0].float()).abs().max().item()
+            assert d <= 2e-2 * b[0].float().abs().max().item()

@@ -295,3 +295,56 @@ def test_rowchain_gated_is_gate_gemm_plus_chain(M, last):
             assert torch.equal(r, g)
     with pytest.raises(RuntimeError):
         U.rowchain(A, W1, b1, W2, b2, flags1=U.RELU, gate16=g16, gate=(Wg, bg), **kw)
+
+
+@pytest.mark.parametrize("M", [1, 1000, 95424])
+@pytest.mark.parametrize("gathered", [False, True])
+def test_rowchain3_is_chain_plus_rowgemm(M, gathered):
+    """dpvo_rowchain3 (the corr MLP of net.py:54-61 and norm(net + inp + .),
+    :78-79, in one launch: both intermediates and the middle LayerNorm on
+    chip) is bit-identical to rowchain(LN | LN_RELU) writing fp16 rows
+    followed by rowgemm(RES | LN) with the context-row gather."""
+    import update_ops as U
+    torch.manual_seed(5)
+    dev = "cuda"
+    A = torch.zeros(M, 896, device=dev, dtype=torch.float16)
+    A[:, :882] = (torch.randn(M, 882, device=dev) * 0.7).half()
+    W1, b1 = U.pack_linear(torch.randn(384, 882, device=dev) / 30.0, torch.randn(384, device=dev) * 0.1)
+    Wm, bm = U.pack_linear(torch.randn(384, 384, device=dev) / 20.0, torch.randn(384, device=dev) * 0.1)
+    W3, b3 = U.pack_linear(torch.randn(384, 384, device=dev) / 20.0, torch.randn(384, device=dev) * 0.1)
+    lnm = (torch.rand(384, device=dev) + 0.5, torch.randn(384, device=dev) * 0.1, 1e-3)
+    ln3 = (torch.rand(384, device=dev) + 0.5, torch.randn(384, device=dev) * 0.1, 1e-3)
+    res32 = torch.randn(M, 384, device=dev)
+    ring = torch.randn(max(M, 64) + 17, 384, device=dev).half()
+    idx = torch.randint(0, ring.shape[0], (M,), device=dev) if gathered else None
+    res16 = ring if gathered else ring[:M].contiguous()
+    kw = dict(flags=U.RES | U.LN, res32=res32, res16=res16, res16_idx=idx, ln=ln3, want32=True)
+    _, h, _ = U.rowchain(A, W1, b1, Wm, bm, flags1=U.RELU, flags=U.LN | U.LN_RELU, ln=lnm)
+    ref = U.rowgemm(h, W3, b3, **kw)
+    got = U.rowchain(A, W1, b1, W3, b3, flags1=U.RELU, mid=(Wm, bm, lnm), **kw)
+    for r, g in zip(ref, got):
+        assert (r is None) == (g is None)
+        if r is not None:
+            assert torch.equal(r, g)
+
+
+def test_update_operator_corr_chain3_is_two_launches():
+    """Update.forward's fused path with the three-GEMM corr chain equals the
+    two-launch path bit for bit"""
+    from dpvo.net import Update
+    from dpvo.synthetic import steady_state_edges
+    torch.manual_seed(6)
+    upd = Update(3).cuda()
+    ii, jj, kk = steady_state_edges(40, 16, 13, 22, "cuda")
+    E = ii.numel()
+    net = torch.randn(1, E, 384, device="cuda")
+    inp = torch.randn(1, E, 384, device="cuda").half()
+    corr = torch.randn(1, E, 882, device="cuda").half()
+    outs = []
+    for chain3 in (True, False):
+        Update.CORR_CHAIN3 = chain3
+        with torch.no_grad(), torch.autocast("cuda", enabled=True):
+            outs.append(upd(net, inp, corr, None, ii, jj, kk))
+    Update.CORR_CHAIN3 = True
+    (a, (da, wa, _)), (b, (db, wb, _)) = outs
+    assert torch.equal(a, b) and torch.equal(da, db) and torch.equal(wa, wb)

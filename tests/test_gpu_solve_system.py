@@ -41,3 +41,19 @@ def test_solve_system_self_edge_raises():
     t = lambda a: torch.from_numpy(a).cuda()
     with pytest.raises(RuntimeError):
         cuda_ba.solve_system(t(Ji), t(Jj), t(ii), t(jj), t(res), 1e-4, 1e-3, -1)
+
+
+def test_solve_system_accepts_host_tensors():
+    """The reference copies its inputs to the host and returns on res.device
+    (ba.cpp:153-234); PGO may hand CPU tensors (optim_utils.py:222-255)."""
+    import cuda_ba
+    Ji, Jj, ii, jj, res = _pgo_case(30, 6, seed=5)
+    want = oracle.solve_system(Ji, Jj, ii, jj, res, 1e-4, 1e-3, -1)
+    t = torch.from_numpy
+    got, = cuda_ba.solve_system(t(Ji), t(Jj), t(ii), t(jj), t(res), 1e-4, 1e-3, -1)
+    assert got.device.type == "cpu" and got.shape == (30, 7)
+    np.testing.assert_allclose(got.numpy(), want, rtol=1e-4, atol=1e-5)
+    # mixed placement: Jacobians on the host, residuals on the GPU -> result on the GPU
+    got2, = cuda_ba.solve_system(t(Ji), t(Jj), t(ii), t(jj), t(res).cuda(), 1e-4, 1e-3, -1)
+    assert got2.device.type == "cuda"
+    np.testing.assert_allclose(got2.cpu().numpy(), want, rtol=1e-4, atol=1e-5)

@@ -68,3 +68,42 @@ def test_deferred_ba_failure_raises_at_the_next_host_read():
         slam._ba_fail.fill_(-1)
         with pytest.raises(RuntimeError, match="patch index out of range"):
             slam.check_ba()
+
+
+def test_window_violation_skips_ba_and_raises():
+    """An edge outside the 64-frame key window: the window-key
+    check writes the BA status word first, BA leaves poses / depths alone, and
+    the next host read raises the window error."""
+    slam = make(seed=8)
+    with torch.no_grad():
+        slam.update()
+        slam.check_ba()
+        # patch 0 of the oldest stored frame as an edge target: ii = 0 < n - 64
+        slam.pg.ii[0] = 0
+        slam.pg.kk[0] = 0
+        poses0 = slam.pg.poses_[:slam.n].clone()
+        depth0 = slam.pg.patches_[:slam.n].clone()
+        slam.update()
+        torch.cuda.synchronize()
+        assert torch.equal(slam.pg.poses_[:slam.n], poses0)
+        assert torch.equal(slam.pg.patches_[:slam.n], depth0)
+        with pytest.raises(RuntimeError, match="64-frame key window"):
+            slam.check_ba()
+
+
+def test_update_get_corr():
+    """dpvo.py:660-687: one update, BA failure reported as a warning, the
+    point cloud of all stored patches and the BA targets returned"""
+    a, b = make(seed=9), make(seed=9)
+    with torch.no_grad():
+        a.update()
+        pts, target = b.update_get_corr()
+    torch.cuda.synchronize()
+    m = a.pg.m
+    assert pts.shape == (m, 3) and target.shape == (1, a.pg.ii.numel(), 2)
+    assert torch.equal(pts, a.pg.points_[:m]) and torch.equal(target, a.pg.target)
+    assert torch.equal(b.pg.poses_[:b.n], a.pg.poses_[:a.n])
+    with torch.no_grad():
+        b._ba_fail.fill_(7)                    # as if this update's BA had failed: caught, as in the reference
+        b.update_get_corr()
+    b.check_ba()                               # the failure was consumed by the warning

@@ -73,9 +73,11 @@ _SIGNATURES = {
     "dpvo_softagg_csr": (_ip, [_ip, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _ip, _fp, _vp, _vp]),
     "dpvo_softagg_csr_long": (_ip, [_ip, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _ip, _fp, _vp, _vp]),
     "dpvo_neighbors_csr": (_ip, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp]),
+    "dpvo_scatter_csr": (_ip, [_ip, _ip, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _fp, _vp, _i64, _vp, _vp]),
     "dpvo_rowgemm": (_ip, [_vp, _vp]),
     "dpvo_rowgemm_pair": (_ip, [_vp, _vp, _vp]),
     "dpvo_rowchain": (_ip, [_vp, _vp, _vp]),
+    "dpvo_rowchain3": (_ip, [_vp, _vp, _vp, _vp]),
     "dpvo_rowchain_gated": (_ip, [_vp, _vp, _vp, _vp]),
     "dpvo_rowadd_ln": (_ip, [_vp, _vp]),
     "dpvo_edge_targets": (_ip, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp]),

@@ -2216,7 +2216,10 @@ extern "C" int dpvo_ba_forward_csr(float* poses, float* patches, int64_t num_pat
         p.lmbda = lmbda; p.ii = ii; p.jj = jj; p.kk = kk; p.num_patches = num_patches; p.mu_max = L.mu_max;
         p.P = P; p.t0 = t0; p.N = N; p.n6 = L.n6; p.nup = L.nup; p.ent = L.ent;
         p.status = status ? status : (int*)(ws + L.hdr) + HDR_STATUS;
-        DPVO_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int), s));
+        // KEEP_STATUS: the caller's word may already hold a failure (the
+        // tracker's window-key check); every bd_* kernel returns on entry when
+        // it is non-zero, so the call then leaves poses and patches untouched
+        if (!(status && (flags & DPVO_BA_KEEP_STATUS))) DPVO_CHECK_HIP(hipMemsetAsync(p.status, 0, sizeof(int), s));
         if (num_edges == 0 || iterations == 0) return 0;
         return ba_forward_det(p, ws, L, num_edges, csr_offs, csr_perm, csr_groups, iterations, s);
     }

@@ -970,12 +970,21 @@ struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflic
 // residual like RES, which is bit-for-bit the GATE epilogue's
 // x + fp16(gate * y) without the 73 MB gate16 round trip (nor a gate held in
 // registers across the GEMMs).
+// TRI (the corr MLP of net.py:54-61 and the `norm(net + inp + corr(.))` of
+// :78-79 in one launch): pg is then the MIDDLE Linear -- GEMM2 runs with pg's
+// W and bias, its y tile gets pg's row epilogue in place (LayerNorm -> ReLU,
+// rounded to fp16: the A operand the next Linear casts to under autocast),
+// then a third GEMM on that tile with p's W and bias feeds p's epilogue.
+// Bit-identical to rowchain (corr0, corr1, LN|LN_RELU) -> fp16 rows ->
+// rowgemm (corr2, RES|LN): the same MFMA k order and the same epilogue code.
 // DBG (timing experiments only, DPVO_RC_DBG, flag RES; scripts/bench_rc_dbg.py):
 // 1 no row pass, 2 no MFMA, 3 neither
-template <int F2, bool GATED = false, int DBG = 0>
+template <int F2, bool GATED = false, int DBG = 0, int FMID = 0>
 __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
                                                                  dpvo_rowgemm_args pg)
 {
+    constexpr bool TRI = FMID != 0;
+    static_assert(!(TRI && GATED), "a chain is either gated or three GEMMs long");
     __shared__ __attribute__((aligned(16))) char smem[RC_LDS];
     typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -985,8 +994,10 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
     const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
     if ((int64_t)blockIdx.x >= ntiles) return;
     const half_t* __restrict__ W1 = (const half_t*)p1.W;
-    const half_t* __restrict__ W2 = (const half_t*)p.W;
+    const half_t* __restrict__ W2 = (const half_t*)(TRI ? pg.W : p.W);
     const half_t* __restrict__ zero = (const half_t*)p1.zero_row;
+    // TRI: the third GEMM's W stages come from p.W ([384][384] like W2)
+    const int64_t w3delta = TRI ? (const half_t*)p.W - W2 : 0;
     const YMapChunk ym;
     // piece (1 KB = 16 rows x 64 B) lane mapping: row base + L/4, physical chunk
     // L%4 holding logical chunk (L%4) ^ ((row>>2)&3)
@@ -1033,9 +1044,9 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         for (int j = 0; j < 4; j++)
             glds16(g1src[j] + k0 + (GATED && gate && 4 * wave + j >= 8 ? gdelta : 0), st + (4 * wave + j) * 1024);
     };
-    auto issue2 = [&](int ks, int buf) {
+    auto issue2 = [&](int ks, int buf, int64_t wdelta = 0) {
         char* st = smem + RC_Y + buf * RC_STAGE + RC_A_STAGE;
-        const int k0 = ks * RC_BK;
+        const int64_t k0 = ks * RC_BK + wdelta;
 #pragma unroll
         for (int j = 0; j < 3; j++) glds16(w2src[j] + k0, st + (3 * wave + j) * 1024);
     };
@@ -1097,6 +1108,45 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             }
         }
     };
+    // TRI: LayerNorm (+ ReLU) of the y tile's rows in place, rounded to fp16 --
+    // epi2_finish's LN arithmetic (two rows per wave pass, lane s of half h
+    // owning columns 4 s + 128 j), the result written back instead of stored
+    auto mid_rows = [&](const dpvo_rowgemm_args& pm) {
+        if (!TRI) return;
+        EpiConsts2 km;
+        load_consts2<FMID>(pm, lane, km);
+        const int h = lane >> 5, s = lane & 31;
+#pragma unroll 1
+        for (int i = 0; i < 8; i++) {
+            const int r = wave * 16 + 2 * i + h;
+            ep_f4 v[3];
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const ep_h4 y = *(const ep_h4*)(smem + ym.off(r, (128 * j + 4 * s) * 2));
+                v[j] = ep_f4{(float)y[0], (float)y[1], (float)y[2], (float)y[3]};
+            }
+            float sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; j++) sm += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+            const float mean = half_sum(sm) * (1.f / RG_BN);
+            float sq = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const ep_f4 d = v[j] - mean;
+                sq += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+            }
+            const float rstd = rsqrtf(half_sum(sq) * (1.f / RG_BN) + pm.ln_eps);
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                v[j] = (v[j] - mean) * rstd * km.g[j] + km.b[j];
+                if (FMID & RG_LN_RELU)
+#pragma unroll
+                    for (int t = 0; t < 4; t++) v[j][t] = fmaxf(v[j][t], 0.f);
+                *(ep_h4*)(smem + ym.off(r, (128 * j + 4 * s) * 2)) =
+                    ep_h4{(half_t)v[j][0], (half_t)v[j][1], (half_t)v[j][2], (half_t)v[j][3]};
+            }
+        }
+    };
     auto gemm1 = [&](bool gate) {
         for (int ks = 0; ks < ks1; ks++) {
             if (ks + 1 < ks1) {
@@ -1129,26 +1179,40 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         acc_to_y((const half_t*)p1.bias, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
         issue2(0, 0);
         sync_lds();
-        // ---- GEMM2: y tile x W2
-        zero_acc();
+        // ---- GEMM2: y tile x W2 (stage 0 already issued); wdelta selects W3
+        auto gemm_y = [&](int64_t wdelta) {
+            zero_acc();
 #pragma unroll 1
-        for (int ks = 0; ks < ks2; ks++) {
-            if (ks + 1 < ks2) {
-                issue2(ks + 1, (ks + 1) & 1);
-                asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            for (int ks = 0; ks < ks2; ks++) {
+                if (ks + 1 < ks2) {
+                    issue2(ks + 1, (ks + 1) & 1, wdelta);
+                    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                const char* st = smem + RC_Y + (ks & 1) * RC_STAGE;
+                h8_t a[4], b[6];
+#pragma unroll
+                for (int mt = 0; mt < 4; mt++)
+                    a[mt] = *(const h8_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, (ks * 4 + fq) * 16));
+#pragma unroll
+                for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+                mfma_step(a, b);
+                __builtin_amdgcn_s_barrier();
             }
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            const char* st = smem + RC_Y + (ks & 1) * RC_STAGE;
-            h8_t a[4], b[6];
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, (ks * 4 + fq) * 16));
-#pragma unroll
-            for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
-            mfma_step(a, b);
-            __builtin_amdgcn_s_barrier();
+        };
+        gemm_y(0);
+        if (TRI) {
+            // the middle Linear's output -> its row epilogue (LayerNorm, ReLU) in
+            // place on the y tile -> the third GEMM's A operand
+            acc_to_y((const half_t*)pg.bias, false, false);
+            issue2(0, 0, w3delta);   // stage 0 of W3 loads under the row pass
+            sync_lds();
+            mid_rows(pg);
+            sync_lds();
+            gemm_y(w3delta);
         }
         acc_to_y((const half_t*)p.bias, F2 & RG_RELU, F2 & RG_SIGMOID);
         if (GATED) {
@@ -1875,6 +1939,48 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
 extern "C" int dpvo_rowchain(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args* g2, void* stream)
 {
     return rowchain_launch(g1, g2, nullptr, stream);
+}
+
+extern "C" int dpvo_rowchain3(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args* g2, const dpvo_rowgemm_args* g3,
+                              void* stream)
+{
+    DPVO_CHECK_ARG(g1 != nullptr && g2 != nullptr && g3 != nullptr, "rowchain3: null args");
+    DPVO_CHECK_ARG(g2->N == RG_BN && g2->K == RG_BN && g2->W && g2->bias && ((uintptr_t)g2->W & 15) == 0 &&
+                       ((uintptr_t)g2->bias & 7) == 0,
+                   "rowchain3: the middle Linear needs W [384][384] (16-byte aligned) and bias (8-byte aligned)");
+    DPVO_CHECK_ARG(g2->flags == (DPVO_RG_LN | DPVO_RG_LN_RELU) && g2->ln_g && g2->ln_b &&
+                       ((uintptr_t)g2->ln_g & 15) == 0 && ((uintptr_t)g2->ln_b & 15) == 0,
+                   "rowchain3: the middle epilogue must be LN | LN_RELU with 16-byte aligned LayerNorm parameters");
+    DPVO_CHECK_ARG(g3->flags == (DPVO_RG_RES | DPVO_RG_LN), "rowchain3: the last epilogue must be RES | LN");
+    DPVO_CHECK_ARG(g1->N == RG_BN && g3->N == RG_BN, "rowchain3: output widths must be 384");
+    DPVO_CHECK_ARG(g1->K > 0 && g1->K % RC_BK == 0, "rowchain3: K1 must be a positive multiple of 32");
+    DPVO_CHECK_ARG(g3->K == RG_BN, "rowchain3: the last GEMM's K must be 384");
+    DPVO_CHECK_ARG(g1->A && g1->W && g1->bias && g1->zero_row && g3->W && g3->bias,
+                   "rowchain3: A, the three W, the biases and zero_row are required");
+    DPVO_CHECK_ARG(g1->lda >= g1->K && g1->lda % 8 == 0, "rowchain3: lda must be >= K1 and a multiple of 8");
+    DPVO_CHECK_ARG(((uintptr_t)g1->A & 15) == 0 && ((uintptr_t)g1->W & 15) == 0 && ((uintptr_t)g3->W & 15) == 0 &&
+                       ((uintptr_t)g1->zero_row & 15) == 0,
+                   "rowchain3: A, W1, W3 and zero_row must be 16-byte aligned");
+    DPVO_CHECK_ARG(((uintptr_t)g1->bias & 7) == 0 && ((uintptr_t)g3->bias & 7) == 0,
+                   "rowchain3: biases must be 8-byte aligned");
+    DPVO_CHECK_ARG((g1->flags & ~(DPVO_RG_RELU | DPVO_RG_SIGMOID)) == 0,
+                   "rowchain3: the first GEMM takes only an activation");
+    DPVO_CHECK_ARG(g3->res32 && g3->ln_g && g3->ln_b, "rowchain3: residual input / LayerNorm weights missing");
+    DPVO_CHECK_ARG(!g3->out16 || (g3->ldo16 % 4 == 0 && ((uintptr_t)g3->out16 & 7) == 0),
+                   "rowchain3: out16 needs 8-byte aligned rows (ldo16 % 4 == 0)");
+    DPVO_CHECK_ARG(!g3->out32 || (g3->ldo32 % 4 == 0 && ((uintptr_t)g3->out32 & 15) == 0),
+                   "rowchain3: out32 needs 16-byte aligned rows (ldo32 % 4 == 0)");
+    if (g1->M <= 0) return 0;
+    if (ensure_num_cus()) return -1;
+    const int64_t ntiles = (g1->M + RG_BM - 1) / RG_BM;
+    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+    dpvo_rowgemm_args a3 = *g3;
+    a3.M = g1->M;
+    a3.M_dev = g1->M_dev;
+    hipLaunchKernelGGL((rowchain_kernel<DPVO_RG_RES | DPVO_RG_LN, false, 0, DPVO_RG_LN | DPVO_RG_LN_RELU>), dim3(grid),
+                       dim3(RG_THREADS), 0, as_stream(stream), *g1, a3, *g2);
+    DPVO_CHECK_LAUNCH();
+    return 0;
 }
 
 extern "C" int dpvo_rowchain_gated(const dpvo_rowgemm_args* gate, const dpvo_rowgemm_args* g1,

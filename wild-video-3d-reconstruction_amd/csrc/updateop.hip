@@ -375,6 +375,7 @@ constexpr int CB_WAVES = 4;
 __global__ __launch_bounds__(64 * CB_WAVES) void cb_fix_kernel(const int* __restrict__ ptmp,
                                                                const int* __restrict__ offs,
                                                                const int64_t* __restrict__ groups,
+                                                               const int64_t* __restrict__ gid, int64_t n,
                                                                int* __restrict__ perm)
 {
     __shared__ __attribute__((aligned(16))) int buf[CB_WAVES][CB_CAP];
@@ -406,11 +407,27 @@ __global__ __launch_bounds__(64 * CB_WAVES) void cb_fix_kernel(const int* __rest
             }
             __builtin_amdgcn_wave_barrier();   // every lane's reads before the next group's writes
         } else {
+            // more than CB_CAP members: they are the edges e with gid[e] == g, so a
+            // scan of gid over [first member, last member] in ascending e emits
+            // them in order -- O(span / 64) per group, at most n / CB_CAP such
+            // groups (a rank by comparison would be O(S^2))
+            int lo = INT_MAX, hi = -1;
             for (int i = lane; i < S; i += 64) {
                 const int v = ptmp[b + i];
-                int rank = 0;
-                for (int j = 0; j < S; j++) rank += ptmp[b + j] < v;
-                perm[b + rank] = v;
+                lo = min(lo, v);
+                hi = max(hi, v);
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                lo = min(lo, __shfl_xor(lo, o));
+                hi = max(hi, __shfl_xor(hi, o));
+            }
+            int w = b;
+            for (int64_t e0 = lo; e0 <= hi; e0 += 64) {
+                const int64_t e = e0 + lane;
+                const bool m = e <= hi && e < n && gid[e] == g;
+                const uint64_t bal = __ballot(m);
+                if (m) perm[w + __popcll(bal & ((1ull << lane) - 1))] = (int)e;
+                w += __popcll(bal);
             }
         }
     }
@@ -730,7 +747,7 @@ extern "C" int dpvo_group_by(const int64_t* key, int64_t n, int key_bits, int64_
             hipLaunchKernelGGL(cb_scatter_kernel, dim3(gn), dim3(256), 0, st, key, n, mask, hist, pre, slot, ptmp, gid,
                                offs, groups);
             const unsigned gf = grid_for(std::min<int64_t>(n, B) * 64, 64 * CB_WAVES, 2048);
-            hipLaunchKernelGGL(cb_fix_kernel, dim3(gf), dim3(64 * CB_WAVES), 0, st, ptmp, offs, groups, perm);
+            hipLaunchKernelGGL(cb_fix_kernel, dim3(gf), dim3(64 * CB_WAVES), 0, st, ptmp, offs, groups, gid, n, perm);
             DPVO_CHECK_LAUNCH();
             return 0;
         }
@@ -893,6 +910,136 @@ extern "C" int dpvo_softagg_csr_long(int dtype, const void* f, int64_t ldf, cons
     else
         hipLaunchKernelGGL(sa_reduce_csr_split_kernel<float>, dim3(grid), dim3(256), 0, as_stream(stream),
                            (const float*)f, ldf, (const float*)s, lds, offs, perm, groups, D, slices, eps, (float*)y);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// torch_scatter 2.1.2 reductions (scatter_sum / mean / max / softmax) over the
+// CSR of dpvo_group_by(index): the reference's SoftAgg (blocks.py:42-43), its
+// Python BA (ba.py:40-56) and loop closure (long_term.py:134) call them.
+// src is viewed as [outer][E][inner] (the scatter dim in the middle) and the
+// index is 1-D along it.  One thread per (group, outer x inner column) walks
+// the group's members in ascending edge order: deterministic, no atomics.
+// ---------------------------------------------------------------------------
+namespace {
+enum { SC_SUM = 0, SC_MEAN = 1, SC_MAX = 2, SC_SOFTMAX = 3 };
+
+template <typename T> struct ScAcc { typedef float type; };
+template <> struct ScAcc<double> { typedef double type; };
+
+template <typename T, int OP>
+__global__ __launch_bounds__(256) void scatter_csr_kernel(const T* __restrict__ src, int64_t outer, int64_t E,
+                                                          int64_t inner, const int64_t* __restrict__ index,
+                                                          const int* __restrict__ offs, const int* __restrict__ perm,
+                                                          const int64_t* __restrict__ groups, int64_t max_groups,
+                                                          float eps, T* __restrict__ out, int64_t out_rows,
+                                                          int64_t* __restrict__ arg)
+{
+    typedef typename ScAcc<T>::type A;
+    const int64_t G = min(*groups, max_groups);
+    const int64_t cols = outer * inner;
+    const int64_t cblocks = (cols + 255) / 256;
+    for (int64_t w = blockIdx.x; w < G * cblocks; w += gridDim.x) {
+        const int64_t g = w / cblocks;
+        const int64_t col = (w % cblocks) * 256 + threadIdx.x;
+        if (col >= cols) continue;
+        const int64_t o = col / inner, c = col % inner;
+        const int b = offs[g], s = offs[g + 1] - b;
+        const T* sp = src + o * E * inner + c;
+        if (OP == SC_SUM || OP == SC_MEAN) {
+            A a = 0;
+            for (int i = 0; i < s; i++) a += (A)sp[(int64_t)perm[b + i] * inner];
+            const int64_t key = index[perm[b]];
+            if (key < 0 || key >= out_rows) continue;
+            T* op = out + (o * out_rows + key) * inner + c;
+            A v = (A)*op + a;
+            if (OP == SC_MEAN) v = v / (A)s;
+            *op = (T)v;
+        } else if (OP == SC_MAX) {
+            A m = 0;
+            int64_t am = -1;
+            for (int i = 0; i < s; i++) {
+                const int e = perm[b + i];
+                const A v = (A)sp[(int64_t)e * inner];
+                if (am < 0 || v > m) {
+                    m = v;
+                    am = e;
+                }
+            }
+            const int64_t key = index[perm[b]];
+            if (key < 0 || key >= out_rows) continue;
+            out[(o * out_rows + key) * inner + c] = (T)m;
+            arg[(o * out_rows + key) * inner + c] = am;
+        } else {   // SOFTMAX: recentre on the group max, exp, / (sum + eps)   (composite/softmax.py)
+            A m = 0;
+            for (int i = 0; i < s; i++) {
+                const A v = (A)sp[(int64_t)perm[b + i] * inner];
+                m = (i == 0 || v > m) ? v : m;
+            }
+            A den = 0;
+            for (int i = 0; i < s; i++) den += exp((A)sp[(int64_t)perm[b + i] * inner] - m);
+            den += (A)eps;
+            T* op = out + o * E * inner + c;
+            for (int i = 0; i < s; i++) {
+                const int64_t e = perm[b + i];
+                op[e * inner] = (T)(exp((A)sp[e * inner] - m) / den);
+            }
+        }
+    }
+}
+
+template <typename T>
+int scatter_dispatch(int op, const T* src, int64_t outer, int64_t E, int64_t inner, const int64_t* index,
+                     const int* offs, const int* perm, const int64_t* groups, int64_t max_groups, float eps, T* out,
+                     int64_t out_rows, int64_t* arg, hipStream_t st)
+{
+    const int64_t cblocks = (outer * inner + 255) / 256;
+    const unsigned grid = grid_for(max_groups * cblocks, 1, 16384);
+#define SC_LAUNCH(OPV)                                                                                          \
+    hipLaunchKernelGGL((scatter_csr_kernel<T, OPV>), dim3(grid), dim3(256), 0, st, src, outer, E, inner, index, \
+                       offs, perm, groups, max_groups, eps, out, out_rows, arg)
+    switch (op) {
+    case SC_SUM: SC_LAUNCH(SC_SUM); break;
+    case SC_MEAN: SC_LAUNCH(SC_MEAN); break;
+    case SC_MAX: SC_LAUNCH(SC_MAX); break;
+    case SC_SOFTMAX: SC_LAUNCH(SC_SOFTMAX); break;
+    default: return -1;
+    }
+#undef SC_LAUNCH
+    return 0;
+}
+}  // namespace
+
+extern "C" int dpvo_scatter_csr(int op, int dtype, const void* src, int64_t outer, int64_t E, int64_t inner,
+                                const int64_t* index, const int* offs, const int* perm, const int64_t* groups,
+                                int64_t max_groups, float eps, void* out, int64_t out_rows, int64_t* argmax,
+                                void* stream)
+{
+    DPVO_CHECK_ARG(op >= SC_SUM && op <= SC_SOFTMAX, "op must be 0 (sum), 1 (mean), 2 (max) or 3 (softmax)");
+    DPVO_CHECK_ARG(outer >= 0 && E >= 0 && inner >= 0 && out_rows >= 0, "bad sizes");
+    DPVO_CHECK_ARG(E < (int64_t(1) << 31), "at most 2^31 - 1 elements along the scatter dim");
+    DPVO_CHECK_ARG(op != SC_MAX || argmax != nullptr, "scatter max needs the argmax output");
+    if (E == 0 || outer == 0 || inner == 0 || max_groups <= 0) return 0;
+    DPVO_CHECK_ARG(src && index && offs && perm && groups && out, "null operand");
+    hipStream_t st = as_stream(stream);
+    int rc;
+    switch (dtype) {
+    case DPVO_F16:
+        rc = scatter_dispatch(op, (const half_t*)src, outer, E, inner, index, offs, perm, groups, max_groups, eps,
+                              (half_t*)out, out_rows, argmax, st);
+        break;
+    case DPVO_F32:
+        rc = scatter_dispatch(op, (const float*)src, outer, E, inner, index, offs, perm, groups, max_groups, eps,
+                              (float*)out, out_rows, argmax, st);
+        break;
+    case DPVO_F64:
+        rc = scatter_dispatch(op, (const double*)src, outer, E, inner, index, offs, perm, groups, max_groups, eps,
+                              (double*)out, out_rows, argmax, st);
+        break;
+    default: rc = -1;
+    }
+    DPVO_CHECK_ARG(rc == 0, "unsupported dtype");
     DPVO_CHECK_LAUNCH();
     return 0;
 }

@@ -49,13 +49,16 @@ def raise_for_status(s):
 
 
 def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t1, iterations, csr=None,
-            status=None):
+            status=None, keep_status=False):
     """ba.cpp:31-43 -> ba_cuda.cu:422-540.  Updates poses and patches in place; returns [].
     csr (optional, not in the reference): (offs int32 [E+1], perm int32 [E],
     groups int64 [1]) of update_ops.group_by(kk) for these edges.
     status (optional, not in the reference): a device int32 [1] the call's
     status word is written to instead of being read here -- no host
-    synchronisation; the caller checks it later (raise_for_status)."""
+    synchronisation; the caller checks it later (raise_for_status).
+    keep_status (with status=): the word is not cleared first; if it already
+    holds a failure (DPVO.update's window-key check) the call leaves poses and
+    patches untouched (deterministic sliding-window path, DPVO_BA_KEEP_STATUS)."""
     global last_status
     H.on_gpu(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk)
     for name, t in (("poses", poses), ("patches", patches), ("intrinsics", intrinsics), ("target", target),
@@ -70,7 +73,7 @@ def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t
     lmbda = lmbda.to(device=poses.device, dtype=torch.float32).contiguous()
     E = ii.numel()
     N = int(t1) - int(t0)
-    flags = (1 if SPARSE else 0) | (0 if DETERMINISTIC else 2)
+    flags = (1 if SPARSE else 0) | (0 if DETERMINISTIC else 2) | (4 if keep_status and status is not None else 0)
     nbytes = H.lib().dpvo_ba_workspace_bytes_ex(E, num_patches, max(N, 0), flags)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=poses.device)
     deferred = status is not None
@@ -131,9 +134,15 @@ def solve_system(J_Ginv_i, J_Ginv_j, ii, jj, res, ep, lm, freen):
     (dpvo_solve_system_assemble); the reference's Eigen SimplicialCholesky is a
     dense fp64 Cholesky here (rocSOLVER via torch.linalg).  freen >= 0 solves
     only the top-left 7*freen block (the rest of delta is zero), like the
-    reference.  An edge with ii == jj raises (the reference calls exit(1))."""
-    H.on_gpu(J_Ginv_i, J_Ginv_j, ii, jj, res)
-    dev = res.device
+    reference.  An edge with ii == jj raises (the reference calls exit(1)).
+
+    Like the reference (which copies every input to the host itself), the
+    inputs may live on any device -- PGO builds its Jacobians with pypose,
+    possibly on the CPU (optim_utils.py:222-255).  The solve runs on the GPU
+    (the current device when res is a CPU tensor) and delta comes back on
+    res.device."""
+    out_dev = res.device
+    dev = res.device if res.is_cuda else torch.device("cuda", torch.cuda.current_device())
     Ji = J_Ginv_i.to(dev, torch.float32).contiguous()
     Jj = J_Ginv_j.to(dev, torch.float32).contiguous()
     rr = res.to(dev, torch.float32).contiguous().view(-1, 7)
@@ -148,11 +157,11 @@ def solve_system(J_Ginv_i, J_Ginv_j, ii, jj, res, ep, lm, freen):
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     H.check(H.lib().dpvo_solve_system_assemble(H.ptr(Ji), H.ptr(Jj), H.ptr(ii), H.ptr(jj), H.ptr(rr), r, m,
                                                float(ep), float(lm), H.ptr(A), H.ptr(b), H.ptr(status),
-                                               H.stream_of(res)))
+                                               H.stream_of(rr)))
     if int(status.item()):
         raise RuntimeError("solve_system: an edge with ii == jj (the reference exits the process, ba.cpp:205)")
     delta = torch.zeros(7 * n, dtype=torch.float32, device=dev)
     if m:
         L = torch.linalg.cholesky(A)
         delta[:m] = torch.cholesky_solve(b[:, None], L)[:, 0].float()
-    return [delta.view(n, 7)]
+    return [delta.view(n, 7).to(out_dev)]

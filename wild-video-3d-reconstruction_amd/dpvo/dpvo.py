@@ -279,7 +279,20 @@ class DPVO:
     def update(self, t0=None):
         """One keyframe of the hot loop (dpvo.py:711-749).  t0: optional lower
         bound of the optimised pose window (the reference's max(t0_, t0 or 1),
-        :730-731)."""
+        :730-731).
+
+        With cfg.DEFER_BA_CHECK (the default) nothing here reads the device:
+        a BA Cholesky failure (the reference raises inside update(),
+        ba_cuda.cu:521) lands in a device status word and is raised by the
+        next host read -- keyframe()'s, check_ba(), terminate(), or the end of
+        the initialisation updates in __call__ -- so it surfaces up to one
+        frame later than in the reference.  The same word first receives the
+        window-key check (an edge outside the 64-frame key window); BA then
+        skips the step instead of updating depths from merged groups.
+        DEFER_BA_CHECK = False restores the immediate raise."""
+        defer = getattr(self.cfg, "DEFER_BA_CHECK", True)
+        if defer:
+            self._ba_status.zero_()
         with Timer("other", enabled=self.enable_timing):
             coords = self.reproject()
             # the edges grouped by patch once, on the device: the update
@@ -291,7 +304,8 @@ class DPVO:
                 # next keyframe() / check_ba() raises)
                 key_kk, key_ij, ctx_idx, jslot = update_ops.window_keys(self.pg.ii, self.pg.jj, self.pg.kk, self.M,
                                                                         self.n - 64, self.M * self.pmem, self.pmem,
-                                                                        flag=self._ba_fail)
+                                                                        flag=self._ba_status if defer
+                                                                        else self._ba_fail)
                 kk_groups = update_ops.group_by(key_kk, key_bits=update_ops.key_bits_for(64 * self.M))
                 ij_groups = update_ops.group_by(key_ij, key_bits=12)
                 slots = (ctx_idx, jslot)
@@ -317,17 +331,31 @@ class DPVO:
         with Timer("BA", enabled=self.enable_timing):
             t0_ = self.n - self.cfg.OPTIMIZATION_WINDOW if self.is_initialized else 1
             t0 = max(t0_, t0 or 1)
-            defer = getattr(self.cfg, "DEFER_BA_CHECK", True)
-            if defer:
-                self._ba_status.zero_()
             fastba.BA(self.poses, self.patches, self.intrinsics, target, weight, self._lmbda, self.pg.ii, self.pg.jj,
                       self.pg.kk, t0, self.n, getattr(self.cfg, "BA_ITERATIONS", 2), csr=kk_groups[1:],
-                      status=self._ba_status if defer else None)
+                      status=self._ba_status if defer else None, keep_status=defer)
             if defer:   # keep the first failure until a host read looks at it
                 torch.where(self._ba_fail == 0, self._ba_status, self._ba_fail, out=self._ba_fail)
             m = self.pg.m
             pops.point_cloud_centre(SE3(self.poses), self.patches[:, :m], self.intrinsics, self.ix[:m],
                                     out=self.pg.points_[:m])
+
+    def update_get_corr(self):
+        """dpvo.py:660-687: update() whose BA failure is caught and reported as
+        a warning (the reference's bare ``except``), returning (points of all
+        m stored patches [m, 3], target [1, E, 2]).  The reference stores the
+        points into ``self.points_``, which DPVO does not have (its
+        AttributeError at :686 makes the method unusable there); they go to
+        ``pg.points_`` here, where update() writes them."""
+        try:
+            self.update()
+            status = int(self._ba_fail.item()) if getattr(self.cfg, "DEFER_BA_CHECK", True) else 0
+        except RuntimeError:
+            status = 1
+        if status:
+            self._ba_fail.zero_()
+            print("Warning BA failed...")
+        return self.pg.points_[:self.pg.m], self.pg.target
 
     def _window_keys(self):
         """True when every edge of the sliding window has n - 64 <= ii, jj < n
@@ -600,6 +628,7 @@ class DPVO:
             self.is_initialized = True
             for _ in range(12):
                 self.update()
+            self.check_ba()   # the initialisation's deferred BA status (one host read, once)
         elif self.is_initialized:
             self.update()
             self.keyframe()

@@ -38,6 +38,7 @@ class Update(nn.Module):
         self._pk = None
 
     FUSED = True  # inference under fp16 autocast runs the fused HIP path (class-level switch for A/B tests)
+    CORR_CHAIN3 = True  # the corr MLP + first LayerNorm as one three-GEMM launch (False: two launches)
 
     # ------------------------------------------------------------ fused path
     def _packed(self):
@@ -73,8 +74,9 @@ class Update(nn.Module):
     def _forward_fused(self, net, inp, corr, ii, jj, kk, inp_idx=None, index_bounds=None, kk_groups=None,
                        ij_groups=None):
         """The same dataflow as the reference under autocast, in 19 full-row
-        fused GEMMs (csrc/rowgemm.hip; 5 Linear->ReLU->Linear pairs chained,
-        14 launches) + 2 SoftAggs: every Linear is an fp16
+        fused GEMMs (csrc/rowgemm.hip; the corr MLP + LayerNorm as one
+        three-GEMM chain, 4 more Linear->ReLU->Linear pairs chained; 11
+        launches) + 2 SoftAggs: every Linear is an fp16
         GEMM with fp32 accumulate; residual adds, LayerNorms, gating and the
         d/w heads run in fp32 in the GEMM epilogues."""
         U = update_ops
@@ -86,13 +88,18 @@ class Update(nn.Module):
             padded[:, :c.shape[1]] = c
             c = padded
         c0, c1, cln, c2 = pk["corr"]
-        # Linear -> ReLU -> Linear pairs run chained, the intermediate in LDS
-        _, h, _ = U.rowchain(c, *c0, *c1, flags1=U.RELU, flags=U.LN | U.LN_RELU, ln=cln)
         # inp rows gathered inside the epilogue when the caller passes the index
         # (DPVO.update: imap[:, kk % (M pmem)], dpvo.py:718) -- no E x 384 copy
         res16, res16_idx = (inp[0], inp_idx) if inp_idx is not None else (inp[0].contiguous(), None)
-        n32, n16, _ = U.rowgemm(h, *c2, flags=U.RES | U.LN, res32=net[0], res16=res16, res16_idx=res16_idx,
-                                ln=pk["norm"], want32=True)
+        if self.CORR_CHAIN3:
+            # the corr MLP (Linear -> ReLU -> Linear -> LN -> ReLU -> Linear) and
+            # norm(net + inp + .) in one launch, both intermediates on chip
+            n32, n16, _ = U.rowchain(c, *c0, *c2, flags1=U.RELU, mid=(*c1, cln), flags=U.RES | U.LN, res32=net[0],
+                                     res16=res16, res16_idx=res16_idx, ln=pk["norm"], want32=True)
+        else:   # two launches, the LN'd intermediate through HBM (bit-identical)
+            _, h, _ = U.rowchain(c, *c0, *c1, flags1=U.RELU, flags=U.LN | U.LN_RELU, ln=cln)
+            n32, n16, _ = U.rowgemm(h, *c2, flags=U.RES | U.LN, res32=net[0], res16=res16, res16_idx=res16_idx,
+                                    ln=pk["norm"], want32=True)
         # the kk group-by (SoftAgg below) also yields the temporal neighbours:
         # fastba.neighbors(kk, jj) without a second sort
         # radix-sort key widths: from the caller's index bounds (the tracker
@@ -190,9 +197,11 @@ class Patchifier(nn.Module):
             self._native = encoder_ops.NativeEncoders(self.fnet, self.inet)
         return self._native
 
-    def _use_native(self, amp_dtype):
+    def _use_native(self, amp_dtype, image):
+        """the native encoders take uint8 frames (the reference accepts any
+        dtype: other frames run the torch encoders)"""
         return (self.NATIVE_ENCODERS and amp_dtype == torch.float16 and not torch.is_grad_enabled() and
-                self.fnet.norm_fn == "instance" and self.inet.norm_fn == "none")
+                image.dtype == torch.uint8 and self.fnet.norm_fn == "instance" and self.inet.norm_fn == "none")
 
     def _image_gradient(self, images):
         gray = ((images + 0.5) * (255.0 / 2)).sum(dim=2)
@@ -209,7 +218,7 @@ class Patchifier(nn.Module):
                 and not torch.is_grad_enabled()):
             return self._forward_graphed(images, patches_per_image, return_color)
         amp = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else None
-        if (self._use_native(amp) and not gradient_bias and mask is None and disps is None and images.is_cuda and
+        if (self._use_native(amp, images) and not gradient_bias and mask is None and disps is None and images.is_cuda and
                 images.dim() == 3):
             x, y = self._draw_centres(images, patches_per_image)
             fmap, gmap, imap, patches, clr = self._ingest(images, x, y, return_color, "native")
@@ -328,7 +337,7 @@ class Patchifier(nn.Module):
         # already in that dtype -- the same values the casts produce, so the
         # same convolutions (bit-identical to the eager path, test_gpu_tracker)
         enc = None
-        if amp and self._use_native(dt):
+        if amp and self._use_native(dt, image):
             enc = "native"
         elif amp:
             enc = tuple(copy.deepcopy(m).to(dt) for m in (self.fnet, self.inet))

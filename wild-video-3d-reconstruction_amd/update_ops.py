@@ -81,12 +81,16 @@ def softagg_csr(f, s, offs, perm, groups, max_groups, eps=1e-12, long_groups=Fal
 
 
 def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=None, res16=None, res16_idx=None,
-             gate16=None, ln=None, heads=None, want32=False, want16=True, M_dev=None, gate=None):
+             gate16=None, ln=None, heads=None, want32=False, want16=True, M_dev=None, gate=None, mid=None):
     """rowgemm(rowgemm(A, W1, b1, flags1, a_idx).y16, W2, b2, flags, ...) in one
     launch, the 384-wide intermediate kept on chip (dpvo_rowchain).
     gate = (Wg, bg) with GATE in flags: gate16 = rowgemm(A, Wg, bg, SIGMOID)
     computed in the same launch (dpvo_rowchain_gated) instead of passed in.
-    Returns (out32, out16, head_out) of the second GEMM."""
+    mid = (Wm, bm, (ln_g, ln_b, eps)): a middle Linear between the two, its
+    output LayerNorm'd and ReLU'd on chip (dpvo_rowchain3; flags must be
+    RES | LN): rowgemm(rowchain(A, W1, b1, Wm, bm, LN | LN_RELU).out16, W2, b2,
+    flags, ...) in one launch.
+    Returns (out32, out16, head_out) of the last GEMM."""
     H.on_gpu(A, W1, b1, W2, b2)
     if flags1 is None:
         flags1 = RELU
@@ -145,6 +149,17 @@ def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=
         gg = RowGemmArgs()
         gg.W, gg.K, gg.N, gg.bias = _p(Wg), Kp, WIDTH, _p(bg)
         H.check(H.lib().dpvo_rowchain_gated(_ct.byref(gg), _ct.byref(g1), _ct.byref(g2), H.stream_of(A)))
+    elif mid is not None:
+        Wm, bm, lnm = mid
+        H.on_gpu(Wm, bm, lnm[0], lnm[1])
+        if (Wm.dtype != torch.float16 or bm.dtype != torch.float16 or tuple(Wm.shape) != (WIDTH, WIDTH) or
+                not Wm.is_contiguous()):
+            raise RuntimeError("rowchain: the middle W must be a contiguous fp16 [384, 384], bias fp16")
+        gm = RowGemmArgs()
+        gm.W, gm.K, gm.N, gm.bias = _p(Wm), WIDTH, WIDTH, _p(bm)
+        gm.ln_g, gm.ln_b, gm.ln_eps = _p(lnm[0]), _p(lnm[1]), float(lnm[2])
+        gm.flags = LN | LN_RELU
+        H.check(H.lib().dpvo_rowchain3(_ct.byref(g1), _ct.byref(gm), _ct.byref(g2), H.stream_of(A)))
     else:
         H.check(H.lib().dpvo_rowchain(_ct.byref(g1), _ct.byref(g2), H.stream_of(A)))
     return out32, out16, head_out
@@ -369,3 +384,20 @@ def rowadd_ln(a, b16=None, b_idx=None, ln=None, want32=True, want16=True):
     args.out32, args.out16 = _p(out32), _p(out16)
     H.check(H.lib().dpvo_rowadd_ln(_ct.byref(args), H.stream_of(a)))
     return out32, out16
+
+
+SCATTER_SUM, SCATTER_MEAN, SCATTER_MAX, SCATTER_SOFTMAX = 0, 1, 2, 3
+
+
+def scatter_csr(op, src3, index, csr, out, out_rows=0, argmax=None, eps=1e-12):
+    """dpvo_scatter_csr: src3 [outer, E, inner] contiguous, index [E] int64,
+    csr = group_by(index); out [outer, out_rows, inner] (sum / mean / max,
+    written only at keys with members) or shaped like src3 (softmax)."""
+    H.on_gpu(src3, index, out)
+    gid, offs, perm, groups = csr
+    outer, E, inner = src3.shape
+    H.check(H.lib().dpvo_scatter_csr(int(op), H.dtype_code(src3), H.ptr(src3), outer, E, inner, H.ptr(index),
+                                     H.ptr(offs), H.ptr(perm), H.ptr(groups), E, float(eps), H.ptr(out),
+                                     int(out_rows), H.ptr(argmax) if argmax is not None else None,
+                                     H.stream_of(src3)))
+    return out
