@@ -74,11 +74,12 @@ def test_window_violation_skips_ba_and_raises():
     """An edge outside the 64-frame key window: the window-key
     check writes the BA status word first, BA leaves poses / depths alone, and
     the next host read raises the window error."""
-    slam = make(seed=8)
+    slam = make(seed=8, buffer=128)
+    assert slam.n > 64 and slam._window_keys()
     with torch.no_grad():
         slam.update()
         slam.check_ba()
-        # patch 0 of the oldest stored frame as an edge target: ii = 0 < n - 64
+        # patch 0 of the oldest stored frame as an edge's patch: ii = 0 < n - 64
         slam.pg.ii[0] = 0
         slam.pg.kk[0] = 0
         poses0 = slam.pg.poses_[:slam.n].clone()

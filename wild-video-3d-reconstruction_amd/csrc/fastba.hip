@@ -1763,6 +1763,16 @@ __device__ __forceinline__ void bd_jterms_add(const BdEdge& o, float* part, floa
     }
 }
 
+// The Schur term  H -= sum_k Q_k e_k e_k^T,  g -= sum_k Q_k u_k e_k  over a
+// workgroup's patches: every wave parks its patch's E row and Q_k, Q_k u_k in
+// a slot of the workgroup's list (slot = wave + BD_WAVES * its local
+// iteration: a fixed order), and at a flush every thread owns upper-triangle
+// entries of the partial and sums the listed patches' products into them in
+// slot order -- a rank-BD_SLOTS update with plain LDS reads, no atomics.
+constexpr int BD_SLOT_IT = 8;                     // wave iterations per flush
+constexpr int BD_SLOTS = BD_SLOT_IT * BD_WAVES;   // 32 listed patches
+constexpr int BD_SLOT_LD = BD_N6MAX + 2;          // E row, Q, Q u
+
 // DBG (timing experiments only, DPVO_BD_DBG; results are wrong): 1 skips the
 // shared-frame / target-frame pose terms, 2 the Schur update, 4 the
 // workgroup partial's write
@@ -1778,10 +1788,12 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
     float* ev = sm + BD_WAVES * ent + wave * BD_N6MAX;
     // (row, column) of every upper-triangle entry k = tri_up(r, c): r | c << 8
     uint16_t* tri_rc = reinterpret_cast<uint16_t*>(sm + BD_WAVES * ent + BD_WAVES * BD_N6MAX);
+    float* slots = sm + BD_WAVES * ent + BD_WAVES * BD_N6MAX + (pose_terms ? (nup + 1) / 2 : 0);
     if (pose_terms) {
         for (int i = threadIdx.x; i < BD_WAVES * ent; i += blockDim.x) sm[i] = 0.f;
         for (int r = threadIdx.x; r < n6; r += blockDim.x)
             for (int c = r; c < n6; c++) tri_rc[tri_up(r, c, n6)] = (uint16_t)(r | c << 8);
+        for (int i = threadIdx.x; i < BD_SLOTS * BD_SLOT_LD; i += blockDim.x) slots[i] = 0.f;
     }
     __syncthreads();
     const int64_t G = min(*p.groups, p.mu_max);
@@ -1791,7 +1803,16 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
     const float dx0 = (APPLY && lane < n6) ? p.dX[lane] : 0.f;
     const float dx1 = (APPLY && lane + 64 < n6) ? p.dX[lane + 64] : 0.f;
 
-    for (int64_t g = (int64_t)blockIdx.x * BD_WAVES + wave; g < G; g += (int64_t)gridDim.x * BD_WAVES) {
+    // every wave of every workgroup runs the same number of iterations (the
+    // flushes are workgroup barriers); g >= G leaves the wave's slot empty
+    const int64_t stride = (int64_t)gridDim.x * BD_WAVES;
+    const int64_t niter = (G + stride - 1) / stride;
+    for (int64_t it = 0; it < niter; it++) {
+        const int64_t g = it * stride + (int64_t)blockIdx.x * BD_WAVES + wave;
+        const int sit = (int)(it % BD_SLOT_IT);
+        float* slot = slots + (sit * BD_WAVES + wave) * BD_SLOT_LD;
+        if (pose_terms && lane == 0) slot[BD_N6MAX] = slot[BD_N6MAX + 1] = 0.f;   // empty until filled
+        if (g < G) do {
         const int start = p.offs[g], cnt = p.offs[g + 1] - start;
         const int64_t k = p.kk[p.perm[start]];
         if (k < 0 || k >= p.num_patches) {
@@ -1816,7 +1837,7 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         } else {
             dk = pd[centre];
         }
-        if (!HESS) continue;
+        if (!HESS) continue;   // (leaves the do-while: the next iteration)
         const float px = p.patches[(k * 3 + 0) * PP + centre], py = p.patches[(k * 3 + 1) * PP + centre];
 
         if (pose_terms) {
@@ -1824,7 +1845,6 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
             if (lane + 64 < n6) ev[lane + 64] = 0.f;
         }
         float Ck = 0.f, uk = 0.f;
-        unsigned touched = 0;  // window poses this patch's E row touches
         wave_lds_fence();
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const bool on = lane < cnt - c0;
@@ -1841,7 +1861,6 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
             Ck += wave64_sum(cl);
             uk += wave64_sum(ul);
             if (!pose_terms) continue;
-            touched |= wave_or((o.iv ? 1u << o.ix : 0u) | (o.jv ? 1u << o.jx : 0u));
             // one pass when every edge of the patch has the same frame i (DPVO:
             // the patch's own frame) and distinct target frames; otherwise one
             // lane per pass, in edge order
@@ -1905,23 +1924,42 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         if (lane < n6) Er[lane] = e0;
         if (lane + 64 < n6) Er[lane + 64] = e1;
         if (lane == 0) { p.Cg[g] = Ck; p.ug[g] = uk; }
-        // Schur term: H -= Q e e^T (upper) over the touched poses' rows, one
-        // lane per upper-triangle entry (e from the wave's LDS row): each entry
-        // gets -(Q e_r) e_c, the same product and the same single add per patch
-        // as a row-by-row sweep, without its idle lanes and per-row readlanes
+        // the Schur term goes through the workgroup's slot list (flushed below)
         const float Q = 1.0f / (Ck + lm);
-        const float qu = Q * uk;
-        if (!(DBG & 2)) {
-#pragma unroll 4
-            for (int k = lane; k < nup; k += 64) {
-                const int rc = tri_rc[k], r = rc & 255, c = rc >> 8;
-                if (touched >> (r / 6) & 1) atomicAdd(&part[k], -(Q * ev[r]) * ev[c]);
-            }
+        if (lane < n6) slot[lane] = e0;
+        if (lane + 64 < n6) slot[lane + 64] = e1;
+        if (lane == 0) {
+            slot[BD_N6MAX] = Q;
+            slot[BD_N6MAX + 1] = Q * uk;
         }
-        // g -= Q u e over the touched poses' entries, one lane per entry
-        if (lane < n6 && (touched >> (lane / 6) & 1)) part[nup + lane] -= qu * e0;
-        if (lane + 64 < n6 && (touched >> ((lane + 64) / 6) & 1)) part[nup + lane + 64] -= qu * e1;
         wave_lds_fence();
+        } while (false);
+        if (pose_terms && (sit == BD_SLOT_IT - 1 || it == niter - 1)) {
+            // flush: H_k -= sum_s (Q_s e_s[r]) e_s[c], g_r -= sum_s (Q u)_s e_s[r],
+            // slots in order, into wave 0's partial (one thread per entry)
+            __syncthreads();
+            const int ns = (sit + 1) * BD_WAVES;
+            if (!(DBG & 2)) {
+                for (int kx = threadIdx.x; kx < ent; kx += blockDim.x) {
+                    float acc = sm[kx];
+                    if (kx < nup) {
+                        const int rc = tri_rc[kx], r = rc & 255, c = rc >> 8;
+                        for (int q = 0; q < ns; q++) {
+                            const float* sl = slots + q * BD_SLOT_LD;
+                            acc -= (sl[BD_N6MAX] * sl[r]) * sl[c];
+                        }
+                    } else {
+                        const int r = kx - nup;
+                        for (int q = 0; q < ns; q++) {
+                            const float* sl = slots + q * BD_SLOT_LD;
+                            acc -= sl[BD_N6MAX + 1] * sl[r];
+                        }
+                    }
+                    sm[kx] = acc;
+                }
+            }
+            __syncthreads();
+        }
     }
     if (!pose_terms) return;
     // the workgroup's partial: its waves' partials summed in wave order
@@ -2117,6 +2155,104 @@ __global__ __launch_bounds__(256) void bd_solve_kernel(BdParams p)
     }
 }
 
+// The same damping / factor / solve / retraction in ONE wave with the system
+// in registers, for windows of up to 10 poses (DPVO's OPTIMIZATION_WINDOW):
+// lane i holds row i of the lower triangle of the augmented [S; g^T] (lane
+// n = 6 NN holds g^T), NN compile-time so every loop unrolls onto registers.
+// Right-looking Cholesky: per column k the pivot comes from lane k and the
+// column's entries L[c][k] from lanes c by readlane -- no LDS, no barriers;
+// the g row rides along as row n, ending as z = L^-1 g.  Back substitution
+// L^T x = z: lane i owns x_i, each x_j is (z_j - sum_{i > j} L[i][j] x_i) /
+// L[j][j] with the sum a wave reduction.  Status: the first failing leading
+// minor, as torch::linalg::cholesky reports it.
+__device__ __forceinline__ float rdl(float v, int lane) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane)); }
+
+template <int NN>
+__global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
+{
+    constexpr int n = 6 * NN;
+    static_assert(n < 64, "one lane per row plus the g row");
+    __shared__ float xs[64];
+    if (*(volatile int*)p.status != 0) return;
+    const int lane = threadIdx.x;
+    const int nup = p.nup;
+    float a[n];
+    // every load issued before any is used: row `lane` of the upper-stored
+    // system, column c at tri_up(c, lane) (lane < n), the g row at nup + c;
+    // other lanes / entries read entry 0 and are zeroed after the loads
+    const bool rowv = lane < n, grow = lane == n;
+    // tri_up(c, lane, n) = c (2n - c + 1) / 2 + lane - c: per-c constant + lane
+    const int base = rowv ? lane : grow ? nup : 0;
+#pragma unroll
+    for (int c = 0; c < n; c++) {
+        const int off = grow ? c : rowv ? c * (2 * n - c + 1) / 2 - c : 0;
+        a[c] = __builtin_nontemporal_load(p.H + (base + off));
+    }
+#pragma unroll
+    for (int c = 0; c < n; c++) {
+        const bool keep = (rowv && c <= lane) || grow;
+        a[c] = keep ? a[c] : 0.f;
+        if (c == lane) a[c] += 1e-4f * a[c] + 1.0f;   // S += diag(1e-4 S + 1), ba_cuda.cu:517-518
+    }
+    int fail = 0;
+#pragma unroll
+    for (int k = 0; k < n; k++) {
+        const float d = rdl(a[k], k);
+        if (!(d > 0.f)) {
+            fail = k + 1;
+            break;
+        }
+        const float l = sqrtf(d), il = 1.0f / l;
+        a[k] = lane == k ? l : a[k] * il;
+#pragma unroll
+        for (int c = k + 1; c < n; c++) a[c] -= a[k] * rdl(a[k], c);
+    }
+    if (fail) {
+        if (lane == 0) atomicExch(p.status, fail);
+        return;
+    }
+    float x = 0.f;
+#pragma unroll
+    for (int j = n - 1; j >= 0; j--) {
+        const float zj = rdl(a[j], n), ljj = rdl(a[j], j);
+        const float sj = wave64_allsum(lane > j && lane < n ? a[j] * x : 0.f);
+        const float xj = (zj - sj) / ljj;
+        x = lane == j ? xj : x;
+    }
+    if (lane < n) {
+        xs[lane] = x;
+        p.dX[lane] = x;
+    }
+    __builtin_amdgcn_s_barrier();   // one wave: orders the LDS write before the reads below
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (lane < NN) {
+        float* P = p.poses + (int64_t)(p.t0 + lane) * 7;
+        const float t0v[3] = {P[0], P[1], P[2]}, q0v[4] = {P[3], P[4], P[5], P[6]};
+        float xi[6], t1v[3], q1v[4];
+#pragma unroll
+        for (int k = 0; k < 6; k++) xi[k] = xs[6 * lane + k];
+        retrSE3(xi, t0v, q0v, t1v, q1v);
+        P[0] = t1v[0]; P[1] = t1v[1]; P[2] = t1v[2];
+        P[3] = q1v[0]; P[4] = q1v[1]; P[5] = q1v[2]; P[6] = q1v[3];
+    }
+}
+
+static void bd_solve_launch(const BdParams& p, hipStream_t s)
+{
+    static const bool blocked = getenv("DPVO_BD_BLOCK_SOLVE") != nullptr;   // A/B switch: the workgroup solver
+    if (blocked || p.N > 10) {
+        hipLaunchKernelGGL(bd_solve_kernel, dim3(1), dim3(256), 0, s, p);
+        return;
+    }
+    switch (p.N) {
+#define BW_CASE(K) \
+    case K: hipLaunchKernelGGL(bd_solve_wave_kernel<K>, dim3(1), dim3(64), 0, s, p); break;
+        BW_CASE(1) BW_CASE(2) BW_CASE(3) BW_CASE(4) BW_CASE(5) BW_CASE(6) BW_CASE(7) BW_CASE(8) BW_CASE(9) BW_CASE(10)
+#undef BW_CASE
+    default: break;
+    }
+}
+
 static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, const int* csr_offs,
                           const int* csr_perm, const int64_t* csr_groups, int iterations, hipStream_t s)
 {
@@ -2141,7 +2277,8 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
     p.H = (float*)(ws + L.H);
     p.dX = (float*)(ws + L.dX);
     const size_t lds = (size_t)(BD_WAVES * (p.N > 0 ? L.ent : 0) + BD_WAVES * BD_N6MAX) * 4 +
-                       (size_t)(p.N > 0 ? L.nup : 0) * 2;
+                       (size_t)(p.N > 0 ? (L.nup + 1) / 2 : 0) * 4 +
+                       (size_t)(p.N > 0 ? BD_SLOTS * BD_SLOT_LD : 0) * 4;
     const unsigned gR = (unsigned)((L.ent + 63) / 64);
     static const int dbg = getenv("DPVO_BD_DBG") ? atoi(getenv("DPVO_BD_DBG")) : 0;
     if (dbg) warn_debug_knob("DPVO_BD_DBG");
@@ -2164,7 +2301,7 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
 #undef BD_HESS
         if (p.N > 0) {
             hipLaunchKernelGGL(bd_reduce_kernel, dim3(gR), dim3(1024), 0, s, p, bd_grid());
-            hipLaunchKernelGGL(bd_solve_kernel, dim3(1), dim3(256), 0, s, p);
+            bd_solve_launch(p, s);
         }
         DPVO_CHECK_LAUNCH();
     }
