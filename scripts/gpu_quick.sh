@@ -15,7 +15,7 @@ timeout -k 10 300 python bench.py --steps 30 --warmup 5 --no-cpu-baseline --e2e-
 rc=$?; echo "bench rc=$rc"; python -c "import json;d=json.load(open('gpurun_out/bench_$TAG.json'));print(d['value'],d['ms_per_step'],d['breakdown_ms'])"
 [ $rc -eq 0 ] || exit $rc
 if [ "${C2:-0}" = "1" ]; then
-  timeout -k 10 300 python bench.py --config C2 --steps 30 --warmup 5 --no-cpu-baseline --e2e-frames 0 > gpurun_out/bench_${TAG}_c2.json 2>&1
+  timeout -k 10 300 python bench.py --config C2 --steps 30 --warmup 5 --no-cpu-baseline --e2e-frames 0 > gpurun_out/bench_${TAG}_c2.json 2> gpurun_out/bench_${TAG}_c2.err
   python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_c2.json'));print('C2',d['value'],d['ms_per_step'],d['breakdown_ms'])"
 fi
 if [ "${TRACE:-1}" = "1" ]; then
