@@ -89,6 +89,31 @@ __device__ __forceinline__ CmRange cm_range(int E, int wave)
     return r;
 }
 
+// The loaded registers l[ks] hold, in lane (q16, kc), chunk
+// 8 (ks >> 1) + 4 (q16 & 1) + kc of pixel (q16 & ~1) + (ks & 1).  The MFMA
+// operand m[j] must hold chunk 4 j + kc of pixel q16 in every lane:
+//   m[2h]     = even lane: l[2h] (own)        odd lane: l[2h+1] of lane - 1
+//   m[2h + 1] = even lane: l[2h] of lane + 1  odd lane: l[2h+1] (own)
+// (DPP quad_perm(0,0,2,2) / (1,1,3,3) fetch the pair partner's register).
+__device__ __forceinline__ void cm_pair_operands(const h8_t* l, h8_t* m, bool odd)
+{
+    typedef unsigned u4_t __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const u4_t e = __builtin_bit_cast(u4_t, l[2 * h]), o = __builtin_bit_cast(u4_t, l[2 * h + 1]);
+        u4_t m0, m1;
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const unsigned from_o = (unsigned)__builtin_amdgcn_update_dpp(0, (int)o[d], 0xA0, 0xF, 0xF, false);
+            const unsigned from_e = (unsigned)__builtin_amdgcn_update_dpp(0, (int)e[d], 0xF5, 0xF, 0xF, false);
+            m0[d] = odd ? from_o : e[d];
+            m1[d] = odd ? o[d] : from_e;
+        }
+        m[2 * h] = __builtin_bit_cast(h8_t, m0);
+        m[2 * h + 1] = __builtin_bit_cast(h8_t, m1);
+    }
+}
+
 // per-edge prologue operands, loaded one edge ahead
 struct CmEdgeIn {
     int e, ix, jx;
@@ -134,6 +159,14 @@ struct CmLevel {
 // bilinear epilogue reads each pixel's window and writes 256-byte coalesced rows.
 // STORE = false: timing experiment only (DPVO_CM_DBG=nostore): the epilogue
 // runs but writes nothing, which bounds what consuming corr on chip could save.
+// Tile loads read full 128-B lines: instruction ks gives lane (q16, kc) 16 B
+// of the EVEN (ks = 0, 2) or ODD (ks = 1, 3) pixel of its lane pair, chunk
+// 8 (ks >> 1) + 4 (q16 & 1) + kc of the pixel's 16 chunks -- eight pixels x 128 B
+// per wave-instruction instead of sixteen pixels x 64 B, the fragment shape
+// that costs the texture addresser twice the cycles (557 -> 388 us measured
+// with the loads alone changed).  Two DPP quad permutations and a select per
+// dword then rebuild the MFMA operand (lane (q16, kc): pixel q16, chunk
+// 4 j + kc): an exchange between the lanes of each pair (cm_pair_operands).
 template <bool STORE = true>
 __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParams p)
 {
@@ -286,22 +319,29 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
                 inb = true;
             }
             inb = inb && gy >= 0 && gy < fc.H && gx >= 0 && gx < fc.W;
-            const unsigned voff = inb ? (unsigned)(gy * (int)fc.rowb + gx * fc.pixb + 16 * kc) : OOB;
+            const int pix = inb ? gy * (int)fc.rowb + gx * fc.pixb : (int)OOB;   // this lane's pixel
             fc.tl++;
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(fc.frame), (short)0, fc.num, 0x00020000);
+            // full-line loads (see cm_pair_operands): the lane pair's even / odd pixel
+            const int pe = __builtin_amdgcn_update_dpp(0, pix, 0xA0, 0xF, 0xF, false);   // quad_perm(0,0,2,2)
+            const int po = __builtin_amdgcn_update_dpp(0, pix, 0xF5, 0xF, 0xF, false);   // quad_perm(1,1,3,3)
+            const unsigned ch = 16u * (unsigned)((q16 & 1) * 4 + kc);
 #pragma unroll
             for (int ks = 0; ks < 4; ks++) {
-                const auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 64 * ks, 0, 0);
-                a[ks] = __builtin_bit_cast(h8_t, v);
+                const unsigned b = (unsigned)((ks & 1) ? po : pe);
+                const unsigned o = b == OOB ? OOB : b + 128u * (ks >> 1) + ch;
+                a[ks] = __builtin_bit_cast(h8_t, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
             }
         };
         int clev = 0, ctl = 0, cntl = L0.ntiles;
         auto consume = [&](int t, const h8_t* a) {
             if (t >= ntot) return;
             f4m_t acc = {0.f, 0.f, 0.f, 0.f};
+            h8_t m[4];
+            cm_pair_operands(a, m, (q16 & 1) != 0);
 #pragma unroll
-            for (int ks = 0; ks < 4; ks++) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[ks], bq[ks], acc, 0, 0, 0);
+            for (int ks = 0; ks < 4; ks++) acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(m[ks], bq[ks], acc, 0, 0, 0);
             // acc[r] = tile pixel 4 kc + r . patch pixel (lane & 15)
             if (ctl == cntl) {
                 clev = 1;
