@@ -400,7 +400,11 @@ int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_args* b, vo
  * pairs).  g1: A, lda, a_idx, a_rows, W (K1 % 32 == 0), bias, zero_row, M,
  * M_dev and flags (DPVO_RG_RELU / DPVO_RG_SIGMOID only); its outputs are not
  * written.  g2: W ([384][384]), bias, flags and every epilogue input / output
- * of dpvo_rowgemm (its A, M and M_dev are taken from g1). */
+ * of dpvo_rowgemm (its A, M and M_dev are taken from g1).
+ * The chain kernels read every W (W1, W2, and the gate / middle W below)
+ * K-BLOCKED: [K/32][384][32] fp16 (k-stage major), so each 32-wide stage of
+ * all 384 output rows is one contiguous block and the stage loads read whole
+ * 128-B lines (update_ops.kblock re-lays out a [384][K] weight). */
 int dpvo_rowchain(const dpvo_rowgemm_args* first, const dpvo_rowgemm_args* second, void* stream);
 
 /* Three chained rowgemms: the update operator's corr MLP and the first

@@ -1023,9 +1023,9 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const int pc = 4 * wave + j;   // A pieces then W pieces, contiguous within the stage
-        if (pc >= 8) {
+        if (pc >= 8) {   // W1 k-blocked [K1/32][384][32]: a stage's 384 rows are one contiguous block
             const int n = (pc - 8) * 16 + srow;
-            g1src[j] = W1 + (int64_t)n * K1 + 8 * (pch ^ ((n >> 2) & 3));
+            g1src[j] = W1 + (int64_t)n * RC_BK + 8 * (pch ^ ((n >> 2) & 3));
         }
     }
     // GEMM2 stage: W2 pieces 3 wave .. 3 wave + 2 of 24
@@ -1033,20 +1033,23 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
 #pragma unroll
     for (int j = 0; j < 3; j++) {
         const int n = (3 * wave + j) * 16 + srow;
-        w2src[j] = W2 + (int64_t)n * RG_BN + 8 * (pch ^ ((n >> 2) & 3));
+        w2src[j] = W2 + (int64_t)n * RC_BK + 8 * (pch ^ ((n >> 2) & 3));   // k-blocked like W1
     }
     // gate pass: the same stage layout, W pieces from Wg ([384][K1] like W1)
     const int64_t gdelta = GATED ? (const half_t*)pg.W - W1 : 0;
+    // A pieces advance 32 columns per stage, k-blocked W pieces one 384 x 32 block
     auto issue1 = [&](int ks, int buf, bool gate = false) {
         char* st = smem + RC_Y + buf * RC_STAGE;
-        const int k0 = ks * RC_BK;
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-            glds16(g1src[j] + k0 + (GATED && gate && 4 * wave + j >= 8 ? gdelta : 0), st + (4 * wave + j) * 1024);
+        for (int j = 0; j < 4; j++) {
+            const bool wp = 4 * wave + j >= 8;
+            const int64_t k0 = wp ? (int64_t)ks * (RG_BN * RC_BK) : ks * RC_BK;
+            glds16(g1src[j] + k0 + (GATED && gate && wp ? gdelta : 0), st + (4 * wave + j) * 1024);
+        }
     };
     auto issue2 = [&](int ks, int buf, int64_t wdelta = 0) {
         char* st = smem + RC_Y + buf * RC_STAGE + RC_A_STAGE;
-        const int64_t k0 = ks * RC_BK + wdelta;
+        const int64_t k0 = (int64_t)ks * (RG_BN * RC_BK) + wdelta;
 #pragma unroll
         for (int j = 0; j < 3; j++) glds16(w2src[j] + k0, st + (3 * wave + j) * 1024);
     };

@@ -49,14 +49,17 @@ class Update(nn.Module):
         P = update_ops.pack_linear
         ln = lambda m: (m.weight.detach().float().contiguous(), m.bias.detach().float().contiguous(), m.eps)
         agg = lambda a: (P(a.f.weight, a.f.bias), P(a.g.weight, a.g.bias), P(a.h.weight, a.h.bias))
-        gr = lambda g: (P(g.gate[0].weight, g.gate[0].bias), P(g.res[0].weight, g.res[0].bias),
-                        P(g.res[2].weight, g.res[2].bias))
+        # chain operands (rowchain reads its W k-blocked: update_ops.kblock)
+        KB = lambda wb: (update_ops.kblock(wb[0]), wb[1])
+        gr = lambda g: (KB(P(g.gate[0].weight, g.gate[0].bias)), KB(P(g.res[0].weight, g.res[0].bias)),
+                        KB(P(g.res[2].weight, g.res[2].bias)))
         pk = {
-            "corr": (P(self.corr[0].weight, self.corr[0].bias), P(self.corr[2].weight, self.corr[2].bias),
-                     ln(self.corr[3]), P(self.corr[5].weight, self.corr[5].bias)),
+            "corr": (KB(P(self.corr[0].weight, self.corr[0].bias)), KB(P(self.corr[2].weight, self.corr[2].bias)),
+                     ln(self.corr[3]), KB(P(self.corr[5].weight, self.corr[5].bias))),
+            "corr5": P(self.corr[5].weight, self.corr[5].bias),   # (the two-launch variant's rowgemm)
             "norm": ln(self.norm),
-            "c1": (P(self.c1[0].weight, self.c1[0].bias), P(self.c1[2].weight, self.c1[2].bias)),
-            "c2": (P(self.c2[0].weight, self.c2[0].bias), P(self.c2[2].weight, self.c2[2].bias)),
+            "c1": (KB(P(self.c1[0].weight, self.c1[0].bias)), KB(P(self.c1[2].weight, self.c1[2].bias))),
+            "c2": (KB(P(self.c2[0].weight, self.c2[0].bias)), KB(P(self.c2[2].weight, self.c2[2].bias))),
             "agg_kk": agg(self.agg_kk), "agg_ij": agg(self.agg_ij),
             "gru": (ln(self.gru[0]), gr(self.gru[1]), ln(self.gru[2]), gr(self.gru[3])),
             "heads": (torch.cat([self.d[1].weight, self.w[1].weight]).detach().half().contiguous(),
@@ -98,8 +101,8 @@ class Update(nn.Module):
                                      res16=res16, res16_idx=res16_idx, ln=pk["norm"], want32=True)
         else:   # two launches, the LN'd intermediate through HBM (bit-identical)
             _, h, _ = U.rowchain(c, *c0, *c1, flags1=U.RELU, flags=U.LN | U.LN_RELU, ln=cln)
-            n32, n16, _ = U.rowgemm(h, *c2, flags=U.RES | U.LN, res32=net[0], res16=res16, res16_idx=res16_idx,
-                                    ln=pk["norm"], want32=True)
+            n32, n16, _ = U.rowgemm(h, *pk["corr5"], flags=U.RES | U.LN, res32=net[0], res16=res16,
+                                    res16_idx=res16_idx, ln=pk["norm"], want32=True)
         # the kk group-by (SoftAgg below) also yields the temporal neighbours:
         # fastba.neighbors(kk, jj) without a second sort
         # radix-sort key widths: from the caller's index bounds (the tracker

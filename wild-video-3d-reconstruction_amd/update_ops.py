@@ -90,17 +90,23 @@ def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=
     output LayerNorm'd and ReLU'd on chip (dpvo_rowchain3; flags must be
     RES | LN): rowgemm(rowchain(A, W1, b1, Wm, bm, LN | LN_RELU).out16, W2, b2,
     flags, ...) in one launch.
+    Weights may be given as [384, Kp] (re-laid out per call) or already
+    k-blocked by kblock() (what the kernel reads; the fused Update caches them).
     Returns (out32, out16, head_out) of the last GEMM."""
     H.on_gpu(A, W1, b1, W2, b2)
     if flags1 is None:
         flags1 = RELU
     if any(t.dtype != torch.float16 for t in (A, W1, b1, W2, b2)):
         raise RuntimeError("rowchain: A, weights and biases must be fp16")
-    if A.dim() != 2 or A.stride(1) != 1 or W1.shape[0] != WIDTH or not W1.is_contiguous():
-        raise RuntimeError("rowchain: A must be [rows, K] row-contiguous and W1 [384, Kp] contiguous")
-    if tuple(W2.shape) != (WIDTH, WIDTH) or not W2.is_contiguous():
-        raise RuntimeError("rowchain: W2 must be a contiguous [384, 384]")
-    Kp = W1.shape[1]
+    if A.dim() != 2 or A.stride(1) != 1:
+        raise RuntimeError("rowchain: A must be [rows, K] row-contiguous")
+    for W in (W1, W2):
+        if W.dim() == 2 and (W.shape[0] != WIDTH or not W.is_contiguous()):
+            raise RuntimeError("rowchain: W must be [384, Kp] contiguous")
+    W1, W2 = kblock(W1), kblock(W2)
+    if _kb_K(W2) != WIDTH:
+        raise RuntimeError("rowchain: W2 must be [384, 384]")
+    Kp = _kb_K(W1)
     if A.stride(0) < Kp:
         raise RuntimeError(f"rowchain: A's row stride {A.stride(0)} < padded K {Kp}")
     dev = A.device
@@ -142,6 +148,7 @@ def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=
     if gate is not None:
         Wg, bg = gate
         H.on_gpu(Wg, bg)
+        Wg = kblock(Wg)
         if Wg.dtype != torch.float16 or bg.dtype != torch.float16 or Wg.shape != W1.shape or not Wg.is_contiguous():
             raise RuntimeError("rowchain: gate W must be fp16 contiguous of W1's shape, bias fp16")
         if gate16 is not None:
@@ -152,8 +159,8 @@ def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=
     elif mid is not None:
         Wm, bm, lnm = mid
         H.on_gpu(Wm, bm, lnm[0], lnm[1])
-        if (Wm.dtype != torch.float16 or bm.dtype != torch.float16 or tuple(Wm.shape) != (WIDTH, WIDTH) or
-                not Wm.is_contiguous()):
+        Wm = kblock(Wm)
+        if Wm.dtype != torch.float16 or bm.dtype != torch.float16 or _kb_K(Wm) != WIDTH:
             raise RuntimeError("rowchain: the middle W must be a contiguous fp16 [384, 384], bias fp16")
         gm = RowGemmArgs()
         gm.W, gm.K, gm.N, gm.bias = _p(Wm), WIDTH, WIDTH, _p(bm)
@@ -273,6 +280,25 @@ def pack_linear(weight, bias, kpad=64):
     w = torch.zeros(n, kp, dtype=torch.float16, device=weight.device)
     w[:, :k] = weight.detach()
     return w.contiguous(), bias.detach().to(torch.float16).contiguous()
+
+
+def kblock(W16):
+    """[384, Kp] fp16 -> the k-blocked layout dpvo_rowchain reads, [Kp / 32, 384, 32]
+    contiguous: every 32-wide k stage of all 384 rows is one contiguous 24 KB
+    block, so the kernel's stage loads read whole 128-B lines."""
+    if W16.dim() == 3:
+        return W16
+    n, kp = W16.shape
+    if n != WIDTH or kp % 32:
+        raise RuntimeError("kblock: W must be [384, Kp] with Kp a multiple of 32")
+    return W16.view(n, kp // 32, 32).permute(1, 0, 2).contiguous()
+
+
+def _kb_K(Wkb):
+    """(Kp) of a k-blocked weight; validates the layout"""
+    if Wkb.dim() != 3 or Wkb.shape[1] != WIDTH or Wkb.shape[2] != 32 or not Wkb.is_contiguous():
+        raise RuntimeError("rowchain: weights must be [384, Kp] or k-blocked [Kp / 32, 384, 32] contiguous")
+    return Wkb.shape[0] * 32
 
 
 def _p(t):
