@@ -227,11 +227,9 @@ def phase_breakdown(slam, reps=5):
         e[0].record()
         coords = slam.reproject()
         e[1].record()
-        key_kk, key_ij, ctx_idx, jslot = update_ops.window_keys(slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M,
-                                                                slam.n - 64, slam.M * slam.pmem, slam.pmem,
-                                                                flag=slam._ba_status)
-        kk_groups = update_ops.group_by(key_kk, key_bits=update_ops.key_bits_for(64 * slam.M))
-        ij_groups = update_ops.group_by(key_ij, key_bits=12)
+        ctx_idx, jslot, kk_groups, ij_groups = update_ops.window_group_by(
+            slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M, slam.n - 64, slam.M * slam.pmem, slam.pmem,
+            flag=slam._ba_status)
         e[2].record()
         with torch.autocast("cuda", enabled=True):
             corr = slam.corr(coords, slots=(ctx_idx, jslot))

@@ -452,6 +452,22 @@ int dpvo_window_keys(const int64_t* ii, const int64_t* jj, const int64_t* kk, in
                      int64_t ring, int64_t frames, int64_t* key_kk, int64_t* key_ij, int64_t* ctx, int64_t* jslot,
                      int* flag, void* stream);
 
+/* dpvo_window_keys followed by dpvo_group_by(key_kk, kk_bits) and
+ * dpvo_group_by(key_ij, 12) (DPVO.update's per-update grouping: the SoftAgg
+ * groups of net.py:86-88 and BA's per-patch CSR), fused into one memset and
+ * four launches.  Writes ctx, jslot and flag as dpvo_window_keys does (the
+ * key arrays are not written out) and the two CSRs exactly as dpvo_group_by
+ * would: gid int64 [E], offs int32 [E + 1], perm int32 [E], groups int64 [1].
+ * kk_bits: 1..22, with 64 M <= 2^kk_bits for in-window keys.  workspace: at
+ * least dpvo_window_group_by_workspace_bytes(E, kk_bits) device bytes (0 for a
+ * bad kk_bits). */
+size_t dpvo_window_group_by_workspace_bytes(int64_t E, int kk_bits);
+int dpvo_window_group_by(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t E, int64_t M, int64_t base,
+                         int64_t ring, int64_t frames, int kk_bits, int64_t* ctx, int64_t* jslot, int* flag,
+                         int64_t* kk_gid, int* kk_offs, int* kk_perm, int64_t* kk_groups, int64_t* ij_gid,
+                         int* ij_offs, int* ij_perm, int64_t* ij_groups, void* workspace, size_t workspace_bytes,
+                         void* stream);
+
 /* DPVO.update after the update operator (dpvo.py:724-727): target[e] =
  * centre[e] + float(delta[e]), weight[e] = float(w[e]), both fp32 [E][2]
  * contiguous.  delta, w: fp16, row e at delta + e * delta_stride (2 values);

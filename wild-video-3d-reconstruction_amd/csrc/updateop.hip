@@ -320,7 +320,23 @@ CbLayout cb_layout(int64_t n, int key_bits)
 }
 
 // runs of equal keys inside a wave take one atomic per run (the run head's),
-// so bins hit by many consecutive edges do not serialise on one address
+// so bins hit by many consecutive edges do not serialise on one address.
+// Called by whole waves (uniform trip counts); valid lanes are a prefix.
+__device__ __forceinline__ int cb_run_slot(uint32_t k, bool valid, int lane, int* __restrict__ hist)
+{
+    const uint32_t prev = __shfl_up(k, 1);
+    const bool head = valid && (lane == 0 || prev != k);
+    const uint64_t hm = __ballot(head), vm = __ballot(valid);
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+    const int hl = 63 - __clzll(hm & upto);                  // my run's head lane
+    const uint64_t above = hm & ~upto;
+    const int end = above ? __ffsll((long long)above) - 1 : 64 - __clzll(vm);
+    int base = 0;
+    if (head) base = atomicAdd(&hist[k], end - lane);
+    base = __shfl(base, valid ? hl : 0);
+    return base + (lane - hl);
+}
+
 __global__ __launch_bounds__(256) void cb_hist_kernel(const int64_t* __restrict__ key, int64_t n, uint32_t mask,
                                                       int* __restrict__ hist, int* __restrict__ slot)
 {
@@ -329,17 +345,8 @@ __global__ __launch_bounds__(256) void cb_hist_kernel(const int64_t* __restrict_
         const int64_t e = e0 + threadIdx.x;   // uniform trip count: whole waves stay converged
         const bool valid = e < n;
         const uint32_t k = valid ? (uint32_t)key[e] & mask : 0xffffffffu;
-        const uint32_t prev = __shfl_up(k, 1);
-        const bool head = valid && (lane == 0 || prev != k);
-        const uint64_t hm = __ballot(head), vm = __ballot(valid);
-        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-        const int hl = 63 - __clzll(hm & upto);                  // my run's head lane
-        const uint64_t above = hm & ~upto;
-        const int end = above ? __ffsll((long long)above) - 1 : 64 - __clzll(vm);   // valid lanes are a prefix
-        int base = 0;
-        if (head) base = atomicAdd(&hist[k], end - lane);
-        base = __shfl(base, valid ? hl : 0);
-        if (valid) slot[e] = base + (lane - hl);
+        const int s = cb_run_slot(k, valid, lane, hist);
+        if (valid) slot[e] = s;
     }
 }
 
@@ -372,6 +379,58 @@ __global__ __launch_bounds__(256) void cb_scatter_kernel(const int64_t* __restri
 constexpr int CB_CAP = 2048;
 constexpr int CB_WAVES = 4;
 
+__device__ __forceinline__ void cb_fix_group(int64_t g, const int* __restrict__ ptmp, const int* __restrict__ offs,
+                                             const int64_t* __restrict__ gid, int64_t n, int* __restrict__ perm,
+                                             int* __restrict__ mine, int lane)
+{
+    const int b = offs[g], S = offs[g + 1] - b;
+    if (S <= 64) {
+        const int v = lane < S ? ptmp[b + lane] : INT_MAX;
+        int rank = 0;
+        for (int j = 0; j < S; j++) rank += __builtin_amdgcn_readlane(v, j) < v;
+        if (lane < S) perm[b + rank] = v;
+    } else if (S <= CB_CAP) {
+        for (int i = lane; i < S; i += 64) mine[i] = ptmp[b + i];
+        for (int i = S + lane; i < ((S + 3) & ~3); i += 64) mine[i] = INT_MAX;   // pad the last int4
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int i = lane; i < S; i += 64) {
+            const int v = mine[i];
+            int rank = 0;
+            for (int j = 0; j < S; j += 4) {
+                const int4 q = *(const int4*)(mine + j);
+                rank += (q.x < v) + (q.y < v) + (q.z < v) + (q.w < v);
+            }
+            perm[b + rank] = v;
+        }
+        __builtin_amdgcn_wave_barrier();   // every lane's reads before the next group's writes
+    } else {
+        // more than CB_CAP members: they are the edges e with gid[e] == g, so a
+        // scan of gid over [first member, last member] in ascending e emits
+        // them in order -- O(span / 64) per group, at most n / CB_CAP such
+        // groups (a rank by comparison would be O(S^2))
+        int lo = INT_MAX, hi = -1;
+        for (int i = lane; i < S; i += 64) {
+            const int v = ptmp[b + i];
+            lo = min(lo, v);
+            hi = max(hi, v);
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            lo = min(lo, __shfl_xor(lo, o));
+            hi = max(hi, __shfl_xor(hi, o));
+        }
+        int w = b;
+        for (int64_t e0 = lo; e0 <= hi; e0 += 64) {
+            const int64_t e = e0 + lane;
+            const bool m = e <= hi && e < n && gid[e] == g;
+            const uint64_t bal = __ballot(m);
+            if (m) perm[w + __popcll(bal & ((1ull << lane) - 1))] = (int)e;
+            w += __popcll(bal);
+        }
+    }
+}
+
 __global__ __launch_bounds__(64 * CB_WAVES) void cb_fix_kernel(const int* __restrict__ ptmp,
                                                                const int* __restrict__ offs,
                                                                const int64_t* __restrict__ groups,
@@ -380,57 +439,10 @@ __global__ __launch_bounds__(64 * CB_WAVES) void cb_fix_kernel(const int* __rest
 {
     __shared__ __attribute__((aligned(16))) int buf[CB_WAVES][CB_CAP];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int* mine = buf[w];
     const int64_t G = *groups;
     for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < G;
-         g += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-        const int b = offs[g], S = offs[g + 1] - b;
-        if (S <= 64) {
-            const int v = lane < S ? ptmp[b + lane] : INT_MAX;
-            int rank = 0;
-            for (int j = 0; j < S; j++) rank += __builtin_amdgcn_readlane(v, j) < v;
-            if (lane < S) perm[b + rank] = v;
-        } else if (S <= CB_CAP) {
-            for (int i = lane; i < S; i += 64) mine[i] = ptmp[b + i];
-            for (int i = S + lane; i < ((S + 3) & ~3); i += 64) mine[i] = INT_MAX;   // pad the last int4
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            for (int i = lane; i < S; i += 64) {
-                const int v = mine[i];
-                int rank = 0;
-                for (int j = 0; j < S; j += 4) {
-                    const int4 q = *(const int4*)(mine + j);
-                    rank += (q.x < v) + (q.y < v) + (q.z < v) + (q.w < v);
-                }
-                perm[b + rank] = v;
-            }
-            __builtin_amdgcn_wave_barrier();   // every lane's reads before the next group's writes
-        } else {
-            // more than CB_CAP members: they are the edges e with gid[e] == g, so a
-            // scan of gid over [first member, last member] in ascending e emits
-            // them in order -- O(span / 64) per group, at most n / CB_CAP such
-            // groups (a rank by comparison would be O(S^2))
-            int lo = INT_MAX, hi = -1;
-            for (int i = lane; i < S; i += 64) {
-                const int v = ptmp[b + i];
-                lo = min(lo, v);
-                hi = max(hi, v);
-            }
-            for (int o = 32; o > 0; o >>= 1) {
-                lo = min(lo, __shfl_xor(lo, o));
-                hi = max(hi, __shfl_xor(hi, o));
-            }
-            int w = b;
-            for (int64_t e0 = lo; e0 <= hi; e0 += 64) {
-                const int64_t e = e0 + lane;
-                const bool m = e <= hi && e < n && gid[e] == g;
-                const uint64_t bal = __ballot(m);
-                if (m) perm[w + __popcll(bal & ((1ull << lane) - 1))] = (int)e;
-                w += __popcll(bal);
-            }
-        }
-    }
+         g += ((int64_t)gridDim.x * blockDim.x) >> 6)
+        cb_fix_group(g, ptmp, offs, gid, n, perm, buf[w], lane);
 }
 
 // SoftAgg over a prebuilt CSR whose group count lives on the device.  Group
@@ -666,6 +678,156 @@ __global__ __launch_bounds__(256) void window_keys_kernel(const int64_t* __restr
     }
 }
 
+// The tracker's whole per-update grouping -- window_keys_kernel's outputs plus
+// the counting-sort group-bys of key_kk (2^kk_bits bins) and key_ij (4096
+// bins) -- in one memset and four launches instead of thirteen (DPVO.update's
+// window keys, then dpvo_group_by twice, each a memset, a histogram, a
+// two-kernel device scan, a scatter and a fix-up).  The launches are short
+// (~5 us) and back to back, so their count, not their bytes, sets the cost.
+// Outputs are dpvo_group_by's exactly (same masking of out-of-window keys).
+constexpr int WG_IJ_BITS = 12;
+
+struct WgLayout {
+    int64_t hist, pre_kk, pre_ij, slot_kk, slot_ij, ptmp_kk, ptmp_ij, key_kk, key_ij, total;
+};
+
+WgLayout wg_layout(int64_t n, int kk_bits)
+{
+    const int64_t Bkk = int64_t(1) << kk_bits, Bij = int64_t(1) << WG_IJ_BITS;
+    WgLayout L;
+    int64_t o = 0;
+    L.hist = o;    o += align256(4 * (Bkk + Bij));   // kk bins then ij bins: one memset
+    L.pre_kk = o;  o += align256(8 * Bkk);
+    L.pre_ij = o;  o += align256(8 * Bij);
+    L.slot_kk = o; o += align256(4 * n);
+    L.slot_ij = o; o += align256(4 * n);
+    L.ptmp_kk = o; o += align256(4 * n);
+    L.ptmp_ij = o; o += align256(4 * n);
+    L.key_kk = o;  o += align256(4 * n);
+    L.key_ij = o;  o += align256(4 * n);
+    L.total = o;
+    return L;
+}
+
+__global__ __launch_bounds__(256) void wg_hist_kernel(const int64_t* __restrict__ ii, const int64_t* __restrict__ jj,
+                                                      const int64_t* __restrict__ kk, int64_t E, int64_t M,
+                                                      int64_t base, int64_t ring, int64_t frames, uint32_t mask_kk,
+                                                      int64_t* __restrict__ ctx, int64_t* __restrict__ jslot,
+                                                      int* __restrict__ flag, int* __restrict__ hist_kk,
+                                                      int* __restrict__ hist_ij, int* __restrict__ slot_kk,
+                                                      int* __restrict__ slot_ij, uint32_t* __restrict__ key_kk,
+                                                      uint32_t* __restrict__ key_ij)
+{
+    const int lane = threadIdx.x & 63;
+    for (int64_t e0 = blockIdx.x * (int64_t)blockDim.x; e0 < E; e0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t e = e0 + threadIdx.x;   // uniform trip count: whole waves stay converged
+        const bool valid = e < E;
+        uint32_t kk_k = 0xffffffffu, ij_k = 0xffffffffu;
+        if (valid) {
+            const int64_t k = kk[e], j = jj[e];
+            const int64_t a = ii[e] - base, b = j - base, kr = k - M * base;
+            kk_k = (uint32_t)kr & mask_kk;
+            ij_k = (uint32_t)(a * 64 + b) & ((1u << WG_IJ_BITS) - 1);
+            if (flag && (a < 0 || a >= 64 || b < 0 || b >= 64 || kr < 0 || kr >= 64 * M)) atomicCAS(flag, 0, -2);
+            const int64_t r = k % ring, f = j % frames;
+            ctx[e] = r < 0 ? r + ring : r;
+            jslot[e] = f < 0 ? f + frames : f;
+            key_kk[e] = kk_k;
+            key_ij[e] = ij_k;
+        }
+        const int s_kk = cb_run_slot(kk_k, valid, lane, hist_kk);
+        const int s_ij = cb_run_slot(ij_k, valid, lane, hist_ij);
+        if (valid) {
+            slot_kk[e] = s_kk;
+            slot_ij[e] = s_ij;
+        }
+    }
+}
+
+// block 0 scans the kk bins, block 1 the ij bins: (start, group index) per
+// bin, the group count and offs[G] = E
+__global__ __launch_bounds__(1024) void wg_scan_kernel(const int* __restrict__ hist, int Bkk, int64_t* __restrict__ pre_kk,
+                                                       int64_t* __restrict__ pre_ij, int* __restrict__ offs_kk,
+                                                       int* __restrict__ offs_ij, int64_t* __restrict__ groups_kk,
+                                                       int64_t* __restrict__ groups_ij, int n)
+{
+    __shared__ int64_t wsum[16];
+    const bool ij = blockIdx.x != 0;
+    const int B = ij ? (1 << WG_IJ_BITS) : Bkk;
+    const int* h = ij ? hist + Bkk : hist;
+    int64_t* pre = ij ? pre_ij : pre_kk;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int per = (B + 1023) / 1024;
+    const int b0 = min(B, t * per), b1 = min(B, b0 + per);
+    int64_t s = 0;
+    for (int b = b0; b < b1; b++) s += CbCombine()(h[b]);
+    int64_t x = s;   // inclusive scan over the wave
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int64_t run = x - s;
+    for (int i = 0; i < w; i++) run += wsum[i];
+    for (int b = b0; b < b1; b++) {
+        pre[b] = run;
+        run += CbCombine()(h[b]);
+    }
+    if (t == 1023) {   // run = the grand total
+        const int64_t G = run >> 32;
+        *(ij ? groups_ij : groups_kk) = G;
+        (ij ? offs_ij : offs_kk)[G] = n;
+    }
+}
+
+__global__ __launch_bounds__(256) void wg_scatter_kernel(int64_t E, const uint32_t* __restrict__ key_kk,
+                                                         const uint32_t* __restrict__ key_ij,
+                                                         const int64_t* __restrict__ pre_kk,
+                                                         const int64_t* __restrict__ pre_ij,
+                                                         const int* __restrict__ slot_kk,
+                                                         const int* __restrict__ slot_ij, int* __restrict__ ptmp_kk,
+                                                         int* __restrict__ ptmp_ij, int64_t* __restrict__ gid_kk,
+                                                         int64_t* __restrict__ gid_ij, int* __restrict__ offs_kk,
+                                                         int* __restrict__ offs_ij)
+{
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = pre_kk[key_kk[e]], q = pre_ij[key_ij[e]];
+        const int sp = slot_kk[e], sq = slot_ij[e];
+        const int ps = (int)(p & 0xffffffff), pg = (int)(p >> 32), qs = (int)(q & 0xffffffff), qg = (int)(q >> 32);
+        ptmp_kk[ps + sp] = (int)e;
+        ptmp_ij[qs + sq] = (int)e;
+        gid_kk[e] = pg;
+        gid_ij[e] = qg;
+        if (sp == 0) offs_kk[pg] = ps;
+        if (sq == 0) offs_ij[qg] = qs;
+    }
+}
+
+// one wave per group, the (larger) ij groups first
+__global__ __launch_bounds__(64 * CB_WAVES) void wg_fix_kernel(int64_t n, const int* __restrict__ ptmp_kk,
+                                                               const int* __restrict__ offs_kk,
+                                                               const int64_t* __restrict__ groups_kk,
+                                                               const int64_t* __restrict__ gid_kk,
+                                                               int* __restrict__ perm_kk,
+                                                               const int* __restrict__ ptmp_ij,
+                                                               const int* __restrict__ offs_ij,
+                                                               const int64_t* __restrict__ groups_ij,
+                                                               const int64_t* __restrict__ gid_ij,
+                                                               int* __restrict__ perm_ij)
+{
+    __shared__ __attribute__((aligned(16))) int buf[CB_WAVES][CB_CAP];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int64_t Gi = *groups_ij, G = Gi + *groups_kk;
+    for (int64_t g = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6; g < G;
+         g += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+        if (g < Gi)
+            cb_fix_group(g, ptmp_ij, offs_ij, gid_ij, n, perm_ij, buf[w], lane);
+        else
+            cb_fix_group(g - Gi, ptmp_kk, offs_kk, gid_kk, n, perm_kk, buf[w], lane);
+    }
+}
+
 // target = coords[..., P/2, P/2] + float(delta), weight = float(w) for every
 // edge (DPVO.update after the update operator, dpvo.py:724-727), one launch
 // instead of three.  delta / w: fp16 rows with their own strides (the fused
@@ -874,6 +1036,60 @@ extern "C" int dpvo_window_keys(const int64_t* ii, const int64_t* jj, const int6
     DPVO_CHECK_ARG(ii && jj && kk && key_kk && key_ij && ctx && jslot, "null operand");
     hipLaunchKernelGGL(window_keys_kernel, dim3(grid_for(E, 256, 4096)), dim3(256), 0, as_stream(stream), ii, jj, kk,
                        E, M, base, ring, frames, key_kk, key_ij, ctx, jslot, flag);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" size_t dpvo_window_group_by_workspace_bytes(int64_t E, int kk_bits)
+{
+    if (kk_bits < 1 || kk_bits > CB_MAX_BITS) return 0;
+    return (size_t)wg_layout(E > 0 ? E : 1, kk_bits).total + 256;
+}
+
+extern "C" int dpvo_window_group_by(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t E, int64_t M,
+                                    int64_t base, int64_t ring, int64_t frames, int kk_bits, int64_t* ctx,
+                                    int64_t* jslot, int* flag, int64_t* kk_gid, int* kk_offs, int* kk_perm,
+                                    int64_t* kk_groups, int64_t* ij_gid, int* ij_offs, int* ij_perm,
+                                    int64_t* ij_groups, void* workspace, size_t workspace_bytes, void* stream)
+{
+    DPVO_CHECK_ARG(E >= 0 && E < (int64_t(1) << 31), "bad size");
+    DPVO_CHECK_ARG(M > 0 && ring > 0 && frames > 0, "M > 0, ring > 0 and frames > 0 required");
+    DPVO_CHECK_ARG(kk_bits >= 1 && kk_bits <= CB_MAX_BITS, "kk_bits must be 1..22");
+    DPVO_CHECK_ARG(kk_groups && kk_offs && ij_groups && ij_offs, "CSR outputs missing");
+    hipStream_t st = as_stream(stream);
+    if (E == 0) {
+        DPVO_CHECK_HIP(hipMemsetAsync(kk_groups, 0, sizeof(int64_t), st));
+        DPVO_CHECK_HIP(hipMemsetAsync(kk_offs, 0, sizeof(int), st));
+        DPVO_CHECK_HIP(hipMemsetAsync(ij_groups, 0, sizeof(int64_t), st));
+        DPVO_CHECK_HIP(hipMemsetAsync(ij_offs, 0, sizeof(int), st));
+        return 0;
+    }
+    DPVO_CHECK_ARG(ii && jj && kk && ctx && jslot && kk_gid && kk_perm && ij_gid && ij_perm, "null operand");
+    const WgLayout L = wg_layout(E, kk_bits);
+    DPVO_CHECK_ARG(workspace != nullptr && workspace_bytes >= (size_t)L.total + 256, "workspace too small");
+    char* ws = (char*)(((uintptr_t)workspace + 255) & ~uintptr_t(255));
+    const int Bkk = 1 << kk_bits;
+    int* hist = (int*)(ws + L.hist);
+    int64_t* pre_kk = (int64_t*)(ws + L.pre_kk);
+    int64_t* pre_ij = (int64_t*)(ws + L.pre_ij);
+    int* slot_kk = (int*)(ws + L.slot_kk);
+    int* slot_ij = (int*)(ws + L.slot_ij);
+    int* ptmp_kk = (int*)(ws + L.ptmp_kk);
+    int* ptmp_ij = (int*)(ws + L.ptmp_ij);
+    uint32_t* key_kk = (uint32_t*)(ws + L.key_kk);
+    uint32_t* key_ij = (uint32_t*)(ws + L.key_ij);
+    const unsigned gn = grid_for(E, 256, 2048);
+    DPVO_CHECK_HIP(hipMemsetAsync(hist, 0, 4 * (size_t)(Bkk + (1 << WG_IJ_BITS)), st));
+    hipLaunchKernelGGL(wg_hist_kernel, dim3(gn), dim3(256), 0, st, ii, jj, kk, E, M, base, ring, frames,
+                       (uint32_t)(Bkk - 1), ctx, jslot, flag, hist, hist + Bkk, slot_kk, slot_ij, key_kk, key_ij);
+    hipLaunchKernelGGL(wg_scan_kernel, dim3(2), dim3(1024), 0, st, hist, Bkk, pre_kk, pre_ij, kk_offs, ij_offs,
+                       kk_groups, ij_groups, (int)E);
+    hipLaunchKernelGGL(wg_scatter_kernel, dim3(gn), dim3(256), 0, st, E, key_kk, key_ij, pre_kk, pre_ij, slot_kk,
+                       slot_ij, ptmp_kk, ptmp_ij, kk_gid, ij_gid, kk_offs, ij_offs);
+    const int64_t waves = std::min<int64_t>(E, Bkk) + std::min<int64_t>(E, 1 << WG_IJ_BITS);
+    const unsigned gf = grid_for(waves * 64, 64 * CB_WAVES, 2048);
+    hipLaunchKernelGGL(wg_fix_kernel, dim3(gf), dim3(64 * CB_WAVES), 0, st, E, ptmp_kk, kk_offs, kk_groups, kk_gid,
+                       kk_perm, ptmp_ij, ij_offs, ij_groups, ij_gid, ij_perm);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

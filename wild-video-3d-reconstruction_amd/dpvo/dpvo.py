@@ -234,21 +234,29 @@ class DPVO:
         self.pg.ii = torch.cat([self.pg.ii, self.ix[kk]])
         self.pg.net = torch.cat([self.pg.net, torch.zeros(1, len(kk), self.DIM, **self.kwargs)], dim=1)
 
-    def remove_factors(self, m, store):
+    def remove_factors(self, m, store, counts=None):
         """Boolean-mask compaction of the edge state (dpvo.py:349-364).  Each
         ``x[mask]`` is a host synchronisation (the output size); here the mask
-        becomes an index once (one sync per side) and every tensor is
-        gathered with it.  store: True (keep the removed edges as inactive
-        factors), False, or a mask inside m: only those are kept."""
+        becomes an index once per side and every tensor is gathered with it.
+        store: True (keep the removed edges as inactive factors), False, or a
+        mask inside m: only those are kept.  counts: (edges kept, edges
+        stored) when the caller already read them (keyframe() does, in its one
+        host read): the indices then come from nonzero_static, with no
+        synchronisation at all."""
         assert self.pg.ii.numel() == self.pg.weight.shape[1]
+        if counts is None:
+            index = lambda mask, _: torch.nonzero(mask).squeeze(1)
+            counts = (None, None)
+        else:
+            index = lambda mask, size: torch.nonzero_static(mask, size=size).squeeze(1)
         if store is not False:
-            rem = torch.nonzero(m if store is True else store).squeeze(1)
+            rem = index(m if store is True else store, counts[1])
             self.pg.ii_inac = torch.cat((self.pg.ii_inac, self.pg.ii[rem]))
             self.pg.jj_inac = torch.cat((self.pg.jj_inac, self.pg.jj[rem]))
             self.pg.kk_inac = torch.cat((self.pg.kk_inac, self.pg.kk[rem]))
             self.pg.weight_inac = torch.cat((self.pg.weight_inac, self.pg.weight[:, rem]), dim=1)
             self.pg.target_inac = torch.cat((self.pg.target_inac, self.pg.target[:, rem]), dim=1)
-        keep = torch.nonzero(~m).squeeze(1)
+        keep = index(~m, counts[0])
         self.pg.weight = self.pg.weight[:, keep]
         self.pg.target = self.pg.target[:, keep]
         self.pg.ii, self.pg.jj, self.pg.kk = self.pg.ii[keep], self.pg.jj[keep], self.pg.kk[keep]
@@ -299,15 +307,12 @@ class DPVO:
             # operator's SoftAgg over kk and temporal neighbours, and BA's
             # per-patch reduction all read this CSR
             if self._window_keys():
-                # both group keys and the ring slots (context rows, corr) in one launch
-                # (an edge outside the window sets the deferred failure word: the
-                # next keyframe() / check_ba() raises)
-                key_kk, key_ij, ctx_idx, jslot = update_ops.window_keys(self.pg.ii, self.pg.jj, self.pg.kk, self.M,
-                                                                        self.n - 64, self.M * self.pmem, self.pmem,
-                                                                        flag=self._ba_status if defer
-                                                                        else self._ba_fail)
-                kk_groups = update_ops.group_by(key_kk, key_bits=update_ops.key_bits_for(64 * self.M))
-                ij_groups = update_ops.group_by(key_ij, key_bits=12)
+                # the ring slots (context rows, corr) and both group-bys over the
+                # window keys in four launches (an edge outside the window sets
+                # the deferred failure word: the next keyframe() / check_ba() raises)
+                ctx_idx, jslot, kk_groups, ij_groups = update_ops.window_group_by(
+                    self.pg.ii, self.pg.jj, self.pg.kk, self.M, self.n - 64, self.M * self.pmem, self.pmem,
+                    flag=self._ba_status if defer else self._ba_fail)
                 slots = (ctx_idx, jslot)
             else:
                 kk_groups, ij_groups = self._kk_groups(), self._ij_groups()
@@ -430,27 +435,38 @@ class DPVO:
         """drop a redundant keyframe, retire old edges (dpvo.py:605-658)."""
         k = self.n - self.cfg.KEYFRAME_INDEX
         i, j = k - 1, k + 1
-        # one host read for both directions (the reference reads each, :609),
-        # for the deferred BA status of the update()s since the last one, and
-        # for the pose-NaN check of the keep path (:647, its own read there)
-        vals = torch.cat([self._motionmag_dev(i, j), self._ba_fail.float(),
-                          torch.isnan(self.pg.poses_[k]).any().float()[None]]).tolist()
+        RW = self.cfg.REMOVAL_WINDOW
+        ii, jj, kk = self.pg.ii, self.pg.jj, self.pg.kk
+        E = kk.numel()
+        # the edge masks of both outcomes, formed before the decision: keep
+        # (edges whose patch left the removal window, :654-658) and drop (the
+        # edges of frame k go, :616-617, and the retirement runs after the
+        # frames above k moved down by one); their sizes ride on the one host
+        # read below, so the compaction needs no synchronisation of its own
+        old_keep = self.ix[kk] < self.n - RW
+        drop = (ii == k) | (jj == k)
+        later = ii > k
+        kk_d = torch.where(later, kk - self.M, kk)
+        old_d = (self.ix[kk_d] < self.n - 1 - RW) & ~drop
+        rm_d = old_d | drop
+        # one host read for both motion directions (the reference reads each,
+        # :609), the deferred BA status of the update()s since the last one,
+        # the pose-NaN check of the keep path (:647, its own read there) and
+        # the compaction sizes
+        sums = torch.stack([old_keep.sum(), old_d.sum(), rm_d.sum()]).double()
+        vals = torch.cat([self._motionmag_dev(i, j).double(), self._ba_fail.double(),
+                          torch.isnan(self.pg.poses_[k]).any().double()[None], sums]).tolist()
         self.check_ba(int(vals[2]))
+        n_old_keep, n_old_d, n_rm_d = (int(v) for v in vals[4:7])
         m = vals[0] + vals[1]
-        drop = None
         if m / 2 < self.cfg.KEYFRAME_THRESH:
             t0, t1 = self.pg.tstamps_[k - 1:k + 1].tolist()
             dP = SE3(self.pg.poses_[k]) * SE3(self.pg.poses_[k - 1]).inv()
             self.pg.delta[t1] = (t0, dP)
-            # the edges of frame k go (remove_factors(store=False), :616-617);
-            # they are compacted away together with the retired ones below (one
-            # gather of the edge state instead of two; stable, so the same order)
-            drop = (self.pg.ii == k) | (self.pg.jj == k)
             # x[x > k] -= 1 as selects: no mask-size synchronisation
-            later = self.pg.ii > k
-            self.pg.kk = torch.where(later, self.pg.kk - self.M, self.pg.kk)
-            self.pg.ii = torch.where(later, self.pg.ii - 1, self.pg.ii)
-            self.pg.jj = torch.where(self.pg.jj > k, self.pg.jj - 1, self.pg.jj)
+            self.pg.kk = kk_d
+            self.pg.ii = torch.where(later, ii - 1, ii)
+            self.pg.jj = torch.where(jj > k, jj - 1, jj)
             # frames k+1 .. n-1 move down by one: one gather per buffer (the
             # reference's per-frame loop, :626-639, reads each source before
             # overwriting it, so a simultaneous shift is the same)
@@ -469,15 +485,13 @@ class DPVO:
                 self.image_buffer_[dst % self.mem] = self.image_buffer_[src % self.mem]
             self.n -= 1
             self.pg.m -= self.M
+            # frame k's edges and the retired ones in one compaction (stable,
+            # so the same order as the reference's two)
+            self.remove_factors(rm_d, store=old_d, counts=(E - n_rm_d, n_old_d))
         elif vals[3]:
             raise Exception("Error: the estimated pose is nan!")
-        # edges whose patch left the removal window become inactive (:654-658)
-        old = self.ix[self.pg.kk] < self.n - self.cfg.REMOVAL_WINDOW
-        if drop is None:
-            self.remove_factors(old, store=True)
         else:
-            old &= ~drop
-            self.remove_factors(old | drop, store=old)
+            self.remove_factors(old_keep, store=True, counts=(E - n_old_keep, n_old_keep))
 
     # ------------------------------------------------------------------ global BA (C4)
     def compute_keyframe_distance(self, i, j, beta=0.5):

@@ -202,6 +202,33 @@ def window_keys(ii, jj, kk, M, base, ring, frames, flag=None):
     return out[0], out[1], out[2], out[3]
 
 
+def window_group_by(ii, jj, kk, M, base, ring, frames, flag=None):
+    """window_keys + group_by(key_kk, key_bits_for(64 M)) + group_by(key_ij, 12)
+    in one memset and four launches (dpvo_window_group_by; same outputs):
+    -> (ctx, jslot, kk_groups, ij_groups), each groups tuple as group_by's."""
+    H.on_gpu(ii, jj, kk)
+    ii, jj, kk = H.idx64(ii), H.idx64(jj), H.idx64(kk)
+    E = kk.numel()
+    if ii.numel() != E or jj.numel() != E:
+        raise RuntimeError("window_group_by: ii, jj and kk must have the same length")
+    bits = key_bits_for(64 * int(M))
+    nbytes = H.lib().dpvo_window_group_by_workspace_bytes(E, bits)
+    if nbytes == 0:
+        raise RuntimeError("window_group_by: 64 M above the counting-sort range")
+    dev = kk.device
+    slots = torch.empty(2, E, dtype=torch.int64, device=dev)
+    gid = torch.empty(2, E, dtype=torch.int64, device=dev)
+    offs = torch.empty(2, E + 1, dtype=torch.int32, device=dev)
+    perm = torch.empty(2, max(E, 1), dtype=torch.int32, device=dev)
+    groups = torch.empty(2, 1, dtype=torch.int64, device=dev)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    H.check(H.lib().dpvo_window_group_by(
+        H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(M), int(base), int(ring), int(frames), bits, H.ptr(slots[0]),
+        H.ptr(slots[1]), H.ptr(flag), H.ptr(gid[0]), H.ptr(offs[0]), H.ptr(perm[0]), H.ptr(groups[0]), H.ptr(gid[1]),
+        H.ptr(offs[1]), H.ptr(perm[1]), H.ptr(groups[1]), H.ptr(ws), nbytes, H.stream_of(kk)))
+    return (slots[0], slots[1], (gid[0], offs[0], perm[0], groups[0]), (gid[1], offs[1], perm[1], groups[1]))
+
+
 def edge_targets(centre, delta, weight):
     """(centre + delta.float(), weight.float()) for [1, E, 2] views (fp32 centre,
     fp16 delta / weight with unit component stride) in one launch."""
