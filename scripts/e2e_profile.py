@@ -56,7 +56,7 @@ def main():
             return r
         setattr(obj, name, g)
 
-    wrap(slam.network, "patchify", "patchify")
+    wrap(slam.network.patchify, "forward", "patchify")
     wrap(slam, "append_factors", "append_factors")
     wrap(slam, "update", "update")
     wrap(slam, "remove_factors", "remove_factors")

@@ -59,3 +59,37 @@ def test_shims_refuse_cpu_tensors():
         cuda_ba.neighbors(torch.zeros(3, dtype=torch.long), torch.zeros(3, dtype=torch.long))
     with pytest.raises(RuntimeError, match="GPU"):
         cuda_corr.patchify_forward(torch.zeros(1, 2, 4, 4), torch.zeros(1, 1, 2), 1)
+
+
+def prototypes():
+    """name -> [parameter type class] for every function the header declares"""
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    out = {}
+    for name, params in re.findall(r"\b(dpvo_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src):
+        ps = [q.strip() for q in params.split(",") if q.strip() and q.strip() != "void"]
+        out[name] = [klass(q) for q in ps]
+    return out
+
+
+def klass(c_param):
+    if "*" in c_param:
+        return "ptr"
+    t = c_param.rsplit(" ", 1)[0].replace("const ", "").strip()
+    return {"int64_t": "i64", "size_t": "size", "int": "int", "float": "float", "double": "double"}[t]
+
+
+def test_ctypes_signatures_match_the_header():
+    """every ctypes binding has the header's arity and argument classes (a
+    miscounted binding fails here instead of as a ctypes error on the GPU)"""
+    import ctypes
+    import _dpvo_hot as H
+    cls = {ctypes.c_void_p: "ptr", ctypes.c_char_p: "ptr", ctypes.c_int64: "i64", ctypes.c_size_t: "size",
+           ctypes.c_int: "int", ctypes.c_float: "float", ctypes.c_double: "double"}
+    protos = prototypes()
+    bad = {}
+    for name, (_, argtypes) in H._SIGNATURES.items():
+        got = [cls[a] for a in argtypes]
+        if protos.get(name) != got:
+            bad[name] = (protos.get(name), got)
+    assert not bad, bad

@@ -2173,7 +2173,7 @@ __global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
     constexpr int n = 6 * NN;
     static_assert(n < 64, "one lane per row plus the g row");
     __shared__ float xs[64];
-    if (*(volatile int*)p.status != 0) return;
+    const int status = *(volatile int*)p.status;   // checked once the system loads below are in flight
     const int lane = threadIdx.x;
     const int nup = p.nup;
     float a[n];
@@ -2188,6 +2188,7 @@ __global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
         const int off = grow ? c : rowv ? c * (2 * n - c + 1) / 2 - c : 0;
         a[c] = __builtin_nontemporal_load(p.H + (base + off));
     }
+    if (status != 0) return;
 #pragma unroll
     for (int c = 0; c < n; c++) {
         const bool keep = (rowv && c <= lane) || grow;
@@ -2237,126 +2238,11 @@ __global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
     }
 }
 
-// The same solve with the factor loop ROLLED over an LDS-resident system.
-// The register kernel above unrolls the n^2/2 column updates into straight-line
-// code -- 67 KB for 10 poses, past the 64 KB instruction cache, and it starts
-// cold after every Hessian pass: 31 us, nearly all of it instruction fetch.
-// Here the loads and the LDS fill unroll over a 64-entry row (~2 KB of code),
-// the factor and back substitution are loops.  Lane i owns row i of the lower
-// triangle of [S; g^T] (row n = g), A[i][c] at i * BDL_LD + c.  Column k: the
-// pivot is a broadcast read, lane i > k scales its L[i][k] and publishes it in
-// Lk[i] (0 for i <= k, so every lane runs the same float4 chunks over columns
-// (k & ~3) .. n and entries at or left of column k subtract zero), then
-// A[i][c] -= L[i][k] L[c][k] -- the register kernel's update, term for term.
-// Back substitution column-wise: x_j = z_j / L[j][j] (z_j from lane j by
-// readlane), then lanes i < j take z_i -= L[j][i] x_j (row j: consecutive
-// words across lanes).  One wave: LDS ops complete in order, so a wave
-// barrier (no s_barrier) orders the column publish before the reads.
-constexpr int BDL_LD = 68;   // row stride in floats: 16-byte aligned rows
-
-__global__ __launch_bounds__(64) void bd_solve_lds_kernel(BdParams p)
-{
-    __shared__ __attribute__((aligned(16))) float A[64 * BDL_LD];
-    __shared__ __attribute__((aligned(16))) float Lk[64];
-    __shared__ float xs[64];
-    if (*(volatile int*)p.status != 0) return;
-    const int lane = threadIdx.x;
-    const int n = 6 * p.N, nup = p.nup;
-    const bool rowv = lane < n, grow = lane == n;
-    float* Ar = A + lane * BDL_LD;
-    {
-        // row `lane` = column `lane` of the upper-stored system, entry c at
-        // tri_up(c, lane); the g row at nup + c.  All 64 loads issued first.
-        const int base = rowv ? lane : grow ? nup : 0;
-        float a[64];
-#pragma unroll
-        for (int c = 0; c < 64; c++) {
-            const int off = grow ? c : rowv ? c * (2 * n - c + 1) / 2 - c : 0;
-            const bool keep = c < n && ((rowv && c <= lane) || grow);
-            a[c] = keep ? __builtin_nontemporal_load(p.H + (base + off)) : 0.f;
-        }
-#pragma unroll
-        for (int c = 0; c < 64; c++)
-            if (c == lane && rowv) a[c] += 1e-4f * a[c] + 1.0f;   // S += diag(1e-4 S + 1), ba_cuda.cu:517-518
-#pragma unroll
-        for (int c = 0; c < 64; c += 4) *(float4*)(Ar + c) = make_float4(a[c], a[c + 1], a[c + 2], a[c + 3]);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    int fail = 0;
-    for (int k = 0; k < n; k++) {
-        const float d = A[k * BDL_LD + k];
-        if (!(d > 0.f)) {
-            fail = k + 1;
-            break;
-        }
-        const float l = sqrtf(d), il = 1.0f / l;
-        float lik = 0.f;
-        if (lane > k && lane <= n) {
-            lik = Ar[k] * il;
-            Ar[k] = lik;
-        }
-        if (lane == k) Ar[k] = l;
-        Lk[lane] = lik;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (int c = k & ~3; c < n; c += 4) {
-            float4 v = *(const float4*)(Ar + c);
-            const float4 lc = *(const float4*)(Lk + c);
-            v.x -= lik * lc.x;
-            v.y -= lik * lc.y;
-            v.z -= lik * lc.z;
-            v.w -= lik * lc.w;
-            *(float4*)(Ar + c) = v;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (fail) {
-        if (lane == 0) atomicExch(p.status, fail);
-        return;
-    }
-    // z = row n (L^-1 g); lane i keeps z_i, then x_i
-    float z = lane < n ? A[n * BDL_LD + lane] : 0.f;
-    for (int j = n - 1; j >= 0; j--) {
-        const float lji = A[j * BDL_LD + lane];   // L[j][lane] for lane < j
-        const float ljj = A[j * BDL_LD + j];
-        const float xj = rdl(z, j) / ljj;
-        if (lane < j) z -= lji * xj;
-        if (lane == j) z = xj;
-    }
-    if (lane < n) {
-        xs[lane] = z;
-        p.dX[lane] = z;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane < p.N) {
-        float* P = p.poses + (int64_t)(p.t0 + lane) * 7;
-        const float t0v[3] = {P[0], P[1], P[2]}, q0v[4] = {P[3], P[4], P[5], P[6]};
-        float xi[6], t1v[3], q1v[4];
-#pragma unroll
-        for (int k = 0; k < 6; k++) xi[k] = xs[6 * lane + k];
-        retrSE3(xi, t0v, q0v, t1v, q1v);
-        P[0] = t1v[0]; P[1] = t1v[1]; P[2] = t1v[2];
-        P[3] = q1v[0]; P[4] = q1v[1]; P[5] = q1v[2]; P[6] = q1v[3];
-    }
-}
-
 static void bd_solve_launch(const BdParams& p, hipStream_t s)
 {
-    static const bool blocked = getenv("DPVO_BD_BLOCK_SOLVE") != nullptr;   // A/B switches: the workgroup solver,
-    static const bool regs = getenv("DPVO_BD_REG_SOLVE") != nullptr;        // the register-resident wave solver
+    static const bool blocked = getenv("DPVO_BD_BLOCK_SOLVE") != nullptr;   // A/B switch: the workgroup solver
     if (blocked || p.N > 10) {
         hipLaunchKernelGGL(bd_solve_kernel, dim3(1), dim3(256), 0, s, p);
-        return;
-    }
-    if (!regs) {
-        hipLaunchKernelGGL(bd_solve_lds_kernel, dim3(1), dim3(64), 0, s, p);
         return;
     }
     switch (p.N) {

@@ -745,7 +745,9 @@ __global__ __launch_bounds__(256) void wg_hist_kernel(const int64_t* __restrict_
 }
 
 // block 0 scans the kk bins, block 1 the ij bins: (start, group index) per
-// bin, the group count and offs[G] = E
+// bin, the group count and offs[G] = E.  8192 bins per round: thread t loads
+// bins 8t .. 8t+7 (two 16-byte loads, coalesced), scans them in registers,
+// one block scan of the thread sums, 64-byte coalesced stores of the results.
 __global__ __launch_bounds__(1024) void wg_scan_kernel(const int* __restrict__ hist, int Bkk, int64_t* __restrict__ pre_kk,
                                                        int64_t* __restrict__ pre_ij, int* __restrict__ offs_kk,
                                                        int* __restrict__ offs_ij, int64_t* __restrict__ groups_kk,
@@ -757,25 +759,48 @@ __global__ __launch_bounds__(1024) void wg_scan_kernel(const int* __restrict__ h
     const int* h = ij ? hist + Bkk : hist;
     int64_t* pre = ij ? pre_ij : pre_kk;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int per = (B + 1023) / 1024;
-    const int b0 = min(B, t * per), b1 = min(B, b0 + per);
-    int64_t s = 0;
-    for (int b = b0; b < b1; b++) s += CbCombine()(h[b]);
-    int64_t x = s;   // inclusive scan over the wave
-    for (int o = 1; o < 64; o <<= 1) {
-        const int64_t y = __shfl_up(x, o);
-        if (lane >= o) x += y;
+    int64_t carry = 0;
+    for (int base = 0; base < B; base += 8192) {
+        const int b0 = base + 8 * t;
+        int c[8];
+        if (b0 + 8 <= B && ((uintptr_t)(h + b0) & 15) == 0) {
+            const int4 x = *(const int4*)(h + b0), y = *(const int4*)(h + b0 + 4);
+            c[0] = x.x; c[1] = x.y; c[2] = x.z; c[3] = x.w;
+            c[4] = y.x; c[5] = y.y; c[6] = y.z; c[7] = y.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; j++) c[j] = b0 + j < B ? h[b0 + j] : 0;
+        }
+        int64_t loc[8], s = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            loc[j] = s;
+            s += CbCombine()(c[j]);
+        }
+        int64_t x = s;   // inclusive scan over the wave
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        int64_t off = carry, tot = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) {
+            const int64_t v = wsum[i];
+            off += i < w ? v : 0;
+            tot += v;
+        }
+        const int64_t ex = off + x - s;
+#pragma unroll
+        for (int j = 0; j < 8; j++)
+            if (b0 + j < B) pre[b0 + j] = ex + loc[j];
+        carry += tot;
+        __syncthreads();   // wsum is rewritten next round
     }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    int64_t run = x - s;
-    for (int i = 0; i < w; i++) run += wsum[i];
-    for (int b = b0; b < b1; b++) {
-        pre[b] = run;
-        run += CbCombine()(h[b]);
-    }
-    if (t == 1023) {   // run = the grand total
-        const int64_t G = run >> 32;
+    if (t == 0) {   // carry = the grand total
+        const int64_t G = carry >> 32;
         *(ij ? groups_ij : groups_kk) = G;
         (ij ? offs_ij : offs_kk)[G] = n;
     }
