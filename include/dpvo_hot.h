@@ -228,6 +228,13 @@ int dpvo_lie_forward(int op, int group, int dtype, const void* X, const void* Y,
 int dpvo_lie_backward(int op, int group, int dtype, const void* grad, const void* X, const void* Y, void* dX,
                       void* dY, int64_t n, void* stream);
 
+/* DPVO.__call__'s DAMPED_LINEAR motion model (dpvo.py:816-825) in one launch:
+ * poses[n] = Exp(s * Log(poses[n-1] * poses[n-2]^-1)) * poses[n-1], SE3 rows
+ * [t, q] fp32, s = MOTION_DAMPING * dt ratio (n >= 2). */
+int dpvo_pose_extrapolate(float* poses, int64_t n, float s, void* stream);
+/* out = a * b^-1 for single SE3 rows (keyframe()'s dP, dpvo.py:613). */
+int dpvo_pose_relative(const float* a, const float* b, float* out, void* stream);
+
 /* ------------------------------------------------------------------------
  * projective ops -- fused forms of dpvo/projective_ops.py
  * --------------------------------------------------------------------- */
@@ -467,6 +474,15 @@ int dpvo_window_group_by(const int64_t* ii, const int64_t* jj, const int64_t* kk
                          int64_t* kk_gid, int* kk_offs, int* kk_perm, int64_t* kk_groups, int64_t* ij_gid,
                          int* ij_offs, int* ij_perm, int64_t* ij_groups, void* workspace, size_t workspace_bytes,
                          void* stream);
+
+/* DPVO.__call__'s edge append (dpvo.py:756-769,799-800) in one launch:
+ * out = [old edges; forward edges (patches of frames [n-r, n-1) -> frame n-1);
+ * backward edges (frame n-1's patches -> frames [n-r, n), patch-major)], with
+ * ii = ix[kk]; n = frame count after the new frame, r = PATCH_LIFETIME.
+ * Outputs hold E + dpvo_append_edges_count(n, M, r) int64 entries. */
+int64_t dpvo_append_edges_count(int64_t n, int64_t M, int64_t r);
+int dpvo_append_edges(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t E, const int64_t* ix, int64_t n,
+                      int64_t M, int64_t r, int64_t* ii_out, int64_t* jj_out, int64_t* kk_out, void* stream);
 
 /* DPVO.update after the update operator (dpvo.py:724-727): target[e] =
  * centre[e] + float(delta[e]), weight[e] = float(w[e]), both fp32 [E][2]

@@ -56,6 +56,8 @@ _SIGNATURES = {
     "dpvo_neighbors": (_ip, [_vp, _vp, _i64, _vp, _vp, _vp, _sz, _vp]),
     "dpvo_lie_forward": (_ip, [_ip, _ip, _ip, _vp, _vp, _vp, _i64, _vp]),
     "dpvo_lie_backward": (_ip, [_ip, _ip, _ip, _vp, _vp, _vp, _vp, _vp, _i64, _vp]),
+    "dpvo_pose_extrapolate": (_ip, [_vp, _i64, _fp, _vp]),
+    "dpvo_pose_relative": (_ip, [_vp, _vp, _vp, _vp]),
     "dpvo_transform": (_ip, [_vp, _vp, _ip, _vp, _vp, _vp, _vp, _i64, _ip, _vp, _vp, _vp]),
     "dpvo_point_cloud": (_ip, [_vp, _vp, _ip, _vp, _vp, _i64, _ip, _vp, _vp]),
     "dpvo_motion_mag": (_ip, [_vp, _vp, _ip, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _fp, _vp, _vp]),
@@ -80,6 +82,8 @@ _SIGNATURES = {
     "dpvo_rowchain3": (_ip, [_vp, _vp, _vp, _vp]),
     "dpvo_rowchain_gated": (_ip, [_vp, _vp, _vp, _vp]),
     "dpvo_rowadd_ln": (_ip, [_vp, _vp]),
+    "dpvo_append_edges_count": (_i64, [_i64, _i64, _i64]),
+    "dpvo_append_edges": (_ip, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),
     "dpvo_edge_targets": (_ip, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp]),
     "dpvo_window_keys": (_ip, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dpvo_window_group_by_workspace_bytes": (_sz, [_i64, _ip]),

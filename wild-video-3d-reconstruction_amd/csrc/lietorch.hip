@@ -212,6 +212,43 @@ extern "C" int dpvo_lie_forward(int op, int group, int dtype, const void* X, con
     return 0;
 }
 
+// DPVO.__call__'s DAMPED_LINEAR motion model (dpvo.py:816-825) in one
+// launch instead of five lietorch calls from Python (inv, mul, log, the scalar
+// product, exp, mul): poses[n] = Exp(s Log(poses[n-1] poses[n-2]^-1)) poses[n-1],
+// s = MOTION_DAMPING * dt ratio rounded to fp32 (as torch rounds the scalar).
+// The same SE3 functions the lietorch kernels use, values kept in registers
+// between them (fp32 either way).
+__global__ void pose_extrapolate_kernel(float* poses, int64_t n, float s)
+{
+    const SE3<float> P1 = SE3<float>::load(poses + (n - 1) * 7), P2 = SE3<float>::load(poses + (n - 2) * 7);
+    float xi[6];
+    P1.mul(P2.inv()).Log(xi);
+    for (int k = 0; k < 6; k++) xi[k] = xi[k] * s;
+    SE3<float>::Exp(xi).mul(P1).store(poses + n * 7);
+}
+
+// keyframe()'s relative pose of a dropped frame (dpvo.py:613): out = a b^-1
+__global__ void pose_relative_kernel(const float* a, const float* b, float* out)
+{
+    SE3<float>::load(a).mul(SE3<float>::load(b).inv()).store(out);
+}
+
+extern "C" int dpvo_pose_extrapolate(float* poses, int64_t n, float s, void* stream)
+{
+    DPVO_CHECK_ARG(poses != nullptr && n >= 2, "poses[n-2], poses[n-1] needed (n >= 2)");
+    hipLaunchKernelGGL(pose_extrapolate_kernel, dim3(1), dim3(1), 0, as_stream(stream), poses, n, s);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_pose_relative(const float* a, const float* b, float* out, void* stream)
+{
+    DPVO_CHECK_ARG(a && b && out, "null operand");
+    hipLaunchKernelGGL(pose_relative_kernel, dim3(1), dim3(1), 0, as_stream(stream), a, b, out);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
 extern "C" int dpvo_lie_backward(int op, int group, int dtype, const void* grad, const void* X, const void* Y,
                                  void* dX, void* dY, int64_t n, void* stream)
 {

@@ -853,6 +853,40 @@ __global__ __launch_bounds__(64 * CB_WAVES) void wg_fix_kernel(int64_t n, const 
     }
 }
 
+// DPVO.__call__'s edge append (dpvo.py:756-769, 799-800): the old edge list
+// followed by the forward edges (patches of frames [n - r, n - 1) into frame
+// n - 1) and the backward edges (frame n - 1's patches into frames
+// [n - r, n), patch-major as flatmeshgrid(indexing="ij") lists them), with
+// ii = ix[kk] -- one launch instead of two aranges + meshgrid per direction,
+// the concatenations and the ix gather.  n: the frame count after the new
+// frame was added.
+__global__ __launch_bounds__(256) void append_edges_kernel(const int64_t* __restrict__ ii, const int64_t* __restrict__ jj,
+                                                           const int64_t* __restrict__ kk, int64_t E,
+                                                           const int64_t* __restrict__ ix, int64_t n, int64_t M,
+                                                           int64_t r, int64_t* __restrict__ ii_o,
+                                                           int64_t* __restrict__ jj_o, int64_t* __restrict__ kk_o)
+{
+    const int64_t f0 = M * (n - r > 0 ? n - r : 0), f1 = M * (n - 1 > 0 ? n - 1 : 0);
+    const int64_t nf = f1 - f0;
+    const int64_t b0 = f1, j0 = n - r > 0 ? n - r : 0, nj = n - j0;
+    const int64_t nb = (M * n - b0) * nj;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E + nf + nb;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        int64_t i, j, k;
+        if (e < E) {
+            i = ii[e], j = jj[e], k = kk[e];
+        } else if (e < E + nf) {
+            k = f0 + (e - E), j = n - 1, i = ix[k];
+        } else {
+            const int64_t t = e - E - nf;
+            k = b0 + t / nj, j = j0 + t % nj, i = ix[k];
+        }
+        ii_o[e] = i;
+        jj_o[e] = j;
+        kk_o[e] = k;
+    }
+}
+
 // target = coords[..., P/2, P/2] + float(delta), weight = float(w) for every
 // edge (DPVO.update after the update operator, dpvo.py:724-727), one launch
 // instead of three.  delta / w: fp16 rows with their own strides (the fused
@@ -1115,6 +1149,27 @@ extern "C" int dpvo_window_group_by(const int64_t* ii, const int64_t* jj, const 
     const unsigned gf = grid_for(waves * 64, 64 * CB_WAVES, 2048);
     hipLaunchKernelGGL(wg_fix_kernel, dim3(gf), dim3(64 * CB_WAVES), 0, st, E, ptmp_kk, kk_offs, kk_groups, kk_gid,
                        kk_perm, ptmp_ij, ij_offs, ij_groups, ij_gid, ij_perm);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int64_t dpvo_append_edges_count(int64_t n, int64_t M, int64_t r)
+{
+    if (n < 1 || M < 1 || r < 1) return -1;
+    const int64_t f0 = M * (n - r > 0 ? n - r : 0), f1 = M * (n - 1 > 0 ? n - 1 : 0), j0 = n - r > 0 ? n - r : 0;
+    return (f1 - f0) + (M * n - f1) * (n - j0);
+}
+
+extern "C" int dpvo_append_edges(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t E, const int64_t* ix,
+                                 int64_t n, int64_t M, int64_t r, int64_t* ii_out, int64_t* jj_out, int64_t* kk_out,
+                                 void* stream)
+{
+    const int64_t add = dpvo_append_edges_count(n, M, r);
+    DPVO_CHECK_ARG(add >= 0 && E >= 0, "n >= 1, M >= 1, PATCH_LIFETIME >= 1 and E >= 0 required");
+    DPVO_CHECK_ARG(ix && ii_out && jj_out && kk_out && (E == 0 || (ii && jj && kk)), "null operand");
+    if (E + add == 0) return 0;
+    hipLaunchKernelGGL(append_edges_kernel, dim3(grid_for(E + add, 256, 4096)), dim3(256), 0, as_stream(stream), ii,
+                       jj, kk, E, ix, n, M, r, ii_out, jj_out, kk_out);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

@@ -461,8 +461,7 @@ class DPVO:
         m = vals[0] + vals[1]
         if m / 2 < self.cfg.KEYFRAME_THRESH:
             t0, t1 = self.pg.tstamps_[k - 1:k + 1].tolist()
-            dP = SE3(self.pg.poses_[k]) * SE3(self.pg.poses_[k - 1]).inv()
-            self.pg.delta[t1] = (t0, dP)
+            self.pg.delta[t1] = (t0, pops.pose_relative(self.pg.poses_[k], self.pg.poses_[k - 1]))
             # x[x > k] -= 1 as selects: no mask-size synchronisation
             self.pg.kk = kk_d
             self.pg.ii = torch.where(later, ii - 1, ii)
@@ -600,10 +599,9 @@ class DPVO:
         self.pg.index_map_[n + 1] = self.pg.m + self.pg.M
         if n > 1:
             if self.cfg.MOTION_MODEL == "DAMPED_LINEAR":
-                P1, P2 = SE3(self.pg.poses_[n - 1]), SE3(self.pg.poses_[n - 2])
+                # Exp(s Log(P1 P2^-1)) P1 in one launch (five lietorch calls in the reference)
                 *_, a, b, c = [1] * 3 + self.tlist
-                xi = self.cfg.MOTION_DAMPING * ((c - b) / (b - a)) * (P1 * P2.inv()).log()
-                self.pg.poses_[n] = (SE3.exp(xi) * P1).data
+                pops.pose_extrapolate(self.pg.poses_, n, self.cfg.MOTION_DAMPING * ((c - b) / (b - a)))
             else:
                 self.pg.poses_[n] = self.pg.poses_[n - 1]
         patches[:, :, 2] = torch.rand_like(patches[:, :, 2, 0, 0, None, None])
@@ -635,9 +633,13 @@ class DPVO:
         self.pg.n += 1
         self.pg.m += self.M
         # forward then backward edges (dpvo.py:799-800) in one append: the
-        # edge state (net: E x 384 fp32) is reallocated once per frame, not twice
-        (kf, jf), (kb, jb) = self._edges_forw(), self._edges_back()
-        self.append_factors(torch.cat([kf, kb]), torch.cat([jf, jb]))
+        # index lists in one launch (update_ops.append_edges = _edges_forw,
+        # _edges_back and append_factors' concatenations), the edge state
+        # (net: E x 384 fp32) reallocated once per frame, not twice
+        E0 = self.pg.ii.numel()
+        self.pg.ii, self.pg.jj, self.pg.kk = update_ops.append_edges(self.pg.ii, self.pg.jj, self.pg.kk, self.ix,
+                                                                     self.n, self.M, self.cfg.PATCH_LIFETIME)
+        self.pg.net = torch.cat([self.pg.net, self.pg.net.new_zeros(1, self.pg.ii.numel() - E0, self.DIM)], dim=1)
         if self.n == self.warm_up and not self.is_initialized:
             self.is_initialized = True
             for _ in range(12):

@@ -66,6 +66,24 @@ def transform_fused(poses, patches, intrinsics, ii, jj, kk, depth=False, valid=F
     return (out, v) if valid else out
 
 
+def pose_extrapolate(poses_, n, s):
+    """poses_[n] = Exp(s Log(poses_[n-1] poses_[n-2]^-1)) poses_[n-1] in place
+    (the DAMPED_LINEAR motion model, dpvo.py:816-825; poses_ [N, 7] fp32)."""
+    H.on_gpu(poses_)
+    if poses_.dtype != torch.float32 or not poses_.is_contiguous() or poses_.shape[-1] != 7 or n >= poses_.shape[0]:
+        raise RuntimeError("pose_extrapolate: contiguous fp32 [N, 7] poses with n < N required")
+    H.check(H.lib().dpvo_pose_extrapolate(H.ptr(poses_), int(n), float(s), H.stream_of(poses_)))
+
+
+def pose_relative(a, b):
+    """SE3 a * b^-1 for two fp32 [7] pose rows, one launch (dpvo.py:613)."""
+    H.on_gpu(a, b)
+    a, b = a.contiguous().float(), b.contiguous().float()
+    out = torch.empty(7, dtype=torch.float32, device=a.device)
+    H.check(H.lib().dpvo_pose_relative(H.ptr(a), H.ptr(b), H.ptr(out), H.stream_of(a)))
+    return SE3(out)
+
+
 def motion_mag_pair(poses, patches, intrinsics, ii, jj, kk, i, j, beta=0.5):
     """[mean flow_mag over the (i -> j) edges, same for (j -> i)] as a 2-float
     device tensor, one launch and no host sync (dpvo.py:507-514 + :609;

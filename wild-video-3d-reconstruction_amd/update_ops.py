@@ -229,6 +229,24 @@ def window_group_by(ii, jj, kk, M, base, ring, frames, flag=None):
     return (slots[0], slots[1], (gid[0], offs[0], perm[0], groups[0]), (gid[1], offs[1], perm[1], groups[1]))
 
 
+def append_edges(ii, jj, kk, ix, n, M, r):
+    """DPVO.__call__'s edge append (dpvo.py:756-769,799-800) in one launch:
+    -> (ii, jj, kk) int64 = the old edges, then the forward and backward edges
+    of the new frame (n = frame count including it, r = PATCH_LIFETIME)."""
+    H.on_gpu(ii, jj, kk, ix)
+    ii, jj, kk, ix = H.idx64(ii), H.idx64(jj), H.idx64(kk), H.idx64(ix)
+    E = kk.numel()
+    if ii.numel() != E or jj.numel() != E:
+        raise RuntimeError("append_edges: ii, jj and kk must have the same length")
+    add = H.lib().dpvo_append_edges_count(int(n), int(M), int(r))
+    if add < 0:
+        raise RuntimeError("append_edges: n >= 1, M >= 1 and PATCH_LIFETIME >= 1 required")
+    out = torch.empty(3, E + add, dtype=torch.int64, device=kk.device)
+    H.check(H.lib().dpvo_append_edges(H.ptr(ii), H.ptr(jj), H.ptr(kk), E, H.ptr(ix), int(n), int(M), int(r),
+                                      H.ptr(out[0]), H.ptr(out[1]), H.ptr(out[2]), H.stream_of(kk)))
+    return out[0], out[1], out[2]
+
+
 def edge_targets(centre, delta, weight):
     """(centre + delta.float(), weight.float()) for [1, E, 2] views (fp32 centre,
     fp16 delta / weight with unit component stride) in one launch."""
