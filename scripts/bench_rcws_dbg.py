@@ -1,8 +1,6 @@
-"""Timing experiment for rowchain_kernel<RES> (the update operator's c1 / c2
-Linear -> ReLU -> Linear pairs with the residual epilogue, E = 95,424 rows):
-DPVO_RC_DBG drops the row pass (1), the MFMAs (2) or both (3), so the time
-left shows what bounds the kernel.  Run under rocprofv3 --kernel-trace: the
-variants differ in their template arguments."""
+"""Timing experiment for rowchain_ws_kernel<RES> (the c1 / c2 chain at C3 size,
+E = 95,424 rows): DPVO_RCWS_DBG variants (csrc/rowgemm.hip) under rocprofv3
+--kernel-trace; RCWS_VARIANTS picks them (results wrong except 0 and 1)."""
 import os
 import sys
 
@@ -21,8 +19,8 @@ def main():
     res32 = torch.randn(E, D, device="cuda")
     W1, b1 = U.pack_linear(torch.randn(D, D, device="cuda") / 20, torch.randn(D, device="cuda") * 0.1)
     W2, b2 = U.pack_linear(torch.randn(D, D, device="cuda") / 20, torch.randn(D, device="cuda") * 0.1)
-    for d in os.environ.get("RC_VARIANTS", "0,1,2,3").split(","):
-        os.environ["DPVO_RC_DBG"] = d
+    for d in os.environ.get("RCWS_VARIANTS", "0,1,2,4,6,8,14").split(","):
+        os.environ["DPVO_RCWS_DBG"] = d
         for _ in range(10):
             U.rowchain(A, W1, b1, W2, b2, flags1=U.RELU, a_idx=idx, flags=U.RES, res32=res32, want32=True)
         torch.cuda.synchronize()

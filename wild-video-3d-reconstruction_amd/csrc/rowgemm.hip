@@ -338,9 +338,11 @@ __device__ __forceinline__ void epi2_load(const dpvo_rowgemm_args& p, int64_t M,
     }
 }
 
-template <int FLAGS, int R, typename YMap>
-__device__ __forceinline__ void epi2_finish(const dpvo_rowgemm_args& p, int64_t M, const char* smem, YMap ym, int lrow0,
-                                            int64_t row0, int lane, const EpiConsts2& k, const EpiOps2<R>& o)
+// yget(i, j): the fp16 y of row 2 i + h, columns 128 j + 4 s .. + 3 (from the
+// y tile in LDS, or from registers in the warp-specialised chain)
+template <int FLAGS, int R, typename YGet>
+__device__ __forceinline__ void epi2_finish(const dpvo_rowgemm_args& p, int64_t M, YGet yget, int64_t row0, int lane,
+                                            const EpiConsts2& k, const EpiOps2<R>& o)
 {
     const int h = lane >> 5, s = lane & 31;
     ep_f4 v[R / 2][3];
@@ -348,7 +350,7 @@ __device__ __forceinline__ void epi2_finish(const dpvo_rowgemm_args& p, int64_t 
     for (int i = 0; i < R / 2; i++) {
 #pragma unroll
         for (int j = 0; j < 3; j++) {
-            const ep_h4 y = *(const ep_h4*)(smem + ym.off(lrow0 + 2 * i + h, (128 * j + 4 * s) * 2));
+            const ep_h4 y = yget(i, j);
             v[i][j] = ep_f4{(float)y[0], (float)y[1], (float)y[2], (float)y[3]};
         }
     }
@@ -435,7 +437,10 @@ __device__ __forceinline__ void epilogue_rows2(const dpvo_rowgemm_args& p, int64
 {
     EpiOps2<R> o;
     epi2_load<FLAGS, R>(p, M, row0, lane, o);
-    epi2_finish<FLAGS, R>(p, M, smem, ym, lrow0, row0, lane, k, o);
+    const int h = lane >> 5, s = lane & 31;
+    epi2_finish<FLAGS, R>(
+        p, M, [&](int i, int j) { return *(const ep_h4*)(smem + ym.off(lrow0 + 2 * i + h, (128 * j + 4 * s) * 2)); },
+        row0, lane, k, o);
 }
 
 template <int FLAGS>
@@ -1262,6 +1267,282 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
 }
 
 // ---------------------------------------------------------------------------
+// rowchain_ws: the chains whose first GEMM has K1 = 384 (c1 / c2 and the GRU's
+// gated residuals, net.py:80-85, blocks.py:27-30), warp-specialised.
+// rowchain_kernel runs the k-loops (latency / address-path bound) and the row
+// epilogue (HBM bound: the residual in, out32 / out16 out) one after the
+// other in the same waves -- measured on the c1 chain: 80 us of k-loop and
+// 67 us of epilogue, in series -- and its next tile's first stage load waits
+// behind the epilogue's stores (one in-order vmcnt per wave).  Here a
+// 512-thread workgroup (one per CU) has two roles:
+//   G, waves 0-3: the GEMMs of tile t (64 rows x 384; wave w owns columns
+//     96 w .. + 96, acc 4 x 6 MFMA tiles) and every LDS-DMA;
+//   E, waves 4-7: the row epilogue of tile t-1 (16 rows each), whose fp16
+//     y rows they copied from LDS into registers when tile t began.
+// Both roles pass the same barriers; E's loads and stores never enter G's
+// vmcnt.
+// LDS (144 KB): two 48 KB tiles T0 / T1 (YMapG layout: [3 column groups of
+// 256 B][64 rows][256 B], 16-byte chunks XOR (row & 15)) and two 24 KB W
+// stages (all 384 output rows x 32 k of the k-blocked W).  Tile t uses
+// T[t & 1]: its A rows (gathered as whole 128-B lines during tile t-1, one
+// piece per k-step), then GEMM1's activation (GEMM2's A), then GEMM2's
+// output, which E copies out at the start of tile t+1.
+// Per output element the MFMAs, their k order and the epilogue arithmetic are
+// rowchain_kernel's: bit-identical results.
+// GATED: the gate GEMM runs first on A; gate = fp16(sigmoid(fp16(A Wg^T +
+// bg))) waits in G's registers and multiplies GEMM2's fp16 output as
+// rowchain_kernel's gate pass does.
+// ---------------------------------------------------------------------------
+constexpr int WS_BM = 64, WS_THREADS = 512;
+constexpr int WS_T = WS_BM * 768;                  // 48 KB
+constexpr int WS_WST = RG_BN * RC_BK * 2;          // 24 KB
+constexpr int WS_LDS = 2 * WS_T + 2 * WS_WST;      // 144 KB
+
+struct YMapG {   // [byte / 256][64 rows][256 B], 16-byte chunks XOR (row & 15): conflict-free
+    // fragment reads down 16 rows, C-layout writes and 256-byte row sweeps
+    __device__ int off(int r, int byte) const
+    {
+        return (byte >> 8) * (WS_BM * 256) + r * 256 + ((((byte >> 4) & 15) ^ (r & 15)) << 4) + (byte & 15);
+    }
+};
+
+// DBG (timing experiments, DPVO_RCWS_DBG, flag RES; results wrong except 1):
+// 1 the next tile's A rows in one burst at step 1, 2 no A loads after the
+// first tile, 4 no W stream, 8 no E work
+template <int F2, bool GATED, int DBG = 0>
+__global__ __launch_bounds__(WS_THREADS, 1) void rowchain_ws_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
+                                                                    dpvo_rowgemm_args pg)
+{
+    __shared__ __attribute__((aligned(16))) char smem[WS_LDS];
+    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t Mrows = p1.M_dev ? min(*p1.M_dev, p1.M) : p1.M;
+    const int64_t ntiles = (Mrows + WS_BM - 1) / WS_BM;
+    if ((int64_t)blockIdx.x >= ntiles) return;
+    const int nmine = (int)((ntiles - 1 - blockIdx.x) / gridDim.x + 1);
+    const YMapG ym;
+    // the tile's GEMM k-steps (12 per GEMM) and the steps ending a GEMM whose
+    // output goes to T (an extra barrier after each)
+    constexpr int NS = GATED ? 36 : 24;
+    constexpr int G1END = GATED ? 23 : 11;
+    auto bar = []() {
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    if (wave < 4) {
+        // =========================== G role ===========================
+        const int wn = wave;
+        const int fr = lane & 15, fq = lane >> 4;
+        const half_t* __restrict__ zero = (const half_t*)p1.zero_row;
+        const half_t* W1 = (const half_t*)p1.W;
+        const half_t* W2 = (const half_t*)p.W;
+        const half_t* Wg = (const half_t*)pg.W;
+        // W stage pieces 6 wave .. 6 wave + 5 of 24 (16 rows x 64 B each)
+        int wsrc[6];
+        {
+            const int srow = lane >> 2, pch = lane & 3;
+#pragma unroll
+            for (int j = 0; j < 6; j++) {
+                const int n = (6 * wave + j) * 16 + srow;
+                wsrc[j] = n * RC_BK + 8 * (pch ^ ((n >> 2) & 3));
+            }
+        }
+        // the W of step s (0 .. NS-1) of a tile: gate (GATED), W1, W2
+        auto wmat = [&](int s) {
+            const int g = s / 12;
+            if (GATED) return g == 0 ? Wg : (g == 1 ? W1 : W2);
+            return g == 0 ? W1 : W2;
+        };
+        auto issue_w = [&](int s, int buf) {
+            const half_t* base = wmat(s) + (int64_t)(s % 12) * (RG_BN * RC_BK);
+            char* st = smem + 2 * WS_T + buf * WS_WST;
+#pragma unroll
+            for (int j = 0; j < 6; j++) glds16(base + wsrc[j], st + (6 * wave + j) * 1024);
+        };
+        // A rows of a tile into T[b]: piece (g, k) = rows 4 wave + 16 k .. + 3 of
+        // column group g; lane L: row 4 wave + 16 k + L / 16, chunk L % 16
+        int64_t arow[4];   // element offsets of this lane's four A rows (-1: zero row)
+        auto load_rows = [&](int64_t tile) {
+            const int r0 = 4 * wave + (lane >> 4);
+            int64_t sidx[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int64_t m = tile * WS_BM + r0 + 16 * k;
+                sidx[k] = m < Mrows ? m : Mrows - 1;
+            }
+            if (p1.a_idx) {   // all four loads before any use
+#pragma unroll
+                for (int k = 0; k < 4; k++) sidx[k] = p1.a_idx[sidx[k]];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const bool ok = tile * WS_BM + r0 + 16 * k < Mrows && sidx[k] >= 0 && sidx[k] < p1.a_rows;
+                arow[k] = ok ? sidx[k] * p1.lda : -1;
+            }
+        };
+        auto issue_a = [&](int q, int b) {   // piece q = 4 g + k of this wave
+            const int g = q >> 2, k = q & 3;
+            const int r = 4 * wave + 16 * k + (lane >> 4);
+            const half_t* row = arow[k] >= 0 ? (const half_t*)p1.A + arow[k] : zero;
+            glds16(row + 128 * g + 8 * ((lane & 15) ^ (r & 15)), smem + b * WS_T + g * (WS_BM * 256) + (r - (lane >> 4)) * 256);
+        };
+        int w_off[6];
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) {
+            const int n = wn * 96 + nt * 16 + fr;
+            w_off[nt] = n * 64 + 16 * (fq ^ ((n >> 2) & 3));
+        }
+        f4_t acc[4][6];
+        h4_t gsv[4][6];
+        auto zero_acc = [&]() {
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                for (int nt = 0; nt < 6; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+        };
+        // acc + bias -> act -> fp16 (-> x gate) -> T[b]
+        auto acc_to_t = [&](int b, const half_t* bias_p, bool relu, bool sigm, bool gated) {
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) {
+                const int col = wn * 96 + nt * 16 + 4 * fq;
+                const h4_t bias = *(const h4_t*)(bias_p + col);
+#pragma unroll
+                for (int mt = 0; mt < 4; mt++) {
+                    h4_t y;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        half_t v = (half_t)(acc[mt][nt][r] + (float)bias[r]);
+                        if (relu) v = v > (half_t)0 ? v : (half_t)0;
+                        if (sigm) v = (half_t)fast_sigmoid((float)v);
+                        if (GATED && gated) v = (half_t)((float)gsv[mt][nt][r] * (float)v);
+                        y[r] = v;
+                    }
+                    *(h4_t*)(smem + b * WS_T + ym.off(mt * 16 + fr, col * 2)) = y;
+                }
+            }
+        };
+
+        // prologue: the first tile's A rows and W stage 0
+        load_rows(blockIdx.x);
+#pragma unroll
+        for (int q = 0; q < 12; q++) issue_a(q, 0);
+        issue_w(0, 0);
+        for (int it = 0; it < nmine; it++) {
+            const int64_t tile = blockIdx.x + (int64_t)it * gridDim.x;
+            const bool next = it + 1 < nmine;
+            const int cur = it & 1;
+            const char* T = smem + cur * WS_T;
+            if (next) load_rows(tile + gridDim.x);   // (plain loads: waited for here, before this tile's DMA)
+            zero_acc();
+#pragma unroll 1
+            for (int s = 0; s < NS; s++) {
+                // W stage s+1 (the next tile's stage 0 after the last step), then
+                // one piece of the next tile's A rows on steps 1 .. 12 (T[cur ^ 1]
+                // was copied out by E before step 0's first barrier)
+                const bool wnext = s + 1 < NS || next;
+                if (wnext && !(DBG & 4)) issue_w((s + 1) % NS, (s + 1) & 1);
+                const bool apiece = next && s >= 1 && s <= 12 && !(DBG & 3);
+                if (apiece) issue_a(s - 1, cur ^ 1);
+                if ((DBG & 1) && next && s == 1)
+#pragma unroll
+                    for (int q = 0; q < 12; q++) issue_a(q, cur ^ 1);
+                // wait for stage s (and everything older): the newest 6 (+1) may fly
+                if (apiece) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+                else if (wnext) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                bar();
+                const char* st = smem + 2 * WS_T + (s & 1) * WS_WST;
+                const int ks = s % 12;
+                h8_t a[4], b[6];
+#pragma unroll
+                for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(T + ym.off(mt * 16 + fr, (ks * 4 + fq) * 16));
+#pragma unroll
+                for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+#pragma unroll
+                for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                    for (int nt = 0; nt < 6; nt++)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                bar();
+                if (GATED && s == 11) {   // gate -> registers
+#pragma unroll
+                    for (int nt = 0; nt < 6; nt++) {
+                        const h4_t bias = *(const h4_t*)((const half_t*)pg.bias + wn * 96 + nt * 16 + 4 * fq);
+#pragma unroll
+                        for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+                            for (int r = 0; r < 4; r++)
+                                gsv[mt][nt][r] = (half_t)fast_sigmoid((float)(half_t)(acc[mt][nt][r] + (float)bias[r]));
+                    }
+                    zero_acc();
+                } else if (s == G1END) {   // GEMM1's activation -> T (A no longer read)
+                    acc_to_t(cur, (const half_t*)p1.bias, p1.flags & RG_RELU, p1.flags & RG_SIGMOID, false);
+                    zero_acc();
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    bar();
+                } else if (s == NS - 1) {  // GEMM2's output (x gate) -> T for E
+                    acc_to_t(cur, (const half_t*)p.bias, F2 & RG_RELU, F2 & RG_SIGMOID, true);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    bar();
+                }
+            }
+        }
+    } else {
+        // =========================== E role ===========================
+        const int e = wave - 4;   // rows 16 e .. 16 e + 15 of a tile
+        const int hh = lane >> 5, sl = lane & 31;
+        ep_h4 yr[8][3];   // pair i: row 16 e + 2 i + hh, columns 128 j + 4 sl ..
+        auto copy_y = [&](int b) {
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+#pragma unroll
+                for (int j = 0; j < 3; j++)
+                    yr[i][j] = *(const ep_h4*)(smem + b * WS_T + ym.off(16 * e + 2 * i + hh, (128 * j + 4 * sl) * 2));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        };
+        EpiConsts2 kc;
+        load_consts2<F2>(p, lane, kc);
+        int64_t prow0 = -1;   // first row of the tile whose y is in yr (-1: none)
+        EpiOps2<2> ops;
+        // pair i of the held tile: loads on one step, the rest on the next
+        auto pair_load = [&](int i) { epi2_load<F2, 2>(p, Mrows, prow0 + 16 * e + 2 * i, lane, ops); };
+        auto pair_finish = [&](int i) {
+            epi2_finish<F2, 2>(
+                p, Mrows, [&](int, int j) { return yr[i][j]; }, prow0 + 16 * e + 2 * i, lane, kc, ops);
+        };
+        constexpr int PER = NS / 12;   // steps per pair: 8 pairs over NS - 4 steps (2 or 3)
+        for (int it = 0; it < nmine; it++) {
+            const int64_t tile = blockIdx.x + (int64_t)it * gridDim.x;
+#pragma unroll 1
+            for (int s = 0; s < NS; s++) {
+                bar();
+                if (prow0 >= 0 && !(DBG & 8)) {
+                    // pair i's loads at step PER i, its LN / stores at step PER i + 1
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        if (s == PER * i + 1) pair_finish(i);
+                        if (s == PER * i) pair_load(i);
+                    }
+                }
+                bar();
+                if (s == G1END || s == NS - 1) bar();
+            }
+            // tile t's y is in T[it & 1]: hold it (every pair of t-1 is stored)
+            copy_y(it & 1);
+            prow0 = tile * WS_BM;
+        }
+        // the last tile's rows (no more barriers: G has finished)
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            pair_load(i);
+            pair_finish(i);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // v4: one GEMM, or two chained (CHAIN), per 128-row tile, with the operand
 // streams decoupled from the MFMA waves.  v1-v3 stage W through LDS next to A
 // and synchronise all eight waves twice per k-step: every k-step then pays one
@@ -1877,6 +2158,63 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
             RC4_CASE(DPVO_RG_GATE | DPVO_RG_LN)
             RC4_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
 #undef RC4_CASE
+        default:
+            set_error("dpvo_rowchain: unsupported epilogue flag combination " + std::to_string(f));
+            return -1;
+        }
+        DPVO_CHECK_LAUNCH();
+        return 0;
+    }
+    static const bool ws = [] {
+        // 1: the warp-specialised 64-row chains (measured slower at C3 so far:
+        // profiles/r3/NOTES.md); default: the one-role 128-row chain kernel
+        const char* v = getenv("DPVO_RCWS");
+        return v && atoi(v) == 1;
+    }();
+    if (const char* d = getenv("DPVO_RCWS_DBG"); ws && g1->K == RG_BN && d && f == DPVO_RG_RES && !gate) {
+        warn_debug_knob("DPVO_RCWS_DBG");
+        const unsigned gws = (unsigned)std::min<int64_t>((g1->M + WS_BM - 1) / WS_BM, g_num_cus);
+        switch (atoi(d)) {
+#define RCWSD_CASE(D)                                                                                       \
+    case (D):                                                                                               \
+        hipLaunchKernelGGL((rowchain_ws_kernel<DPVO_RG_RES, false, (D)>), dim3(gws), dim3(WS_THREADS), 0,   \
+                           as_stream(stream), *g1, a2, a2);                                                 \
+        break;
+            RCWSD_CASE(0) RCWSD_CASE(1) RCWSD_CASE(2) RCWSD_CASE(4) RCWSD_CASE(6) RCWSD_CASE(8) RCWSD_CASE(14)
+#undef RCWSD_CASE
+        default:
+            set_error("DPVO_RCWS_DBG: unsupported value");
+            return -1;
+        }
+        DPVO_CHECK_LAUNCH();
+        return 0;
+    }
+    if (ws && g1->K == RG_BN) {
+        const int64_t ntw = (g1->M + WS_BM - 1) / WS_BM;
+        const unsigned gws = (unsigned)std::min<int64_t>(ntw, g_num_cus);
+        if (gate) {
+            a2.gate16 = nullptr;
+            a2.res16 = nullptr;
+        }
+        switch (f | (gate ? 1024 : 0)) {
+#define RCWS_CASE(F)                                                                                              \
+    case (F):                                                                                                     \
+        hipLaunchKernelGGL((rowchain_ws_kernel<(F), false>), dim3(gws), dim3(WS_THREADS), 0, as_stream(stream), *g1, \
+                           a2, a2);                                                                                \
+        break;
+#define RCWSG_CASE(F)                                                                                              \
+    case ((F) | 1024):                                                                                             \
+        hipLaunchKernelGGL((rowchain_ws_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES, true>), dim3(gws),             \
+                           dim3(WS_THREADS), 0, as_stream(stream), *g1, a2, *gate);                                \
+        break;
+            RCWS_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
+            RCWS_CASE(DPVO_RG_RES)
+            RCWS_CASE(DPVO_RG_GATE | DPVO_RG_LN)
+            RCWS_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
+            RCWSG_CASE(DPVO_RG_GATE | DPVO_RG_LN)
+            RCWSG_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
+#undef RCWS_CASE
+#undef RCWSG_CASE
         default:
             set_error("dpvo_rowchain: unsupported epilogue flag combination " + std::to_string(f));
             return -1;
