@@ -1296,7 +1296,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
 constexpr int WS_BM = 64, WS_THREADS = 512;
 constexpr int WS_T = WS_BM * 768;                  // 48 KB
 constexpr int WS_WST = RG_BN * RC_BK * 2;          // 24 KB
-constexpr int WS_LDS = 2 * WS_T + 2 * WS_WST;      // 144 KB
+constexpr int WS_LDS = 2 * WS_T + 2 * WS_WST + 64; // 144 KB + the sync counters
 
 struct YMapG {   // [byte / 256][64 rows][256 B], 16-byte chunks XOR (row & 15): conflict-free
     // fragment reads down 16 rows, C-layout writes and 256-byte row sweeps
@@ -1306,9 +1306,8 @@ struct YMapG {   // [byte / 256][64 rows][256 B], 16-byte chunks XOR (row & 15):
     }
 };
 
-// DBG (timing experiments, DPVO_RCWS_DBG, flag RES; results wrong except 1):
-// 1 the next tile's A rows in one burst at step 1, 2 no A loads after the
-// first tile, 4 no W stream, 8 no E work
+// DBG (timing experiments, DPVO_RCWS_DBG, flag RES; results wrong): 2 no A loads
+// after the first tile, 4 no W stream, 8 no E work
 template <int F2, bool GATED, int DBG = 0>
 __global__ __launch_bounds__(WS_THREADS, 1) void rowchain_ws_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
                                                                     dpvo_rowgemm_args pg)
@@ -1321,12 +1320,45 @@ __global__ __launch_bounds__(WS_THREADS, 1) void rowchain_ws_kernel(dpvo_rowgemm
     if ((int64_t)blockIdx.x >= ntiles) return;
     const int nmine = (int)((ntiles - 1 - blockIdx.x) / gridDim.x + 1);
     const YMapG ym;
-    // the tile's GEMM k-steps (12 per GEMM) and the steps ending a GEMM whose
-    // output goes to T (an extra barrier after each)
+    // the tile's GEMM k-steps (12 per GEMM); GEMM1 ends at G1END
     constexpr int NS = GATED ? 36 : 24;
     constexpr int G1END = GATED ? 23 : 11;
-    auto bar = []() {
-        __builtin_amdgcn_s_barrier();
+    // ---- synchronisation: counters in LDS, no workgroup barrier after the
+    // first (a barrier would tie the roles' paces together).  Every counter
+    // only grows; a waiter spins (s_sleep) until it reaches its target.
+    //   ctr[0]  G step counter: a G wave adds 1 when its pieces of the current
+    //           W stage have landed and its reads of the previous stage are done
+    //   ctr[1]  y ready: a G wave adds 1 after writing its part of a tile's y
+    //   ctr[2]  T free: an E wave adds 1 after copying its rows of a tile's y
+    //   ctr[3]  abort: a spin that timed out (the kernel then drains and exits;
+    //           results are wrong but no wave hangs)
+    // (the counter accesses are inline asm with their own lgkmcnt waits: as
+    // atomics the compiler would add vmcnt(0) waits, draining the LDS-DMA that
+    // is meant to stay in flight)
+    const unsigned cbase = (unsigned)(uintptr_t)(smem + WS_LDS - 64);
+    if (tid < 4) ((int*)(smem + WS_LDS - 64))[tid] = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    auto add = [&](int i) {
+        // this wave's LDS writes (and reads) first; one lane adds
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) asm volatile("ds_add_u32 %0, %1" ::"v"(cbase + 4 * i), "v"(1) : "memory");
+    };
+    auto ld = [&](int i) {
+        int v;
+        asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(cbase + 4 * i) : "memory");
+        return __builtin_amdgcn_readfirstlane(v);
+    };
+    auto wait = [&](int i, int target) {
+        for (int n = 0;; n++) {
+            if (ld(i) >= target || ld(3)) break;
+            if (n > (1 << 22)) {   // ~0.2 s: give up (wrong results, no hang)
+                add(3);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
         asm volatile("" ::: "memory");
     };
 
@@ -1338,16 +1370,12 @@ __global__ __launch_bounds__(WS_THREADS, 1) void rowchain_ws_kernel(dpvo_rowgemm
         const half_t* W1 = (const half_t*)p1.W;
         const half_t* W2 = (const half_t*)p.W;
         const half_t* Wg = (const half_t*)pg.W;
-        // W stage pieces 6 wave .. 6 wave + 5 of 24 (16 rows x 64 B each)
-        int wsrc[6];
-        {
-            const int srow = lane >> 2, pch = lane & 3;
-#pragma unroll
-            for (int j = 0; j < 6; j++) {
-                const int n = (6 * wave + j) * 16 + srow;
-                wsrc[j] = n * RC_BK + 8 * (pch ^ ((n >> 2) & 3));
-            }
-        }
+        // W stage pieces 6 wave .. 6 wave + 5 of 24 (16 rows x 64 B each); the
+        // swizzle ((n >> 2) & 3) does not depend on the piece: one base offset
+        const int wsrc0 = [&] {
+            const int srow = lane >> 2, pch = lane & 3, n = 96 * wave + srow;
+            return n * RC_BK + 8 * (pch ^ ((n >> 2) & 3));
+        }();
         // the W of step s (0 .. NS-1) of a tile: gate (GATED), W1, W2
         auto wmat = [&](int s) {
             const int g = s / 12;
@@ -1355,10 +1383,11 @@ __global__ __launch_bounds__(WS_THREADS, 1) void rowchain_ws_kernel(dpvo_rowgemm
             return g == 0 ? W1 : W2;
         };
         auto issue_w = [&](int s, int buf) {
+            if (DBG & 4) return;
             const half_t* base = wmat(s) + (int64_t)(s % 12) * (RG_BN * RC_BK);
             char* st = smem + 2 * WS_T + buf * WS_WST;
 #pragma unroll
-            for (int j = 0; j < 6; j++) glds16(base + wsrc[j], st + (6 * wave + j) * 1024);
+            for (int j = 0; j < 6; j++) glds16(base + wsrc0 + 512 * j, st + (6 * wave + j) * 1024);
         };
         // A rows of a tile into T[b]: piece (g, k) = rows 4 wave + 16 k .. + 3 of
         // column group g; lane L: row 4 wave + 16 k + L / 16, chunk L % 16
@@ -1385,14 +1414,12 @@ __global__ __launch_bounds__(WS_THREADS, 1) void rowchain_ws_kernel(dpvo_rowgemm
             const int g = q >> 2, k = q & 3;
             const int r = 4 * wave + 16 * k + (lane >> 4);
             const half_t* row = arow[k] >= 0 ? (const half_t*)p1.A + arow[k] : zero;
-            glds16(row + 128 * g + 8 * ((lane & 15) ^ (r & 15)), smem + b * WS_T + g * (WS_BM * 256) + (r - (lane >> 4)) * 256);
+            glds16(row + 128 * g + 8 * ((lane & 15) ^ (r & 15)),
+                   smem + b * WS_T + g * (WS_BM * 256) + (r - (lane >> 4)) * 256);
         };
-        int w_off[6];
-#pragma unroll
-        for (int nt = 0; nt < 6; nt++) {
-            const int n = wn * 96 + nt * 16 + fr;
-            w_off[nt] = n * 64 + 16 * (fq ^ ((n >> 2) & 3));
-        }
+        // W fragment nt of this wave: row n = 96 wn + 16 nt + fr (the swizzle
+        // ((n >> 2) & 3) is fr's)
+        const int w_off0 = (wn * 96 + fr) * 64 + 16 * (fq ^ ((fr >> 2) & 3));
         f4_t acc[4][6];
         h4_t gsv[4][6];
         auto zero_acc = [&]() {
@@ -1422,50 +1449,80 @@ __global__ __launch_bounds__(WS_THREADS, 1) void rowchain_ws_kernel(dpvo_rowgemm
                 }
             }
         };
+        int gsync = 0;   // G-sync rounds passed
+        auto gbar = [&]() {
+            add(0);
+            wait(0, 4 * ++gsync);
+        };
 
-        // prologue: the first tile's A rows and W stage 0
+        // Software-pipelined k-loop (one G wave per SIMD: nothing else hides
+        // the LDS reads): step g starts with stage g's fragments in registers
+        // and stage g+1's DMA in flight; it waits for that DMA, syncs the G
+        // waves once (stage g+1 landed everywhere, stage g read everywhere),
+        // issues stage g+2's DMA into stage g's buffer, and reads stage g+1's
+        // fragments between its MFMAs (each W fragment right after the four
+        // MFMAs that used it).  Tiles chain: the flat step sequence runs over
+        // this workgroup's tiles.
+        h8_t acur[4], anxt[4], b[6];
+        auto read_a = [&](const char* Tb, int ks, h8_t (&a)[4]) {
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(Tb + ym.off(mt * 16 + fr, (ks * 4 + fq) * 16));
+        };
+        auto read_b = [&](int buf, int nt) { return *(const h8_t*)(smem + 2 * WS_T + buf * WS_WST + w_off0 + 1024 * nt); };
         load_rows(blockIdx.x);
 #pragma unroll
         for (int q = 0; q < 12; q++) issue_a(q, 0);
         issue_w(0, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        gbar();
+        issue_w(1 % NS, 1);   // (NS > 1)
+        read_a(smem, 0, acur);
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) b[nt] = read_b(0, nt);
         for (int it = 0; it < nmine; it++) {
             const int64_t tile = blockIdx.x + (int64_t)it * gridDim.x;
             const bool next = it + 1 < nmine;
             const int cur = it & 1;
             const char* T = smem + cur * WS_T;
-            if (next) load_rows(tile + gridDim.x);   // (plain loads: waited for here, before this tile's DMA)
+            if (next) load_rows(tile + gridDim.x);   // (plain loads: waited for at their first use)
             zero_acc();
 #pragma unroll 1
             for (int s = 0; s < NS; s++) {
-                // W stage s+1 (the next tile's stage 0 after the last step), then
-                // one piece of the next tile's A rows on steps 1 .. 12 (T[cur ^ 1]
-                // was copied out by E before step 0's first barrier)
-                const bool wnext = s + 1 < NS || next;
-                if (wnext && !(DBG & 4)) issue_w((s + 1) % NS, (s + 1) & 1);
-                const bool apiece = next && s >= 1 && s <= 12 && !(DBG & 3);
-                if (apiece) issue_a(s - 1, cur ^ 1);
-                if ((DBG & 1) && next && s == 1)
+                const bool more = s + 1 < NS || next;   // a stage g+1 exists
+                // stage g's fragments in registers before the sync (the uses tell
+                // the compiler, which then adds no wait covering later reads)
 #pragma unroll
-                    for (int q = 0; q < 12; q++) issue_a(q, cur ^ 1);
-                // wait for stage s (and everything older): the newest 6 (+1) may fly
-                if (apiece) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-                else if (wnext) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                bar();
-                const char* st = smem + 2 * WS_T + (s & 1) * WS_WST;
-                const int ks = s % 12;
-                h8_t a[4], b[6];
+                for (int nt = 0; nt < 6; nt++) asm volatile("" ::"v"(b[nt]));
 #pragma unroll
-                for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(T + ym.off(mt * 16 + fr, (ks * 4 + fq) * 16));
+                for (int mt = 0; mt < 4; mt++) asm volatile("" ::"v"(acur[mt]));
+                if (more) {
+                    // stage g+1 landed (the newest A piece of the previous step may fly)
+                    const bool aprev = next && s >= 2 && s <= 13 && !(DBG & 2);
+                    if (aprev) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    gbar();
+                    // stage g+2 into stage g's buffer; one piece of the next tile's
+                    // A rows on steps 1 .. 12 (into T[cur ^ 1], which E has copied
+                    // tile it-1's y out of)
+                    if (s + 2 < NS || next) issue_w((s + 2) % NS, s & 1);
+                    if (next && s >= 1 && s <= 12 && !(DBG & 2)) {
+                        if (s == 1) wait(2, 4 * it);
+                        issue_a(s - 1, cur ^ 1);
+                    }
+                }
+                // stage g+1's fragments (read unconditionally: past the last stage,
+                // or at the GEMM1 -> GEMM2 boundary where GEMM1's output is not in
+                // T yet, they are harmless in-range reads, replaced below)
+                read_a(s + 1 < NS ? T : smem + (cur ^ 1) * WS_T, (s + 1) % 12, anxt);
 #pragma unroll
-                for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+                for (int nt = 0; nt < 6; nt++) {
 #pragma unroll
-                for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-                    for (int nt = 0; nt < 6; nt++)
-                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                bar();
+                    for (int mt = 0; mt < 4; mt++)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[nt], acur[mt], acc[mt][nt], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                    b[nt] = read_b((s + 1) & 1, nt);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
                 if (GATED && s == 11) {   // gate -> registers
 #pragma unroll
                     for (int nt = 0; nt < 6; nt++) {
@@ -1477,16 +1534,19 @@ __global__ __launch_bounds__(WS_THREADS, 1) void rowchain_ws_kernel(dpvo_rowgemm
                                 gsv[mt][nt][r] = (half_t)fast_sigmoid((float)(half_t)(acc[mt][nt][r] + (float)bias[r]));
                     }
                     zero_acc();
-                } else if (s == G1END) {   // GEMM1's activation -> T (A no longer read)
+                } else if (s == G1END) {   // GEMM1's activation -> T once every G wave is done reading A
+                    gbar();
                     acc_to_t(cur, (const half_t*)p1.bias, p1.flags & RG_RELU, p1.flags & RG_SIGMOID, false);
                     zero_acc();
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    bar();
-                } else if (s == NS - 1) {  // GEMM2's output (x gate) -> T for E
+                    gbar();
+                    read_a(T, 0, anxt);
+                } else if (s == NS - 1) {  // GEMM2's output (x gate) -> T, then E may take it
+                    gbar();
                     acc_to_t(cur, (const half_t*)p.bias, F2 & RG_RELU, F2 & RG_SIGMOID, true);
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                    bar();
+                    add(1);
                 }
+#pragma unroll
+                for (int mt = 0; mt < 4; mt++) acur[mt] = anxt[mt];
             }
         }
     } else {
@@ -1494,50 +1554,27 @@ __global__ __launch_bounds__(WS_THREADS, 1) void rowchain_ws_kernel(dpvo_rowgemm
         const int e = wave - 4;   // rows 16 e .. 16 e + 15 of a tile
         const int hh = lane >> 5, sl = lane & 31;
         ep_h4 yr[8][3];   // pair i: row 16 e + 2 i + hh, columns 128 j + 4 sl ..
-        auto copy_y = [&](int b) {
+        EpiConsts2 kc;
+        load_consts2<F2>(p, lane, kc);
+        for (int it = 0; it < nmine; it++) {
+            const int64_t row0 = (blockIdx.x + (int64_t)it * gridDim.x) * WS_BM + 16 * e;
+            wait(1, 4 * (it + 1));   // tile it's y is in T[it & 1]
 #pragma unroll
             for (int i = 0; i < 8; i++)
 #pragma unroll
                 for (int j = 0; j < 3; j++)
-                    yr[i][j] = *(const ep_h4*)(smem + b * WS_T + ym.off(16 * e + 2 * i + hh, (128 * j + 4 * sl) * 2));
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        };
-        EpiConsts2 kc;
-        load_consts2<F2>(p, lane, kc);
-        int64_t prow0 = -1;   // first row of the tile whose y is in yr (-1: none)
-        EpiOps2<2> ops;
-        // pair i of the held tile: loads on one step, the rest on the next
-        auto pair_load = [&](int i) { epi2_load<F2, 2>(p, Mrows, prow0 + 16 * e + 2 * i, lane, ops); };
-        auto pair_finish = [&](int i) {
-            epi2_finish<F2, 2>(
-                p, Mrows, [&](int, int j) { return yr[i][j]; }, prow0 + 16 * e + 2 * i, lane, kc, ops);
-        };
-        constexpr int PER = NS / 12;   // steps per pair: 8 pairs over NS - 4 steps (2 or 3)
-        for (int it = 0; it < nmine; it++) {
-            const int64_t tile = blockIdx.x + (int64_t)it * gridDim.x;
-#pragma unroll 1
-            for (int s = 0; s < NS; s++) {
-                bar();
-                if (prow0 >= 0 && !(DBG & 8)) {
-                    // pair i's loads at step PER i, its LN / stores at step PER i + 1
+                    yr[i][j] = *(const ep_h4*)(smem + (it & 1) * WS_T + ym.off(16 * e + 2 * i + hh, (128 * j + 4 * sl) * 2));
+            add(2);   // (add waits for the reads)
+            if (DBG & 8) continue;
+            // the rows: pair i + 1's loads in flight while pair i finishes
+            EpiOps2<2> ops[2];
+            epi2_load<F2, 2>(p, Mrows, row0, lane, ops[0]);
 #pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        if (s == PER * i + 1) pair_finish(i);
-                        if (s == PER * i) pair_load(i);
-                    }
-                }
-                bar();
-                if (s == G1END || s == NS - 1) bar();
+            for (int i = 0; i < 8; i++) {
+                if (i + 1 < 8) epi2_load<F2, 2>(p, Mrows, row0 + 2 * (i + 1), lane, ops[(i + 1) & 1]);
+                epi2_finish<F2, 2>(
+                    p, Mrows, [&](int, int j) { return yr[i][j]; }, row0 + 2 * i, lane, kc, ops[i & 1]);
             }
-            // tile t's y is in T[it & 1]: hold it (every pair of t-1 is stored)
-            copy_y(it & 1);
-            prow0 = tile * WS_BM;
-        }
-        // the last tile's rows (no more barriers: G has finished)
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            pair_load(i);
-            pair_finish(i);
         }
     }
 }
@@ -2180,7 +2217,7 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
         hipLaunchKernelGGL((rowchain_ws_kernel<DPVO_RG_RES, false, (D)>), dim3(gws), dim3(WS_THREADS), 0,   \
                            as_stream(stream), *g1, a2, a2);                                                 \
         break;
-            RCWSD_CASE(0) RCWSD_CASE(1) RCWSD_CASE(2) RCWSD_CASE(4) RCWSD_CASE(6) RCWSD_CASE(8) RCWSD_CASE(14)
+            RCWSD_CASE(0) RCWSD_CASE(2) RCWSD_CASE(4) RCWSD_CASE(6) RCWSD_CASE(8) RCWSD_CASE(14)
 #undef RCWSD_CASE
         default:
             set_error("DPVO_RCWS_DBG: unsupported value");
