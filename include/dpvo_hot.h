@@ -446,6 +446,7 @@ typedef struct dpvo_rowadd_args {
     const void* b16; const int64_t* b_idx; int64_t b_rows;
     const float* ln_g; const float* ln_b; float ln_eps;
     void* out32; void* out16;
+    const void* c16; const int64_t* c_idx; int64_t c_rows;   /* optional second gathered addend */
 } dpvo_rowadd_args;
 int dpvo_rowadd_ln(const dpvo_rowadd_args* args, void* stream);
 

@@ -161,6 +161,15 @@ def test_rowadd_ln():
     want = torch.nn.functional.layer_norm(a16.float() + add, (D,), g, be, 1e-3)
     torch.testing.assert_close(o32, want, rtol=1e-4, atol=1e-4)
     assert U.rowadd_ln(a[:0], hk, jx[:0])[0].shape == (0, D)
+    # a second gathered addend: bit-identical to two calls (the update
+    # operator's net + agg_kk + agg_ij without the fp32 rows in between)
+    h2 = torch.randn(300, D, device="cuda").half()
+    ix2 = torch.randint(-1, 301, (M,), device="cuda")
+    s32, s16 = U.rowadd_ln(a, hk, jx, want16=False)[0], U.rowadd_ln(a, hk, jx, want32=False)[1]
+    r32, r16 = U.rowadd_ln(s32, h2, ix2, ln=(g, be, 1e-3))
+    c32, c16 = U.rowadd_ln(a, hk, jx, ln=(g, be, 1e-3), c16=h2, c_idx=ix2)
+    assert torch.equal(c32, r32) and torch.equal(c16, r16)
+    assert torch.equal(s16, U.rowadd_ln(a, hk, jx)[1])
 
 
 def test_errors():

@@ -1886,9 +1886,14 @@ __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
          row += ((int64_t)gridDim.x * blockDim.x) >> 5) {
         float v[12];
         const half_t* b = nullptr;
+        const half_t* c2 = nullptr;
         if (p.b16) {
             const int64_t s = p.b_idx ? p.b_idx[row] : row;
             if (s >= 0 && s < p.b_rows) b = (const half_t*)p.b16 + s * RG_BN;
+        }
+        if (p.c16) {
+            const int64_t s = p.c_idx ? p.c_idx[row] : row;
+            if (s >= 0 && s < p.c_rows) c2 = (const half_t*)p.c16 + s * RG_BN;
         }
 #pragma unroll
         for (int j = 0; j < 3; j++) {
@@ -1907,6 +1912,14 @@ __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
 #pragma unroll
             for (int j = 0; j < 3; j++) {
                 const rl_h4 h = *(const rl_h4*)(b + 128 * j + 4 * sub);
+#pragma unroll
+                for (int t = 0; t < 4; t++) v[4 * j + t] += (float)h[t];
+            }
+        }
+        if (c2) {   // ((a + b) + c: the two row adds of consecutive rowadd_ln calls, in order)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const rl_h4 h = *(const rl_h4*)(c2 + 128 * j + 4 * sub);
 #pragma unroll
                 for (int t = 0; t < 4; t++) v[4 * j + t] += (float)h[t];
             }
@@ -2376,6 +2389,8 @@ extern "C" int dpvo_rowadd_ln(const dpvo_rowadd_args* a, void* stream)
     DPVO_CHECK_ARG(a->lda >= RG_BN && a->lda % 4 == 0, "rowadd_ln: lda must be a multiple of 4 and >= 384");
     DPVO_CHECK_ARG((uintptr_t)a->a % (a->a_f16 ? 8 : 16) == 0, "rowadd_ln: input rows must be vector aligned");
     DPVO_CHECK_ARG(!a->b16 || (uintptr_t)a->b16 % 8 == 0, "rowadd_ln: b16 must be 8-byte aligned");
+    DPVO_CHECK_ARG(!a->c16 || (uintptr_t)a->c16 % 8 == 0, "rowadd_ln: c16 must be 8-byte aligned");
+    DPVO_CHECK_ARG(!a->c16 || a->b16, "rowadd_ln: c16 needs b16 (the second addend follows the first)");
     DPVO_CHECK_ARG(!a->ln_g || ((uintptr_t)a->ln_g % 16 == 0 && (uintptr_t)a->ln_b % 16 == 0),
                    "rowadd_ln: LayerNorm parameters must be 16-byte aligned");
     DPVO_CHECK_ARG((!a->out32 || (uintptr_t)a->out32 % 16 == 0) && (!a->out16 || (uintptr_t)a->out16 % 8 == 0),

@@ -120,6 +120,7 @@ class Update(nn.Module):
         for (la, lb), nb in ((pk["c1"], ix), (pk["c2"], jx)):
             n32, n16, _ = U.rowchain(n16, *la, *lb, flags1=U.RELU, a_idx=nb, flags=U.RES, res32=n32, want32=True)
         ln0, gr1, ln1, gr2 = pk["gru"]
+        kk_add = None
         for (pf, pg_, ph), key, ln in ((pk["agg_kk"], None, None), (pk["agg_ij"], ii * 12345 + jj, ln0)):
             # unique(key) + CSR on the device (no host sync); G stays on the device
             if key is None:
@@ -130,7 +131,13 @@ class Update(nn.Module):
             # frame-pair groups are few and long (~190 edges at C3): split over waves
             y = U.softagg_csr(f16, g16, offs, perm, G, E, long_groups=key is not None)
             _, hy, _ = U.rowgemm(y, *ph, M_dev=G)
-            n32, n16 = U.rowadd_ln(n32, hy, gid, ln=ln)
+            if kk_add is None:
+                # net + agg_kk(net): only its fp16 rows (agg_ij's GEMM operand) are
+                # stored; the fp32 sum is recomputed by the next add, in order
+                _, n16 = U.rowadd_ln(n32, hy, gid, want32=False)
+                kk_add = (hy, gid)
+            else:
+                n32, n16 = U.rowadd_ln(n32, *kk_add, c16=hy, c_idx=gid, ln=ln)
         # gru = LN0 (fused above), GatedResidual, LN1, GatedResidual; then the d / w heads
         for gr, last in ((gr1, False), (gr2, True)):
             pgate, pr1, pr2 = gr

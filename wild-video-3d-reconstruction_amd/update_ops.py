@@ -303,7 +303,8 @@ class RowAddArgs(_ct.Structure):
     _fields_ = [("a", _ct.c_void_p), ("a_f16", _ct.c_int), ("lda", _ct.c_int64), ("M", _ct.c_int64),
                 ("b16", _ct.c_void_p), ("b_idx", _ct.c_void_p), ("b_rows", _ct.c_int64),
                 ("ln_g", _ct.c_void_p), ("ln_b", _ct.c_void_p), ("ln_eps", _ct.c_float),
-                ("out32", _ct.c_void_p), ("out16", _ct.c_void_p)]
+                ("out32", _ct.c_void_p), ("out16", _ct.c_void_p),
+                ("c16", _ct.c_void_p), ("c_idx", _ct.c_void_p), ("c_rows", _ct.c_int64)]
 
 
 _ZEROS = {}
@@ -434,8 +435,11 @@ def rowgemm_pair(A, Wa, ba, Wb, bb, M_dev=None):
     return outs[0], outs[1]
 
 
-def rowadd_ln(a, b16=None, b_idx=None, ln=None, want32=True, want16=True):
-    """v = a (+ b16[b_idx]) [-> LayerNorm] over 384-wide rows -> (out32, out16)."""
+def rowadd_ln(a, b16=None, b_idx=None, ln=None, want32=True, want16=True, c16=None, c_idx=None):
+    """v = a (+ b16[b_idx]) (+ c16[c_idx]) [-> LayerNorm] over 384-wide rows ->
+    (out32, out16).  The second addend is the next row add, in order: one call
+    with c16 is bit-identical to rowadd_ln(a, b16, b_idx)[0] fed to
+    rowadd_ln(., c16, c_idx, ln), without the fp32 rows in between."""
     H.on_gpu(a)
     if a.dim() != 2 or a.shape[1] != WIDTH or a.stride(1) != 1 or a.dtype not in (torch.float16, torch.float32):
         raise RuntimeError("rowadd_ln: a must be [M, 384] fp16/fp32 with contiguous rows")
@@ -450,6 +454,12 @@ def rowadd_ln(a, b16=None, b_idx=None, ln=None, want32=True, want16=True):
         if b16.dtype != torch.float16 or not b16.is_contiguous():
             raise RuntimeError("rowadd_ln: b16 must be contiguous fp16 [*, 384]")
         args.b16, args.b_idx, args.b_rows = _p(b16), _p(b_idx), b16.shape[0]
+    if c16 is not None:
+        if b16 is None or c16.dtype != torch.float16 or not c16.is_contiguous():
+            raise RuntimeError("rowadd_ln: c16 must be contiguous fp16 [*, 384] and follow b16")
+        if c_idx is not None:
+            c_idx = H.idx64(c_idx)
+        args.c16, args.c_idx, args.c_rows = _p(c16), _p(c_idx), c16.shape[0]
     if ln is not None:
         args.ln_g, args.ln_b, args.ln_eps = _p(ln[0]), _p(ln[1]), float(ln[2])
     args.out32, args.out16 = _p(out32), _p(out16)
