@@ -468,44 +468,47 @@ def cpu_baseline(slam, sample_edges, iterations):
                               "sample": f"altcorr on {sample_edges} edges, update operator on 2048 rows, 1 thread"}}
 
 
-def end_to_end(cfgd, buffer, iterations, frames, warmup=8, device="cuda"):
+def end_to_end(cfgd, buffer, iterations, frames, warmup=8, device="cuda", defer=True):
     """North-star end-to-end frames/s: DPVO.__call__ per synthetic 512x384
     frame (ingest CNNs + patchify + edges + update + keyframe) from the
     injected steady state.  Random weights give the motion magnitude no
     natural scale, so keyframe()'s decision alternates keep / drop frame by
     frame (KEYFRAME_THRESH set to -1 / +inf before each call; the motion
     magnitude is still computed and read): both paths are timed in equal
-    shares, and the counts are reported."""
+    shares, and the counts are reported.  defer: cfg.DEFER_KEYFRAME (each
+    decision applied by the next __call__, after its encoders are enqueued;
+    the last one inside the timed region, by flush_keyframe())."""
     from dpvo.synthetic import image_stream, steady_state_tracker
     total = frames + warmup
     slam = steady_state_tracker(cfgd["preset"], buffer=buffer, n=buffer - 8 - total, seed=0, iterations=iterations,
-                                device=device, **cfgd["overrides"])
+                                device=device, DEFER_KEYFRAME=defer, **cfgd["overrides"])
     intr = torch.tensor([320.0, 320.0, 320.0, 240.0], device=slam.device)
     imgs = [img for _, img in image_stream(total, device=slam.device)]
-    kept = [0, 0]
+    calls = [0]
     inner = slam.keyframe
 
     def keyframe():
-        drop = (kept[0] + kept[1]) % 2 == 0
-        slam.cfg.KEYFRAME_THRESH = float("inf") if drop else -1.0
-        n0 = slam.n
+        slam.cfg.KEYFRAME_THRESH = float("inf") if calls[0] % 2 == 0 else -1.0
+        calls[0] += 1
         inner()
-        kept[int(slam.n == n0)] += 1
     slam.keyframe = keyframe
     t_first = slam.n
     with torch.no_grad():
         for k, img in enumerate(imgs):
             if k == warmup:
-                kept[:] = [0, 0]
+                slam.flush_keyframe()
+                calls[0], drops0 = 0, getattr(slam, "keyframes_dropped", 0)
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
             slam(t_first + k, img, None, None, intr)
+        slam.flush_keyframe()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+    dropped = getattr(slam, "keyframes_dropped", 0) - drops0
     return {"metric": "end-to-end frames/s (DPVO.__call__: ingest CNNs + patchify + update + keyframe)",
             "value": round(frames / dt, 2), "unit": "frames/s", "ms_per_frame": round(dt / frames * 1e3, 3),
-            "frames": frames, "warmup": warmup, "keyframes_kept": kept[1], "keyframes_dropped": kept[0],
-            "keyframe_policy": "alternating keep / drop"}
+            "frames": frames, "warmup": warmup, "keyframes_kept": calls[0] - dropped, "keyframes_dropped": dropped,
+            "keyframe_policy": "alternating keep / drop", "deferred_keyframe": bool(defer)}
 
 
 def main():
@@ -592,7 +595,11 @@ def main():
         if world == 1 and args.e2e_frames > 0:
             del slam
             torch.cuda.empty_cache()
-            line["end_to_end"] = end_to_end(cfgd, args.buffer, args.iterations, args.e2e_frames, device=f"cuda:{local}")
+            e2e = end_to_end(cfgd, args.buffer, args.iterations, args.e2e_frames, device=f"cuda:{local}")
+            torch.cuda.empty_cache()
+            imm = end_to_end(cfgd, args.buffer, args.iterations, args.e2e_frames, device=f"cuda:{local}", defer=False)
+            e2e["immediate_keyframe"] = {"value": imm["value"], "ms_per_frame": imm["ms_per_frame"]}
+            line["end_to_end"] = e2e
         print(json.dumps(line), flush=True)
 
     if world > 1:

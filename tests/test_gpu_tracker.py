@@ -357,6 +357,51 @@ def test_edge_construction_follows_reference_rules():
     assert True in decisions and False in decisions
 
 
+def test_deferred_keyframe_equals_immediate():
+    """cfg.DEFER_KEYFRAME: the decision applied by the next __call__ (after its
+    encoders are enqueued) leaves the same state as the immediate keyframe():
+    edges, poses, patches and the trajectory from terminate() bit-identical,
+    on a stream that both keeps and drops frames."""
+    from dpvo.config import make_cfg
+    from dpvo.dpvo import DPVO
+    from dpvo.net import VONet
+    from dpvo.synthetic import image_stream
+    intr = torch.tensor([320.0, 320.0, 320.0, 240.0], device="cuda")
+    frames = list(image_stream(24))
+    out = []
+    for defer in (False, True):
+        torch.manual_seed(0)
+        net = VONet()
+        with torch.no_grad():
+            net.update.d[1].weight.mul_(40.0)  # random weights: make the motion probe pass
+        cfg = make_cfg("fast", BUFFER_SIZE=64, DEFER_KEYFRAME=defer)
+        calls = [0]
+        with torch.no_grad():
+            slam = DPVO(cfg, net, ht=384, wd=512)
+            orig_kf = slam.keyframe
+
+            def keyframe():
+                slam.cfg.KEYFRAME_THRESH = float("inf") if calls[0] % 3 == 0 else -1.0
+                calls[0] += 1
+                orig_kf()
+            slam.keyframe = keyframe
+            torch.manual_seed(1)
+            for t, img in frames:
+                slam(t, img, None, None, intr)
+            if defer:
+                assert slam._kf_pending is not None
+            slam.flush_keyframe()
+            state = [x.clone() for x in (slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.pg.poses_, slam.pg.patches_,
+                                         slam.pg.net)]
+            poses, tstamps = slam.terminate()
+        out.append((state, poses, tstamps, getattr(slam, "keyframes_dropped", 0), calls[0]))
+    (s0, p0, t0, d0, c0), (s1, p1, t1, d1, c1) = out
+    assert c0 == c1 and d0 == d1 and 0 < d0 < c0
+    for a, b in zip(s0, s1):
+        assert a.shape == b.shape and torch.equal(a, b)
+    assert np.array_equal(p0, p1) and np.array_equal(t0, t1)
+
+
 @pytest.mark.parametrize("preset,buffer,n", [("fast", 96, 70), ("dpvo_2k", 2048, 2040)])
 def test_window_ij_groups_equal_the_operator_key(preset, buffer, n):
     """DPVO._ij_groups (12-bit window key, counting sort) == the update

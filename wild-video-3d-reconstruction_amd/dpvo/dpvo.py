@@ -146,6 +146,7 @@ class DPVO:
 
     # ------------------------------------------------------------------ outputs
     def get_pts_clr_intri(self, inlier=False):
+        self.flush_keyframe()
         m = self.pg.m
         pts = pops.point_cloud_centre(SE3(self.poses), self.patches[:, :m], self.intrinsics, self.ix[:m])
         points = pts.cpu().numpy()
@@ -163,6 +164,7 @@ class DPVO:
         return dP * self.get_pose(t0)
 
     def terminate(self):
+        self.flush_keyframe()
         self.check_ba()
         if self.enable_global_ba:
             self.global_bundle_adjustment()
@@ -172,6 +174,7 @@ class DPVO:
         return poses, torch.as_tensor(self.tlist, dtype=torch.float64).numpy()
 
     def terminate_keyframe(self):
+        self.flush_keyframe()
         self.traj = {self.pg.tstamps_[i].item(): self.pg.poses_[i] for i in range(self.n)}
         poses = stack([SE3(self.pg.poses_[i]) for i in range(self.n)], dim=0).inv().data.cpu().numpy()
         return poses, torch.as_tensor([self.pg.tstamps_[i] for i in range(self.n)], dtype=torch.float64).numpy()
@@ -298,6 +301,7 @@ class DPVO:
         window-key check (an edge outside the 64-frame key window); BA then
         skips the step instead of updating depths from merged groups.
         DEFER_BA_CHECK = False restores the immediate raise."""
+        self.flush_keyframe()
         defer = getattr(self.cfg, "DEFER_BA_CHECK", True)
         if defer:
             self._ba_status.zero_()
@@ -432,17 +436,40 @@ class DPVO:
                          self.n, t0, self.gmap_._version, net_in.data_ptr(), net_in.shape), g, outs)
 
     def keyframe(self):
-        """drop a redundant keyframe, retire old edges (dpvo.py:605-658)."""
+        """drop a redundant keyframe, retire old edges (dpvo.py:605-658).
+
+        With cfg.DEFER_KEYFRAME the decision's one host read is deferred: this
+        call only enqueues the device work (both outcomes' edge masks, the
+        motion magnitudes, the BA status, the NaN check) and an asynchronous
+        copy of its values, and the next __call__ applies the decision after
+        enqueueing its frame's encoders -- the GPU runs them while the host
+        waits for the copy and launches the bookkeeping, instead of idling.
+        The state is the reference's once the decision is applied: by the next
+        __call__, terminate(), flush_keyframe() or any accessor that reads it."""
+        self.flush_keyframe()
+        pend = self._keyframe_begin()
+        if getattr(self.cfg, "DEFER_KEYFRAME", False):
+            self._kf_pending = pend
+        else:
+            self._keyframe_finish(pend)
+
+    def flush_keyframe(self):
+        """apply a deferred keyframe() decision (cfg.DEFER_KEYFRAME), if any."""
+        pend = getattr(self, "_kf_pending", None)
+        if pend is not None:
+            self._kf_pending = None
+            self._keyframe_finish(pend)
+
+    def _keyframe_begin(self):
         k = self.n - self.cfg.KEYFRAME_INDEX
         i, j = k - 1, k + 1
         RW = self.cfg.REMOVAL_WINDOW
         ii, jj, kk = self.pg.ii, self.pg.jj, self.pg.kk
-        E = kk.numel()
         # the edge masks of both outcomes, formed before the decision: keep
         # (edges whose patch left the removal window, :654-658) and drop (the
         # edges of frame k go, :616-617, and the retirement runs after the
         # frames above k moved down by one); their sizes ride on the one host
-        # read below, so the compaction needs no synchronisation of its own
+        # read, so the compaction needs no synchronisation of its own
         old_keep = self.ix[kk] < self.n - RW
         drop = (ii == k) | (jj == k)
         later = ii > k
@@ -455,11 +482,25 @@ class DPVO:
         # the compaction sizes
         sums = torch.stack([old_keep.sum(), old_d.sum(), rm_d.sum()]).double()
         vals = torch.cat([self._motionmag_dev(i, j).double(), self._ba_fail.double(),
-                          torch.isnan(self.pg.poses_[k]).any().double()[None], sums]).tolist()
+                          torch.isnan(self.pg.poses_[k]).any().double()[None], sums])
+        host = getattr(self, "_kf_host", None)
+        if host is None:
+            host = self._kf_host = torch.empty(7, dtype=torch.float64, pin_memory=True)
+        host.copy_(vals, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return dict(k=k, E=kk.numel(), old_keep=old_keep, old_d=old_d, rm_d=rm_d, later=later, kk_d=kk_d,
+                    thresh=self.cfg.KEYFRAME_THRESH, event=ev)
+
+    def _keyframe_finish(self, pd):
+        pd["event"].synchronize()
+        vals = self._kf_host.tolist()
+        k, E, later, kk_d = pd["k"], pd["E"], pd["later"], pd["kk_d"]
+        ii, jj = self.pg.ii, self.pg.jj
         self.check_ba(int(vals[2]))
         n_old_keep, n_old_d, n_rm_d = (int(v) for v in vals[4:7])
         m = vals[0] + vals[1]
-        if m / 2 < self.cfg.KEYFRAME_THRESH:
+        if m / 2 < pd["thresh"]:
             t0, t1 = self.pg.tstamps_[k - 1:k + 1].tolist()
             self.pg.delta[t1] = (t0, pops.pose_relative(self.pg.poses_[k], self.pg.poses_[k - 1]))
             # x[x > k] -= 1 as selects: no mask-size synchronisation
@@ -484,13 +525,14 @@ class DPVO:
                 self.image_buffer_[dst % self.mem] = self.image_buffer_[src % self.mem]
             self.n -= 1
             self.pg.m -= self.M
+            self.keyframes_dropped = getattr(self, "keyframes_dropped", 0) + 1
             # frame k's edges and the retired ones in one compaction (stable,
             # so the same order as the reference's two)
-            self.remove_factors(rm_d, store=old_d, counts=(E - n_rm_d, n_old_d))
+            self.remove_factors(pd["rm_d"], store=pd["old_d"], counts=(E - n_rm_d, n_old_d))
         elif vals[3]:
             raise Exception("Error: the estimated pose is nan!")
         else:
-            self.remove_factors(old_keep, store=True, counts=(E - n_old_keep, n_old_keep))
+            self.remove_factors(pd["old_keep"], store=True, counts=(E - n_old_keep, n_old_keep))
 
     # ------------------------------------------------------------------ global BA (C4)
     def compute_keyframe_distance(self, i, j, beta=0.5):
@@ -538,6 +580,7 @@ class DPVO:
 
     def global_bundle_adjustment(self):
         """one fastba pass over every keyframe (dpvo.py:436-505)."""
+        self.flush_keyframe()
         if not self.enable_global_ba or self.n < 2:
             return
         if self.use_distance_edges:
@@ -584,12 +627,17 @@ class DPVO:
 
     def __call__(self, tstamp, image, depth, mask, intrinsics):
         """track one frame (dpvo.py:771-875)."""
-        if self.pg.n + 1 >= self.pg.N:
+        if self.pg.n + 1 >= self.pg.N and getattr(self, "_kf_pending", None) is None:
             raise Exception(f'The buffer size is too small. You can increase it using "--buffer {self.N * 2}"')
         with torch.autocast("cuda", enabled=self.cfg.MIXED_PRECISION):
             fmap, gmap, imap, patches, _, clr = self.network.patchify(
                 image, patches_per_image=self.cfg.PATCHES_PER_FRAME, gradient_bias=self.cfg.GRADIENT_BIAS,
                 return_color=True, mask=mask)
+        # the previous frame's deferred keyframe decision (cfg.DEFER_KEYFRAME),
+        # its host read overlapping this frame's encoders
+        self.flush_keyframe()
+        if self.pg.n + 1 >= self.pg.N:
+            raise Exception(f'The buffer size is too small. You can increase it using "--buffer {self.N * 2}"')
         n = self.n
         self.tlist.append(tstamp)
         self.pg.tstamps_[n] = self.counter
