@@ -44,7 +44,8 @@ UPD_BYTES_PER_EDGE = (
     + 2 * (768 + 1536 + 1536 + 768)    # c1, c2 chains: gathered row, net32 in; net32, net16 out
     + 2 * (768 + 1536)                 # SoftAgg f|g pair GEMMs: net16 in, f16 | g16 out
     + 2 * 1536                         # SoftAgg reduce: f, g rows in
-    + 2 * (1536 + 1536 + 768)          # rowadd_ln: net32 in; net32, net16 out
+    + (1536 + 768)                     # rowadd (agg_kk): net32 in; net16 out (the fp32 sum is recomputed)
+    + (1536 + 1536 + 768)              # rowadd + LN (agg_ij): net32 in; net32, net16 out
     + (768 + 1536 + 1536 + 768)        # gated chain 1: net16, net32 in; net32, net16 out
     + (768 + 1536 + 1536 + 8))         # gated chain 2: net16, net32 in; net32, heads out
 COUNTERS_JSON = os.path.join(REPO, "profiles", "counters_c3.json")
@@ -468,7 +469,7 @@ def cpu_baseline(slam, sample_edges, iterations):
                               "sample": f"altcorr on {sample_edges} edges, update operator on 2048 rows, 1 thread"}}
 
 
-def end_to_end(cfgd, buffer, iterations, frames, warmup=8, device="cuda", defer=True):
+def end_to_end(cfgd, buffer, iterations, frames, warmup=8, device="cuda", defer=True, mark_gap=0.0):
     """North-star end-to-end frames/s: DPVO.__call__ per synthetic 512x384
     frame (ingest CNNs + patchify + edges + update + keyframe) from the
     injected steady state.  Random weights give the motion magnitude no
@@ -499,6 +500,8 @@ def end_to_end(cfgd, buffer, iterations, frames, warmup=8, device="cuda", defer=
                 slam.flush_keyframe()
                 calls[0], drops0 = 0, getattr(slam, "keyframes_dropped", 0)
                 torch.cuda.synchronize()
+                if mark_gap:   # an idle gap that marks the timed frames in a kernel trace
+                    time.sleep(mark_gap)
                 t0 = time.perf_counter()
             slam(t_first + k, img, None, None, intr)
         slam.flush_keyframe()

@@ -436,11 +436,13 @@ int dpvo_rowchain_gated(const dpvo_rowgemm_args* gate, const dpvo_rowgemm_args* 
                         const dpvo_rowgemm_args* second, void* stream);
 
 /* Row add + LayerNorm over 384-wide rows (one pass):
- *   v = a[m] (+ b16[b_idx[m]])  [-> LayerNorm]  -> out32 [M][384] / out16 [M][384]
+ *   v = (a[m] (+ b16[b_idx[m]])) (+ c16[c_idx[m]])  [-> LayerNorm]  -> out32 [M][384] / out16 [M][384]
  * a is fp16 (a_f16=1) or fp32 with row stride lda (a multiple of 4); b_idx[m] < 0
- * adds nothing.  Vector access: a, out32, ln_g / ln_b 16-byte aligned (a 8-byte
- * when fp16), b16 and out16 8-byte aligned.
- * Used for `net + h(y)[:, jx]` after SoftAgg and the GRU's first LayerNorm. */
+ * (c_idx[m] < 0) adds nothing; c16 needs b16.  Vector access: a, out32, ln_g /
+ * ln_b 16-byte aligned (a 8-byte when fp16), b16, c16 and out16 8-byte aligned.
+ * Used for `net + h(y)[:, jx]` after SoftAgg and the GRU's first LayerNorm: the
+ * agg_kk add writes out16 only, the agg_ij add passes both SoftAggs' rows
+ * (b16 = agg_kk's, c16 = agg_ij's) -- the same fp32 adds in the same order. */
 typedef struct dpvo_rowadd_args {
     const void* a; int a_f16; int64_t lda; int64_t M;
     const void* b16; const int64_t* b_idx; int64_t b_rows;

@@ -963,6 +963,8 @@ constexpr int RC_STAGE = RC_A_STAGE + RC_W_STAGE;  // 32 KB
 constexpr int RC_Y = RG_BM * 768;                  // 96 KB
 constexpr int RC_LDS = RC_Y + 2 * RC_STAGE;        // 160 KB
 
+constexpr int RC_RN = 6, RC_RD = RC_RN - 2;   // A ring: 6 x 16 KB slots in the y-tile region, 4 stages ahead
+
 struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflict-free
     // ds_read_b128 fragment reads down 16 rows and 256-byte row sweeps
     __device__ int off(int r, int byte) const { return r * 768 + (((byte >> 4) ^ (r & 15)) << 4) + (byte & 15); }
@@ -983,7 +985,7 @@ struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflic
 // Bit-identical to rowchain (corr0, corr1, LN|LN_RELU) -> fp16 rows ->
 // rowgemm (corr2, RES|LN): the same MFMA k order and the same epilogue code.
 // DBG (timing experiments only, DPVO_RC_DBG, flag RES; scripts/bench_rc_dbg.py):
-// 1 no row pass, 2 no MFMA, 3 neither
+// 1 no row pass, 2 no MFMA, 3 neither; 256 GEMM1's A through a ring in the y-tile region
 template <int F2, bool GATED = false, int DBG = 0, int FMID = 0>
 __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
                                                                  dpvo_rowgemm_args pg)
@@ -1062,6 +1064,48 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+    };
+    // ---- GEMM1's A stream through a ring in the (then unused) y-tile region
+    // (RING, DPVO_RC_DBG=256): stages of 64 k (128 rows x 128 B = 16 KB, whole
+    // lines), RC_RD stages in flight, issued by waves 0-3 only while waves 4-7
+    // issue the W stages: vmcnt counts each wave's own loads in order, so the
+    // W waves wait for one W stage and the A waves for the A stage issued
+    // RC_RD stages back -- the gathered rows' HBM latency leaves the k-step.
+    // Piece j of wave w (0-3) holds rows 8 (4 w + j) .. + 7, lane L row
+    // 8 (4 w + j) + L / 8, physical chunk L % 8 = logical chunk ^ ((row >> 1) & 7).
+    // measured slower than the stage-buffer A stream (c1 chain 157 vs 147 us,
+    // k-loops alone 94 vs 85: profiles/r3/NOTES.md): timing experiment only
+    constexpr bool RING = (DBG & 256) != 0;
+    const bool awave = wave < 4;
+    const half_t* rsrc[4];
+    auto set_ring_tile = [&](int64_t tile) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int r = 8 * (4 * (wave & 3) + j) + (lane >> 3);
+            const int64_t m = tile * RG_BM + r;
+            const half_t* row = zero;
+            if (m < Mrows) {
+                const int64_t s = p1.a_idx ? p1.a_idx[m] : m;
+                if (s >= 0 && s < p1.a_rows) row = (const half_t*)p1.A + s * p1.lda;
+            }
+            rsrc[j] = row + 8 * ((lane & 7) ^ ((r >> 1) & 7));
+        }
+    };
+    auto issue_ring = [&](int st) {   // A stage st (k = 64 st ..) into ring slot st % RC_RN
+        char* dst = smem + (st % RC_RN) * 16384 + (4 * (wave & 3)) * 1024;
+#pragma unroll
+        for (int j = 0; j < 4; j++) glds16(rsrc[j] + 64 * st, dst + j * 1024);
+    };
+    // W waves 4-7: the stage's 24 pieces, 6 each, into the W part of stage buffer buf
+    auto issue_wonly = [&](int ks, int buf) {
+        char* st = smem + RC_Y + buf * RC_STAGE;
+#pragma unroll
+        for (int j = 0; j < 6; j++) {
+            const int pc = 6 * (wave - 4) + j;   // W piece 0 .. 23 = stage piece 8 + pc
+            const int n = pc * 16 + (lane >> 2);
+            const half_t* src = W1 + (int64_t)n * RC_BK + 8 * ((lane & 3) ^ ((n >> 2) & 3));
+            glds16(src + (int64_t)ks * (RG_BN * RC_BK), st + (8 + pc) * 1024);
+        }
     };
 
     f4_t acc[4][6];
@@ -1155,6 +1199,55 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             }
         }
     };
+    // GEMM1 with the A ring (not the gate pass: the y tile is in use then).
+    // Caller: W stage 0 issued by the W waves into buffer 0, nothing of A.
+    int ring_off[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++) {
+        const int row = wm * 64 + mt * 16 + fr;
+        ring_off[mt] = row * 128 + 16 * (fq ^ ((row >> 1) & 7));   // + 16 * 4 (ks & 1) via the xor below
+    }
+    auto gemm1_ring = [&]() {
+        const int nst = ks1 / 2;   // A stages (K1 % 64 == 0 on this path)
+        if (awave) {
+#pragma unroll
+            for (int st = 0; st < RC_RD; st++)
+                if (st < nst) issue_ring(st);
+        }
+#pragma unroll 1
+        for (int ks = 0; ks < ks1; ks++) {
+            if (!awave) {
+                if (ks + 1 < ks1) {
+                    issue_wonly(ks + 1, (ks + 1) & 1);
+                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+            } else if ((ks & 1) == 0) {
+                // A stage ks/2 landed: the stages issued after it may fly (4 pieces each)
+                const int st = ks >> 1, after = min(RC_RD - 1, nst - 1 - st);
+                if (after >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+                else if (after == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                else if (after == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // the slot of stage st + RC_RD held stage st - 2 (RC_RN = RC_RD + 2),
+                // read by every wave before the previous step's barriers
+                if (st + RC_RD < nst) issue_ring(st + RC_RD);
+            }
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const char* sa = smem + ((ks >> 1) % RC_RN) * 16384;
+            const char* st = smem + RC_Y + (ks & 1) * RC_STAGE;
+            const int sub = (ks & 1) * 64;   // logical chunks 4 (ks & 1) + fq: xor-ing 4 flips bit 2 only
+            h8_t a[4], b[6];
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(sa + (ring_off[mt] ^ sub));
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+            mfma_step(a, b);
+            __builtin_amdgcn_s_barrier();
+        }
+    };
     auto gemm1 = [&](bool gate) {
         for (int ks = 0; ks < ks1; ks++) {
             if (ks + 1 < ks1) {
@@ -1176,13 +1269,20 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         }
     };
     int64_t tile = blockIdx.x;
-    set_tile(tile);
-    issue1(0, 0);
+    if (RING) {
+        set_ring_tile(tile);
+        if (GATED) set_tile(tile);   // the gate pass streams A through the stages
+        if (!awave) issue_wonly(0, 0);
+    } else {
+        set_tile(tile);
+        issue1(0, 0);
+    }
     for (; tile < ntiles; tile += gridDim.x) {
         const bool more = tile + gridDim.x < ntiles;
         // ---- GEMM1: A (global, gathered) x W1
         zero_acc();
-        gemm1(false);
+        if (RING) gemm1_ring();
+        else gemm1(false);
         // ---- intermediate -> y tile; W2's first stage into the released stage 0
         acc_to_y((const half_t*)p1.bias, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
         issue2(0, 0);
@@ -1247,8 +1347,14 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         }
         // ---- the next tile's first GEMM1 stage loads under this epilogue
         if (more) {
-            set_tile(tile + gridDim.x);
-            issue1(0, 0);
+            if (RING) {
+                set_ring_tile(tile + gridDim.x);
+                if (GATED) set_tile(tile + gridDim.x);
+                if (!awave) issue_wonly(0, 0);
+            } else {
+                set_tile(tile + gridDim.x);
+                issue1(0, 0);
+            }
         }
         sync_lds();
         // LayerNorm / head constants loaded per tile, not held across the GEMMs
@@ -2300,7 +2406,7 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
         hipLaunchKernelGGL((rowchain_kernel<DPVO_RG_RES, false, (D)>), dim3(grid), dim3(RG_THREADS), 0,            \
                            as_stream(stream), *g1, a2, a2);                                                       \
         break;
-            RCD_CASE(0) RCD_CASE(1) RCD_CASE(2) RCD_CASE(3) RCD_CASE(16) RCD_CASE(32) RCD_CASE(48)
+            RCD_CASE(0) RCD_CASE(1) RCD_CASE(2) RCD_CASE(3) RCD_CASE(16) RCD_CASE(32) RCD_CASE(48) RCD_CASE(256) RCD_CASE(257)
 #undef RCD_CASE
         default:
             set_error("DPVO_RC_DBG: unsupported value");
