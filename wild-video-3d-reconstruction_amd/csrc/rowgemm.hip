@@ -985,7 +985,8 @@ struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflic
 // Bit-identical to rowchain (corr0, corr1, LN|LN_RELU) -> fp16 rows ->
 // rowgemm (corr2, RES|LN): the same MFMA k order and the same epilogue code.
 // DBG (timing experiments only, DPVO_RC_DBG, flag RES; scripts/bench_rc_dbg.py):
-// 1 no row pass, 2 no MFMA, 3 neither; 256 GEMM1's A through a ring in the y-tile region
+// 1 no row pass, 2 no MFMA, 3 neither; 256 GEMM1's A through a ring in the y-tile region;
+// 512 ping-pong wave groups
 template <int F2, bool GATED = false, int DBG = 0, int FMID = 0>
 __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
                                                                  dpvo_rowgemm_args pg)
@@ -1062,6 +1063,54 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
     };
     auto sync_lds = [&]() {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    // ---- ping-pong k-loops (PP, DPVO_RC_DBG=512; measured no faster: the
+    // k-loops are bound by the per-CU LDS-DMA fill rate, profiles/r3/NOTES.md):
+    // the waves run as two groups,
+    // G0 = waves 0-3 and G1 = waves 4-7 (one of each per SIMD), G1 one barrier
+    // behind, so on every SIMD one wave's MFMAs run while the other wave reads
+    // its fragments -- with both in step (DPVO_RC_DBG=512) each k-step costs
+    // MFMA + LDS reads + DMA one after the other.  G0 issues every stage's
+    // LDS-DMA (8 pieces per wave for GEMM1, 6 for the W-only stages) at the
+    // start of its read phase and waits for it before the barrier that opens
+    // its next read phase; G1 reads a stage one phase after G0.
+    constexpr bool PP = (DBG & 512) != 0;
+    const bool G0 = wave < 4;
+    // G0 wave w issues stage pieces 2w, 2w+1 (A rows) and 8 + 6w .. + 5 (W rows;
+    // one base pointer: the pieces are 512 elements apart in the k-blocked W)
+    const half_t* qa[2];
+    const int wq = ((6 * (wave & 3)) * 16 + srow) * RC_BK + 8 * (pch ^ ((srow >> 2) & 3));
+    auto set_tile_pp = [&](int64_t tile) {
+        if (!PP || !G0) return;
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const int r = (2 * wave + j) * 16 + srow;
+            const int64_t m = tile * RG_BM + r;
+            const half_t* row = zero;
+            if (m < Mrows) {
+                const int64_t s = p1.a_idx ? p1.a_idx[m] : m;
+                if (s >= 0 && s < p1.a_rows) row = (const half_t*)p1.A + s * p1.lda;
+            }
+            qa[j] = row + 8 * (pch ^ ((r >> 2) & 3));
+        }
+    };
+    auto issue1_pp = [&](int ks, int buf, bool gate) {
+        char* st = smem + RC_Y + buf * RC_STAGE;
+#pragma unroll
+        for (int j = 0; j < 2; j++) glds16(qa[j] + ks * RC_BK, st + (2 * wave + j) * 1024);
+        const half_t* w = W1 + wq + (int64_t)ks * (RG_BN * RC_BK) + (GATED && gate ? gdelta : 0);
+#pragma unroll
+        for (int j = 0; j < 6; j++) glds16(w + 512 * j, st + (8 + 6 * wave + j) * 1024);
+    };
+    auto issue2_pp = [&](int ks, int buf, int64_t wdelta) {
+        char* st = smem + RC_Y + buf * RC_STAGE + RC_A_STAGE;
+        const half_t* w = W2 + wq + (int64_t)ks * (RG_BN * RC_BK) + wdelta;
+#pragma unroll
+        for (int j = 0; j < 6; j++) glds16(w + 512 * j, st + (6 * wave + j) * 1024);
+    };
+    auto bar = []() {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
     };
@@ -1199,6 +1248,39 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             }
         }
     };
+    // One ping-pong GEMM: stage 0 issued (any mapping) into buffer 0 by the caller.
+    auto pp_loop = [&](int nks, auto issue, auto read) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stage-0 pieces
+        bar();
+        if (!G0) bar();   // G1: one phase behind
+#pragma unroll 1
+        for (int ks = 0; ks < nks; ks++) {
+            // read phase (G0: during G1's MFMAs of the previous step)
+            if (G0 && ks + 1 < nks) issue(ks + 1, (ks + 1) & 1);
+            h8_t a[4], b[6];
+            read(ks, ks & 1, a, b);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // (pinned: the scheduler would move MFMAs -- not memory operations --
+            // across the barrier, into the read phase)
+            __builtin_amdgcn_sched_barrier(0);
+            bar();
+            __builtin_amdgcn_sched_barrier(0);
+            // MFMA phase (G0: during G1's read phase)
+            mfma_step(a, b);
+            __builtin_amdgcn_sched_barrier(0);
+            if (G0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // stage ks+1 landed
+            bar();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (G0) bar();   // back in step: every read and MFMA of the loop is done
+    };
+    auto read1 = [&](int, int buf, h8_t (&a)[4], h8_t (&b)[6]) {
+        const char* st = smem + RC_Y + buf * RC_STAGE;
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(st + a_off[mt]);
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+    };
     // GEMM1 with the A ring (not the gate pass: the y tile is in use then).
     // Caller: W stage 0 issued by the W waves into buffer 0, nothing of A.
     int ring_off[4];
@@ -1249,6 +1331,10 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         }
     };
     auto gemm1 = [&](bool gate) {
+        if (PP) {
+            pp_loop(ks1, [&](int ks, int buf) { issue1_pp(ks, buf, gate); }, read1);
+            return;
+        }
         for (int ks = 0; ks < ks1; ks++) {
             if (ks + 1 < ks1) {
                 issue1(ks + 1, (ks + 1) & 1, gate);
@@ -1275,6 +1361,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         if (!awave) issue_wonly(0, 0);
     } else {
         set_tile(tile);
+        set_tile_pp(tile);
         issue1(0, 0);
     }
     for (; tile < ntiles; tile += gridDim.x) {
@@ -1290,6 +1377,19 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         // ---- GEMM2: y tile x W2 (stage 0 already issued); wdelta selects W3
         auto gemm_y = [&](int64_t wdelta) {
             zero_acc();
+            if (PP) {
+                pp_loop(
+                    ks2, [&](int ks, int buf) { issue2_pp(ks, buf, wdelta); },
+                    [&](int ks, int buf, h8_t (&a)[4], h8_t (&b)[6]) {
+                        const char* st = smem + RC_Y + buf * RC_STAGE;
+#pragma unroll
+                        for (int mt = 0; mt < 4; mt++)
+                            a[mt] = *(const h8_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, (ks * 4 + fq) * 16));
+#pragma unroll
+                        for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+                    });
+                return;
+            }
 #pragma unroll 1
             for (int ks = 0; ks < ks2; ks++) {
                 if (ks + 1 < ks2) {
@@ -1353,6 +1453,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
                 if (!awave) issue_wonly(0, 0);
             } else {
                 set_tile(tile + gridDim.x);
+                set_tile_pp(tile + gridDim.x);
                 issue1(0, 0);
             }
         }
@@ -2406,7 +2507,7 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
         hipLaunchKernelGGL((rowchain_kernel<DPVO_RG_RES, false, (D)>), dim3(grid), dim3(RG_THREADS), 0,            \
                            as_stream(stream), *g1, a2, a2);                                                       \
         break;
-            RCD_CASE(0) RCD_CASE(1) RCD_CASE(2) RCD_CASE(3) RCD_CASE(16) RCD_CASE(32) RCD_CASE(48) RCD_CASE(256) RCD_CASE(257)
+            RCD_CASE(0) RCD_CASE(1) RCD_CASE(2) RCD_CASE(3) RCD_CASE(16) RCD_CASE(32) RCD_CASE(48) RCD_CASE(256) RCD_CASE(257) RCD_CASE(512) RCD_CASE(513)
 #undef RCD_CASE
         default:
             set_error("DPVO_RC_DBG: unsupported value");
