@@ -468,14 +468,17 @@ int dpvo_window_keys(const int64_t* ii, const int64_t* jj, const int64_t* kk, in
  * four launches.  Writes ctx, jslot and flag as dpvo_window_keys does (the
  * key arrays are not written out) and the two CSRs exactly as dpvo_group_by
  * would: gid int64 [E], offs int32 [E + 1], perm int32 [E], groups int64 [1].
- * kk_bits: 1..22, with 64 M <= 2^kk_bits for in-window keys.  workspace: at
- * least dpvo_window_group_by_workspace_bytes(E, kk_bits) device bytes (0 for a
- * bad kk_bits). */
+ * kk_bits: 1..22, with 64 M <= 2^kk_bits for in-window keys.  jj_order
+ * (optional int32 [E]): the edges grouped by target frame (jj - base, in
+ * ascending jj; any order within a frame) -- the visiting order of
+ * dpvo_corr_pyramid_mfma, as dpvo_edge_order would give it by ring slot.
+ * workspace: at least dpvo_window_group_by_workspace_bytes(E, kk_bits) device
+ * bytes (0 for a bad kk_bits). */
 size_t dpvo_window_group_by_workspace_bytes(int64_t E, int kk_bits);
 int dpvo_window_group_by(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t E, int64_t M, int64_t base,
                          int64_t ring, int64_t frames, int kk_bits, int64_t* ctx, int64_t* jslot, int* flag,
                          int64_t* kk_gid, int* kk_offs, int* kk_perm, int64_t* kk_groups, int64_t* ij_gid,
-                         int* ij_offs, int* ij_perm, int64_t* ij_groups, void* workspace, size_t workspace_bytes,
+                         int* ij_offs, int* ij_perm, int64_t* ij_groups, int* jj_order, void* workspace, size_t workspace_bytes,
                          void* stream);
 
 /* DPVO.__call__'s edge append (dpvo.py:756-769,799-800) in one launch:

@@ -53,6 +53,13 @@ def test_random_window_edges(E, M, seed):
     ii, jj, kk = ii.cuda(), jj.cuda(), kk.cuda()
     args = (ii, jj, kk, M, n - 64, M * 40, 40)
     assert_same(update_ops.window_group_by(*args), separate(*args))
+    # the optional target-frame order: the same CSRs, and a permutation of the
+    # edges with jj ascending (altcorr's visiting order)
+    got = update_ops.window_group_by(*args, jj_order=True)
+    assert_same(got[:4], separate(*args))
+    order = got[4].long()
+    assert torch.equal(torch.sort(order).values, torch.arange(E, device="cuda"))
+    assert bool((jj[order][1:] >= jj[order][:-1]).all())
 
 
 def test_groups_above_the_lds_cap():

@@ -87,7 +87,7 @@ _SIGNATURES = {
     "dpvo_edge_targets": (_ip, [_vp, _i64, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp]),
     "dpvo_window_keys": (_ip, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp]),
     "dpvo_window_group_by_workspace_bytes": (_sz, [_i64, _ip]),
-    "dpvo_window_group_by": (_ip, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _ip] + [_vp] * 12 + [_sz, _vp]),
+    "dpvo_window_group_by": (_ip, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _ip] + [_vp] * 13 + [_sz, _vp]),
     "dpvo_encoder_tiles": (_i64, [_ip, _ip, _ip, _ip]),
     "dpvo_encoder_stem": (_ip, [_vp, _ip, _ip, _vp, _ip, _vp]),
     "dpvo_encoder_conv": (_ip, [_ip] * 7 + [_vp, _ip, _vp]),

@@ -688,7 +688,7 @@ __global__ __launch_bounds__(256) void window_keys_kernel(const int64_t* __restr
 constexpr int WG_IJ_BITS = 12;
 
 struct WgLayout {
-    int64_t hist, pre_kk, pre_ij, slot_kk, slot_ij, ptmp_kk, ptmp_ij, key_kk, key_ij, total;
+    int64_t hist, pre_kk, pre_ij, pre_j, slot_kk, slot_ij, ptmp_kk, ptmp_ij, key_kk, key_ij, total;
 };
 
 WgLayout wg_layout(int64_t n, int kk_bits)
@@ -699,6 +699,7 @@ WgLayout wg_layout(int64_t n, int kk_bits)
     L.hist = o;    o += align256(4 * (Bkk + Bij));   // kk bins then ij bins: one memset
     L.pre_kk = o;  o += align256(8 * Bkk);
     L.pre_ij = o;  o += align256(8 * Bij);
+    L.pre_j = o;   o += align256(4 * Bij);           // ij bins' starts in jj-major order
     L.slot_kk = o; o += align256(4 * n);
     L.slot_ij = o; o += align256(4 * n);
     L.ptmp_kk = o; o += align256(4 * n);
@@ -751,9 +752,42 @@ __global__ __launch_bounds__(256) void wg_hist_kernel(const int64_t* __restrict_
 __global__ __launch_bounds__(1024) void wg_scan_kernel(const int* __restrict__ hist, int Bkk, int64_t* __restrict__ pre_kk,
                                                        int64_t* __restrict__ pre_ij, int* __restrict__ offs_kk,
                                                        int* __restrict__ offs_ij, int64_t* __restrict__ groups_kk,
-                                                       int64_t* __restrict__ groups_ij, int n)
+                                                       int64_t* __restrict__ groups_ij, int n,
+                                                       int* __restrict__ pre_j)
 {
     __shared__ int64_t wsum[16];
+    if (blockIdx.x == 2) {
+        // the (ii, jj) bins visited jj-major (bin a * 64 + b at transposed
+        // position b * 64 + a): their starts give altcorr's target-frame order
+        // from the ij slots, with no histogram of its own
+        const int* h = hist + Bkk;
+        const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+        int c[4], loc[4], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int tix = 4 * t + j, b = tix >> 6, a = tix & 63;
+            c[j] = h[a * 64 + b];
+            loc[j] = sum;
+            sum += c[j];
+        }
+        int x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[w] = x;
+        __syncthreads();
+        int off = 0;
+#pragma unroll
+        for (int i = 0; i < 16; i++) off += i < w ? (int)wsum[i] : 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int tix = 4 * t + j, b = tix >> 6, a = tix & 63;
+            pre_j[a * 64 + b] = off + x - sum + loc[j];
+        }
+        return;
+    }
     const bool ij = blockIdx.x != 0;
     const int B = ij ? (1 << WG_IJ_BITS) : Bkk;
     const int* h = ij ? hist + Bkk : hist;
@@ -814,9 +848,11 @@ __global__ __launch_bounds__(256) void wg_scatter_kernel(int64_t E, const uint32
                                                          const int* __restrict__ slot_ij, int* __restrict__ ptmp_kk,
                                                          int* __restrict__ ptmp_ij, int64_t* __restrict__ gid_kk,
                                                          int64_t* __restrict__ gid_ij, int* __restrict__ offs_kk,
-                                                         int* __restrict__ offs_ij)
+                                                         int* __restrict__ offs_ij, const int* __restrict__ pre_j,
+                                                         int* __restrict__ order_j)
 {
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
+        if (order_j) order_j[pre_j[key_ij[e]] + slot_ij[e]] = (int)e;
         const int64_t p = pre_kk[key_kk[e]], q = pre_ij[key_ij[e]];
         const int sp = slot_kk[e], sq = slot_ij[e];
         const int ps = (int)(p & 0xffffffff), pg = (int)(p >> 32), qs = (int)(q & 0xffffffff), qg = (int)(q >> 32);
@@ -1109,7 +1145,8 @@ extern "C" int dpvo_window_group_by(const int64_t* ii, const int64_t* jj, const 
                                     int64_t base, int64_t ring, int64_t frames, int kk_bits, int64_t* ctx,
                                     int64_t* jslot, int* flag, int64_t* kk_gid, int* kk_offs, int* kk_perm,
                                     int64_t* kk_groups, int64_t* ij_gid, int* ij_offs, int* ij_perm,
-                                    int64_t* ij_groups, void* workspace, size_t workspace_bytes, void* stream)
+                                    int64_t* ij_groups, int* jj_order, void* workspace, size_t workspace_bytes,
+                                    void* stream)
 {
     DPVO_CHECK_ARG(E >= 0 && E < (int64_t(1) << 31), "bad size");
     DPVO_CHECK_ARG(M > 0 && ring > 0 && frames > 0, "M > 0, ring > 0 and frames > 0 required");
@@ -1137,14 +1174,15 @@ extern "C" int dpvo_window_group_by(const int64_t* ii, const int64_t* jj, const 
     int* ptmp_ij = (int*)(ws + L.ptmp_ij);
     uint32_t* key_kk = (uint32_t*)(ws + L.key_kk);
     uint32_t* key_ij = (uint32_t*)(ws + L.key_ij);
+    int* pre_j = (int*)(ws + L.pre_j);
     const unsigned gn = grid_for(E, 256, 2048);
     DPVO_CHECK_HIP(hipMemsetAsync(hist, 0, 4 * (size_t)(Bkk + (1 << WG_IJ_BITS)), st));
     hipLaunchKernelGGL(wg_hist_kernel, dim3(gn), dim3(256), 0, st, ii, jj, kk, E, M, base, ring, frames,
                        (uint32_t)(Bkk - 1), ctx, jslot, flag, hist, hist + Bkk, slot_kk, slot_ij, key_kk, key_ij);
-    hipLaunchKernelGGL(wg_scan_kernel, dim3(2), dim3(1024), 0, st, hist, Bkk, pre_kk, pre_ij, kk_offs, ij_offs,
-                       kk_groups, ij_groups, (int)E);
+    hipLaunchKernelGGL(wg_scan_kernel, dim3(jj_order ? 3 : 2), dim3(1024), 0, st, hist, Bkk, pre_kk, pre_ij, kk_offs,
+                       ij_offs, kk_groups, ij_groups, (int)E, pre_j);
     hipLaunchKernelGGL(wg_scatter_kernel, dim3(gn), dim3(256), 0, st, E, key_kk, key_ij, pre_kk, pre_ij, slot_kk,
-                       slot_ij, ptmp_kk, ptmp_ij, kk_gid, ij_gid, kk_offs, ij_offs);
+                       slot_ij, ptmp_kk, ptmp_ij, kk_gid, ij_gid, kk_offs, ij_offs, pre_j, jj_order);
     const int64_t waves = std::min<int64_t>(E, Bkk) + std::min<int64_t>(E, 1 << WG_IJ_BITS);
     const unsigned gf = grid_for(waves * 64, 64 * CB_WAVES, 2048);
     hipLaunchKernelGGL(wg_fix_kernel, dim3(gf), dim3(64 * CB_WAVES), 0, st, E, ptmp_kk, kk_offs, kk_groups, kk_gid,

@@ -180,9 +180,11 @@ class DPVO:
         return poses, torch.as_tensor([self.pg.tstamps_[i] for i in range(self.n)], dtype=torch.float64).numpy()
 
     # ------------------------------------------------------------------ hot path
-    def corr(self, coords, indicies=None, slots=None):
+    def corr(self, coords, indicies=None, slots=None, order=None):
         """2-level local correlation -> [1, E, 882] (dpvo.py:326-333), one fused launch.
-        slots: the ring slots (kk mod M pmem, jj mod pmem) when the caller has them."""
+        slots: the ring slots (kk mod M pmem, jj mod pmem) when the caller has them;
+        order: the edges grouped by target frame (the matrix-core kernel's
+        visiting order) when the caller has it."""
         if slots is not None:
             ii1, jj1 = slots
         else:
@@ -199,7 +201,8 @@ class DPVO:
             if not getattr(self.cfg, "EXACT_CORR", False) and getattr(self.cfg, "CHANNEL_LAST_FMAPS", True):
                 # matrix cores, fp32 accumulation (csrc/corrmfma.hip)
                 # edges grouped by target frame: one frame's map per XCD L2 at a time
-                order = cuda_corr.edge_order(jj1, self.pmem)
+                if order is None:
+                    order = cuda_corr.edge_order(jj1, self.pmem)
                 return altcorr.corr_pyramid_mfma(self._gmap_table(mfma=True), self.gmap.shape[1], self.pyramid,
                                                  coords, ii1, jj1, out=out, order=order).view(1, E, -1)
             table = self._gmap_table()
@@ -314,16 +317,17 @@ class DPVO:
                 # the ring slots (context rows, corr) and both group-bys over the
                 # window keys in four launches (an edge outside the window sets
                 # the deferred failure word: the next keyframe() / check_ba() raises)
-                ctx_idx, jslot, kk_groups, ij_groups = update_ops.window_group_by(
+                # (+ the edges grouped by target frame: altcorr's visiting order)
+                ctx_idx, jslot, kk_groups, ij_groups, order = update_ops.window_group_by(
                     self.pg.ii, self.pg.jj, self.pg.kk, self.M, self.n - 64, self.M * self.pmem, self.pmem,
-                    flag=self._ba_status if defer else self._ba_fail)
+                    flag=self._ba_status if defer else self._ba_fail, jj_order=True)
                 slots = (ctx_idx, jslot)
             else:
                 kk_groups, ij_groups = self._kk_groups(), self._ij_groups()
                 ctx_idx = self.pg.kk % (self.M * self.pmem)
-                slots = None
+                slots = order = None
             with torch.autocast("cuda", enabled=True):
-                corr = self.corr(coords, slots=slots)
+                corr = self.corr(coords, slots=slots, order=order)
                 # ctx = imap[:, kk % (M pmem)] (dpvo.py:718), gathered by the consumer
                 self.pg.net, (delta, weight, _) = self.network.update(self.pg.net, self.imap, corr, None, self.pg.ii,
                                                                       self.pg.jj, self.pg.kk, inp_idx=ctx_idx,

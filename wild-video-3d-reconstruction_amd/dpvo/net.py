@@ -121,15 +121,17 @@ class Update(nn.Module):
             n32, n16, _ = U.rowchain(n16, *la, *lb, flags1=U.RELU, a_idx=nb, flags=U.RES, res32=n32, want32=True)
         ln0, gr1, ln1, gr2 = pk["gru"]
         kk_add = None
-        for (pf, pg_, ph), key, ln in ((pk["agg_kk"], None, None), (pk["agg_ij"], ii * 12345 + jj, ln0)):
+        for (pf, pg_, ph), ij, ln in ((pk["agg_kk"], False, None), (pk["agg_ij"], True, ln0)):
             # unique(key) + CSR on the device (no host sync); G stays on the device
-            if key is None:
+            if not ij:
                 gid, offs, perm, G = kk_groups
+            elif ij_groups is not None:   # (the caller's window key: ii * 12345 + jj is not formed)
+                gid, offs, perm, G = ij_groups
             else:
-                gid, offs, perm, G = ij_groups if ij_groups is not None else U.group_by(key, key_bits=ij_bits)
+                gid, offs, perm, G = U.group_by(ii * 12345 + jj, key_bits=ij_bits)
             f16, g16 = U.rowgemm_pair(n16, *pf, *pg_)
             # frame-pair groups are few and long (~190 edges at C3): split over waves
-            y = U.softagg_csr(f16, g16, offs, perm, G, E, long_groups=key is not None)
+            y = U.softagg_csr(f16, g16, offs, perm, G, E, long_groups=ij)
             _, hy, _ = U.rowgemm(y, *ph, M_dev=G)
             if kk_add is None:
                 # net + agg_kk(net): only its fp16 rows (agg_ij's GEMM operand) are

@@ -202,10 +202,12 @@ def window_keys(ii, jj, kk, M, base, ring, frames, flag=None):
     return out[0], out[1], out[2], out[3]
 
 
-def window_group_by(ii, jj, kk, M, base, ring, frames, flag=None):
+def window_group_by(ii, jj, kk, M, base, ring, frames, flag=None, jj_order=False):
     """window_keys + group_by(key_kk, key_bits_for(64 M)) + group_by(key_ij, 12)
     in one memset and four launches (dpvo_window_group_by; same outputs):
-    -> (ctx, jslot, kk_groups, ij_groups), each groups tuple as group_by's."""
+    -> (ctx, jslot, kk_groups, ij_groups[, order]), each groups tuple as
+    group_by's; jj_order: also the edges grouped by target frame (int32 [E],
+    altcorr's visiting order, what cuda_corr.edge_order gives by ring slot)."""
     H.on_gpu(ii, jj, kk)
     ii, jj, kk = H.idx64(ii), H.idx64(jj), H.idx64(kk)
     E = kk.numel()
@@ -222,11 +224,13 @@ def window_group_by(ii, jj, kk, M, base, ring, frames, flag=None):
     perm = torch.empty(2, max(E, 1), dtype=torch.int32, device=dev)
     groups = torch.empty(2, 1, dtype=torch.int64, device=dev)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    order = torch.empty(max(E, 1), dtype=torch.int32, device=dev) if jj_order else None
     H.check(H.lib().dpvo_window_group_by(
         H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(M), int(base), int(ring), int(frames), bits, H.ptr(slots[0]),
         H.ptr(slots[1]), H.ptr(flag), H.ptr(gid[0]), H.ptr(offs[0]), H.ptr(perm[0]), H.ptr(groups[0]), H.ptr(gid[1]),
-        H.ptr(offs[1]), H.ptr(perm[1]), H.ptr(groups[1]), H.ptr(ws), nbytes, H.stream_of(kk)))
-    return (slots[0], slots[1], (gid[0], offs[0], perm[0], groups[0]), (gid[1], offs[1], perm[1], groups[1]))
+        H.ptr(offs[1]), H.ptr(perm[1]), H.ptr(groups[1]), H.ptr(order), H.ptr(ws), nbytes, H.stream_of(kk)))
+    out = (slots[0], slots[1], (gid[0], offs[0], perm[0], groups[0]), (gid[1], offs[1], perm[1], groups[1]))
+    return out + (order[:E],) if jj_order else out
 
 
 def append_edges(ii, jj, kk, ix, n, M, r):
