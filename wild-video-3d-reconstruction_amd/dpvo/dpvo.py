@@ -484,7 +484,7 @@ class DPVO:
         # :609), the deferred BA status of the update()s since the last one,
         # the pose-NaN check of the keep path (:647, its own read there) and
         # the compaction sizes
-        sums = torch.stack([old_keep.sum(), old_d.sum(), rm_d.sum()]).double()
+        sums = torch.stack([old_keep, old_d, rm_d]).sum(dim=1).double()   # one reduction launch
         vals = torch.cat([self._motionmag_dev(i, j).double(), self._ba_fail.double(),
                           torch.isnan(self.pg.poses_[k]).any().double()[None], sums])
         host = getattr(self, "_kf_host", None)
