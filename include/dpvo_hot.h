@@ -546,6 +546,45 @@ int dpvo_encoder_conv(int ks, int stride, int cin, int cout, int xmode, int Hi, 
 int dpvo_encoder_head_at(const dpvo_conv_args* e, int cout, int Hi, int Wi, const int64_t* x, const int64_t* y,
                          int64_t M, void* stream);
 
+/* The Patchifier's gathers at the M patch centres (x[m], y[m]) on the stride-4
+ * map, one launch (net.py:301-315: four altcorr.patchify calls and the
+ * coordinate grid, ~80 torch launches in the reference's composition):
+ *   gmap    fp32 [M][128][3][3] = patchify(fmap, c, 1)
+ *   imap    fp32 [M][dim]       = imap_at (fp16 [M][dim], head_at's rows)
+ *   patches fp32 [M][3][3][3]   = patchify((x, y, 1) grid of the h x w map, c, 1)
+ *   clr     fp32 [M][3]         = patchify(lut[image], 4 (c + 0.5), 0), or NULL
+ * c = (float)(x, y).  patchify: the (2r+2)^2 window at floor(c) - r, zero
+ * outside the map (correlation_kernel.cu:288-308), reduced bilinearly with
+ * frac(c) in the order of correlation.py:51-69, fp32, no contraction.
+ * fmap fp16 with element strides (channel, row, col); image uint8 [3][H][W];
+ * lut: 256 floats, lut[v] = the frame normalisation 2 (v / 255) - 0.5 as the
+ * caller computes it (net.py:116). */
+int dpvo_patch_gather(const void* fmap, const int64_t* fmap_strides, int h, int w, const void* imap_at, int dim,
+                      const uint8_t* image, int H, int W, const float* lut, const int64_t* x, const int64_t* y,
+                      int64_t M, float* gmap, float* imap, float* patches, float* clr, void* stream);
+
+/* keyframe() (dpvo.py:605-658): both outcomes' edge state before the decision,
+ * and the decision's one host read.  For edge e, k the candidate frame:
+ *   masks[0][e] = ix[kk] < n - RW (keep: edges retired, :654-658)
+ *   masks[1][e] = ix[kk_d] < n - 1 - RW && !drop (drop: retired after the shift)
+ *   masks[2][e] = masks[1][e] || drop,  drop = ii == k || jj == k (:616-617)
+ *   idx[0..2][e] = ii_d, jj_d, kk_d: ii - (ii > k), jj - (jj > k), kk - M (ii > k)
+ * masks uint8 [3][E], idx int64 [3][E]; vals double [7] = mm[0], mm[1] (the
+ * motion magnitudes, dpvo_motion_mag_ws), ba_fail[0], any(isnan(pose_k[0..7))),
+ * and the three masks' counts.  kk outside [0, ix_len) counts as not old. */
+size_t dpvo_keyframe_masks_workspace_bytes(int64_t num_edges);
+int dpvo_keyframe_masks(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t num_edges,
+                        const int64_t* ix, int64_t ix_len, int64_t k, int64_t M, int64_t n, int64_t RW,
+                        const float* mm, const int* ba_fail, const float* pose_k, uint8_t* masks, int64_t* idx,
+                        double* vals, void* workspace, size_t workspace_bytes, void* stream);
+
+/* A keyframe drop's shift of frames k+1 .. n-1 down by one slot (dpvo.py:626-639)
+ * in up to 16 per-frame buffers at once: buffer i holds frame f in slot
+ * (rings[i] ? f % rings[i] : f) of slot_bytes[i] bytes at bases[i].  The same
+ * result as moving the frames one after another, in ascending order. */
+int dpvo_frame_shift(void* const* bases, const int64_t* slot_bytes, const int64_t* rings, int nseg, int64_t k,
+                     int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

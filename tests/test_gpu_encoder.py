@@ -151,3 +151,34 @@ def test_patchifier_float_frames_take_the_torch_encoders():
             assert a[0].shape == b[0].shape and torch.isfinite(a[0]).all()
             d = (a[0].float() - b[0].float()).abs().max().item()
             assert d <= 2e-2 * b[0].float().abs().max().item()
+
+
+@pytest.mark.parametrize("size", SIZES)
+def test_patch_gather_matches_torch_gathers(size):
+    """dpvo_patch_gather (one launch) against the Patchifier's torch
+    composition of the four altcorr.patchify gathers + coordinate grid
+    (net.py:301-315), bit for bit -- centres inside, on and past the map
+    border (windows partly or wholly outside: zeros)."""
+    import encoder_ops
+    H, W = size
+    pf = _nets()
+    img = _image(H, W, "noise")
+    enc = encoder_ops.NativeEncoders(pf.fnet, pf.inet)
+    g = torch.Generator().manual_seed(7)
+    with torch.no_grad(), torch.autocast("cuda", enabled=True):
+        fmap, _ = enc.run(img, torch.zeros(1, dtype=torch.long, device="cuda"),
+                          torch.zeros(1, dtype=torch.long, device="cuda"))
+        h, w = fmap.shape[-2:]
+        xs = torch.cat([torch.randint(1, w - 1, (90,), generator=g), torch.tensor([0, w - 1, -1, w, 0, w - 1])])
+        ys = torch.cat([torch.randint(1, h - 1, (90,), generator=g), torch.tensor([0, h - 1, 0, h - 1, -1, h])])
+        xs, ys = xs.cuda(), ys.cuda()
+        fmap, imap = enc.run(img, xs, ys)
+        got = enc.gather(img, fmap, imap, xs, ys, return_color=True)
+        images = 2 * (img[None, None] / 255.0) - 0.5
+        ref = pf._gather(images, fmap, None, xs[None], ys[None], None, True, imap_at=imap)
+        nocl = enc.gather(img, fmap, imap, xs, ys, return_color=False)
+    torch.cuda.synchronize()
+    for name, a, b in zip(("gmap", "imap", "patches", "clr"), got, ref):
+        assert a.shape == b.shape and a.dtype == b.dtype, name
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), name
+    assert nocl[3] is None and all(torch.equal(a, b) for a, b in zip(nocl[:3], got[:3]))

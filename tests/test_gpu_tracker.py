@@ -172,6 +172,14 @@ def test_keyframe_matches_reference_loop(drop):
     for name in ("imap_", "gmap_", "fmap1_", "fmap2_", "image_buffer_"):
         assert torch.equal(getattr(a, name), getattr(b, name)), name
     assert a.pg.delta.keys() == b.pg.delta.keys()
+    # the next update() reads the shifted rings (the packed gmap table is
+    # rebuilt after the native shift, as after the reference's index writes)
+    with torch.no_grad():
+        a.update()
+        b.update()
+    for name in ("poses_", "patches_"):
+        assert torch.equal(getattr(a.pg, name), getattr(b.pg, name)), name
+    assert torch.equal(a.pg.net, b.pg.net)
 
 
 def test_keyframe_raises_on_nan_pose_when_kept():
@@ -452,3 +460,46 @@ def test_window_keys_flag_out_of_window_edges():
     assert int(flag.item()) == 7
     with pytest.raises(RuntimeError, match="key window"):
         cuda_ba.raise_for_status(-2)
+
+
+def test_keyframe_masks_and_frame_shift_edges():
+    """dpvo_keyframe_masks against the torch expressions it replaces (masks,
+    shifted indices, counts, NaN flag), and dpvo_frame_shift against the
+    sequential per-frame move on rings that wrap, odd slot sizes included."""
+    from dpvo import projective_ops as pops
+    g = torch.Generator().manual_seed(3)
+    E, M, n, RW, k = 5000, 8, 40, 6, 36
+    ix = torch.arange(n + 4, device="cuda").repeat_interleave(M)
+    ii = torch.randint(n - 20, n, (E,), generator=g).cuda()
+    kk = ii * M + torch.randint(0, M, (E,), generator=g).cuda()
+    jj = torch.randint(n - 20, n, (E,), generator=g).cuda()
+    mm = torch.tensor([0.25, float("nan")], device="cuda")
+    fail = torch.tensor([-3], dtype=torch.int32, device="cuda")
+    pose = torch.tensor([0, 0, float("nan"), 0, 0, 0, 1], device="cuda")
+    masks, idx, vals = pops.keyframe_masks(ii, jj, kk, ix, k, M, n, RW, mm, fail, pose)
+    old_keep = ix[kk] < n - RW
+    drop = (ii == k) | (jj == k)
+    later = ii > k
+    kk_d = torch.where(later, kk - M, kk)
+    old_d = (ix[kk_d] < n - 1 - RW) & ~drop
+    rm_d = old_d | drop
+    assert torch.equal(masks, torch.stack([old_keep, old_d, rm_d]))
+    assert torch.equal(idx, torch.stack([torch.where(later, ii - 1, ii), torch.where(jj > k, jj - 1, jj), kk_d]))
+    v = vals.cpu().tolist()
+    assert v[0] == 0.25 and np.isnan(v[1]) and v[2] == -3.0 and v[3] == 1.0
+    assert v[4:] == [float(old_keep.sum()), float(old_d.sum()), float(rm_d.sum())]
+    # frame shift: a wrapping ring, a plain buffer with 28-byte slots, a byte buffer
+    ring = torch.randn(6, 5, 4, device="cuda")
+    plain = torch.randn(20, 7, device="cuda")
+    raw = torch.randint(0, 255, (20, 3), dtype=torch.uint8, device="cuda")
+    refs = [t.clone() for t in (ring, plain, raw)]
+    k, n = 9, 14
+    for f in range(k, n - 1):
+        refs[0][f % 6] = refs[0][(f + 1) % 6]
+        refs[1][f] = refs[1][f + 1]
+        refs[2][f] = refs[2][f + 1]
+    v0 = ring._version
+    pops.frame_shift([(ring, 0, 6), (plain, 0, 0), (raw, 0, 0)], k, n)
+    assert ring._version > v0
+    for a, b in zip((ring, plain, raw), refs):
+        assert torch.equal(a, b)

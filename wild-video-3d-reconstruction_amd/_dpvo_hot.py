@@ -92,6 +92,12 @@ _SIGNATURES = {
     "dpvo_encoder_stem": (_ip, [_vp, _ip, _ip, _vp, _ip, _vp]),
     "dpvo_encoder_conv": (_ip, [_ip] * 7 + [_vp, _ip, _vp]),
     "dpvo_encoder_head_at": (_ip, [_vp, _ip, _ip, _ip, _vp, _vp, _i64, _vp]),
+    "dpvo_keyframe_masks_workspace_bytes": (_sz, [_i64]),
+    "dpvo_keyframe_masks": (_ip, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _vp, _sz, _vp]),
+    "dpvo_frame_shift": (_ip, [_vp, _vp, _vp, _ip, _i64, _i64, _vp]),
+    "dpvo_patch_gather": (_ip, [_vp, _vp, _ip, _ip, _vp, _ip, _vp, _ip, _ip, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
+                                _vp, _vp]),
 }
 EXPORTED = tuple(_SIGNATURES)
 

@@ -448,6 +448,96 @@ int fill_batch(EncBatch& b, const dpvo_conv_args* enc, int n_enc, int Hi, int Wi
     return 0;
 }
 
+
+// The Patchifier's gathers at the M patch centres (net.py:301-315), one
+// workgroup per patch, in one launch instead of ~80 torch launches:
+//   gmap    = patchify(fmap, c, 1)            [M][128][3][3]
+//   imap    = inet at c (head_at's rows)      [M][dim]
+//   patches = patchify(grid(x, y, 1), c, 1)   [M][3][3][3]
+//   clr     = patchify(image', 4 (c + 0.5), 0) [M][3], image' = lut[u8]
+// Each patchify gathers the (2r+2)^2 window at floor(c) - r (zero outside
+// the map, correlation_kernel.cu:288-308) and reduces it bilinearly with
+// frac(c) as correlation.py:51-69 does -- ((w00 p00 + w01 p01) + w10 p10) +
+// w11 p11, w00 = (1-dy)(1-dx), w01 = (1-dy) dx, w10 = dy (1-dx), w11 = dy dx --
+// in fp32 with every product and sum rounded on its own (the torch
+// composition's separate kernels: bit-identical).
+struct PgWin {
+    float w00, w01, w10, w11;
+    int x0, y0;   // floor(c)
+};
+
+__device__ __forceinline__ PgWin pg_window(float cx, float cy)
+{
+    const float dx = __fsub_rn(cx, floorf(cx)), dy = __fsub_rn(cy, floorf(cy));
+    const float ux = __fsub_rn(1.f, dx), uy = __fsub_rn(1.f, dy);
+    return {__fmul_rn(uy, ux), __fmul_rn(uy, dx), __fmul_rn(dy, ux), __fmul_rn(dy, dx), floor_to_int_sat(cx),
+            floor_to_int_sat(cy)};
+}
+
+__device__ __forceinline__ float pg_bilinear(const PgWin& w, float p00, float p01, float p10, float p11)
+{
+    return __fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(w.w00, p00), __fmul_rn(w.w01, p01)), __fmul_rn(w.w10, p10)),
+                     __fmul_rn(w.w11, p11));
+}
+
+struct PgArgs {
+    const half_t* fmap; int64_t f_sc, f_sy, f_sx; int h, w;
+    const half_t* imap_at; int dim;
+    const uint8_t* image; int H, W; const float* lut;
+    const int64_t* xs; const int64_t* ys;
+    float* gmap; float* imap; float* patches; float* clr;
+};
+
+__global__ __launch_bounds__(256) void patch_gather_kernel(PgArgs a, int64_t M)
+{
+    const int64_t m = blockIdx.x;
+    if (m >= M) return;
+    const int tid = threadIdx.x;
+    const float cx = (float)a.xs[m], cy = (float)a.ys[m];
+    const PgWin g = pg_window(cx, cy);
+    // gmap: channel fastest, so a wave reads whole pixel rows of the NHWC map
+    for (int idx = tid; idx < 9 * 128; idx += 256) {
+        const int c = idx & 127, ab = idx >> 7, ia = ab / 3, ib = ab - 3 * ia;
+        float p[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                const int i = wrap_add(g.y0, ia + u - 1), j = wrap_add(g.x0, ib + v - 1);
+                p[u][v] = (i >= 0 && i < a.h && j >= 0 && j < a.w)
+                              ? (float)a.fmap[c * a.f_sc + (int64_t)i * a.f_sy + (int64_t)j * a.f_sx] : 0.f;
+            }
+        a.gmap[m * 1152 + c * 9 + ab] = pg_bilinear(g, p[0][0], p[0][1], p[1][0], p[1][1]);
+    }
+    for (int k = tid; k < a.dim; k += 256) a.imap[m * a.dim + k] = (float)a.imap_at[m * a.dim + k];
+    if (tid < 27) {   // the (x, y, 1) grid of the stride-4 map
+        const int ch = tid / 9, ab = tid - 9 * ch, ia = ab / 3, ib = ab - 3 * ia;
+        float p[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                const int i = wrap_add(g.y0, ia + u - 1), j = wrap_add(g.x0, ib + v - 1);
+                const bool in = i >= 0 && i < a.h && j >= 0 && j < a.w;
+                p[u][v] = !in ? 0.f : ch == 0 ? (float)j : ch == 1 ? (float)i : 1.f;
+            }
+        a.patches[m * 27 + tid] = pg_bilinear(g, p[0][0], p[0][1], p[1][0], p[1][1]);
+    } else if (a.clr && tid >= 64 && tid < 67) {   // colour at 4 (c + 0.5) of the full frame
+        const int ch = tid - 64;
+        const PgWin q = pg_window(__fmul_rn(4.f, __fadd_rn(cx, 0.5f)), __fmul_rn(4.f, __fadd_rn(cy, 0.5f)));
+        float p[2][2];
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                const int i = wrap_add(q.y0, u), j = wrap_add(q.x0, v);
+                p[u][v] = (i >= 0 && i < a.H && j >= 0 && j < a.W)
+                              ? a.lut[a.image[((int64_t)ch * a.H + i) * a.W + j]] : 0.f;
+            }
+        a.clr[m * 3 + ch] = pg_bilinear(q, p[0][0], p[0][1], p[1][0], p[1][1]);
+    }
+}
+
 }  // namespace
 }  // namespace dpvo
 
@@ -512,6 +602,22 @@ extern "C" int dpvo_encoder_head_at(const dpvo_conv_args* e, int cout, int Hi, i
     if (M == 0) return 0;
     hipLaunchKernelGGL(enc_head_at_kernel, dim3((unsigned)M), dim3(EN_THREADS), 0, as_stream(stream), *e, cout, Hi, Wi,
                        x, y, M);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_patch_gather(const void* fmap, const int64_t* fmap_strides, int h, int w, const void* imap_at,
+                                 int dim, const uint8_t* image, int H, int W, const float* lut, const int64_t* x,
+                                 const int64_t* y, int64_t M, float* gmap, float* imap, float* patches, float* clr,
+                                 void* stream)
+{
+    DPVO_CHECK_ARG(fmap && fmap_strides && imap_at && x && y && gmap && imap && patches, "null pointer");
+    DPVO_CHECK_ARG(M >= 0 && h > 0 && w > 0 && dim >= 0, "M >= 0, a non-empty map and dim >= 0 are required");
+    DPVO_CHECK_ARG(!clr || (image && lut && H > 0 && W > 0), "clr needs image, lut and the frame size");
+    if (M == 0) return 0;
+    PgArgs a{(const half_t*)fmap, fmap_strides[0], fmap_strides[1], fmap_strides[2], h, w,
+             (const half_t*)imap_at, dim, image, H, W, lut, x, y, gmap, imap, patches, clr};
+    hipLaunchKernelGGL(patch_gather_kernel, dim3((unsigned)M), dim3(256), 0, as_stream(stream), a, M);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

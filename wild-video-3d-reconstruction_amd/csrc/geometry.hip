@@ -306,6 +306,115 @@ __global__ __launch_bounds__(KF_THREADS) void keyframe_flow_kernel(const float* 
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// keyframe() device work (dpvo.py:605-658), both outcomes before the decision.
+// Per edge e (patch kk from frame ii, target jj), k the candidate frame:
+//   old_keep = ix[kk] < n - RW                        (keep: :654-658)
+//   drop     = ii == k || jj == k                     (drop: :616-617)
+//   kk_d = ii > k ? kk - M : kk,  ii_d = ii > k ? ii - 1 : ii,  jj_d = jj > k ? jj - 1 : jj
+//   old_d    = ix[kk_d] < n - 1 - RW && !drop         (retirement after the drop)
+//   rm_d     = old_d || drop
+// masks u8 [3][E] (old_keep, old_d, rm_d), idx [3][E] (ii_d, jj_d, kk_d),
+// part[b][4]: block b's counts of the three masks.  kk outside [0, ix_len)
+// reads no index and counts as not old.
+constexpr int KM_THREADS = 256, KM_MAXBLK = 512;
+
+__global__ __launch_bounds__(KM_THREADS) void kf_masks_kernel(const int64_t* ii, const int64_t* jj,
+                                                              const int64_t* kk, const int64_t* ix, int64_t ix_len,
+                                                              int64_t E, int64_t k, int64_t M, int64_t n, int64_t RW,
+                                                              uint8_t* masks, int64_t* idx, int* part)
+{
+    __shared__ int red[3][KM_THREADS / 64];
+    int c0 = 0, c1 = 0, c2 = 0;
+    for (int64_t e = blockIdx.x * (int64_t)KM_THREADS + threadIdx.x; e < E; e += (int64_t)gridDim.x * KM_THREADS) {
+        const int64_t a = ii[e], b = jj[e], p = kk[e];
+        const bool later = a > k, drop = a == k || b == k;
+        const int64_t pd = later ? p - M : p;
+        const bool keep_old = p >= 0 && p < ix_len && ix[p] < n - RW;
+        const bool old_d = !drop && pd >= 0 && pd < ix_len && ix[pd] < n - 1 - RW;
+        const bool rm_d = old_d || drop;
+        masks[e] = keep_old;
+        masks[E + e] = old_d;
+        masks[2 * E + e] = rm_d;
+        idx[e] = later ? a - 1 : a;
+        idx[E + e] = b > k ? b - 1 : b;
+        idx[2 * E + e] = pd;
+        c0 += keep_old;
+        c1 += old_d;
+        c2 += rm_d;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        c0 += __shfl_xor(c0, o);
+        c1 += __shfl_xor(c1, o);
+        c2 += __shfl_xor(c2, o);
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) { red[0][wv] = c0; red[1][wv] = c1; red[2][wv] = c2; }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        int t = 0;
+        for (int w = 0; w < KM_THREADS / 64; w++) t += red[threadIdx.x][w];
+        part[blockIdx.x * 4 + threadIdx.x] = t;
+    }
+}
+
+// vals = [mm[0], mm[1], ba_fail, any(isnan(pose_k)), n_old_keep, n_old_d, n_rm_d]
+// as doubles: keyframe()'s one host read (dpvo.py:609, :647, the compaction sizes)
+__global__ __launch_bounds__(64) void kf_pack_kernel(const int* part, int nblk, const float* mm,
+                                                     const int* ba_fail, const float* pose_k, double* vals)
+{
+    const int t = threadIdx.x;
+    long long c[3] = {0, 0, 0};
+    for (int b = t; b < nblk; b += 64)
+        for (int q = 0; q < 3; q++) c[q] += part[b * 4 + q];
+    for (int o = 32; o > 0; o >>= 1)
+        for (int q = 0; q < 3; q++) c[q] += __shfl_xor(c[q], o);
+    if (t == 0) {
+        bool nan = false;
+        for (int q = 0; q < 7; q++) nan = nan || isnan(pose_k[q]);
+        vals[0] = (double)mm[0];
+        vals[1] = (double)mm[1];
+        vals[2] = (double)ba_fail[0];
+        vals[3] = nan ? 1.0 : 0.0;
+        vals[4] = (double)c[0];
+        vals[5] = (double)c[1];
+        vals[6] = (double)c[2];
+    }
+}
+
+// A keyframe drop moves frames k+1 .. n-1 down by one slot in every per-frame
+// buffer (dpvo.py:626-639).  Segment s: slots of slot_bytes at base, frame f
+// in slot f % ring (ring 0: slot f).  Each thread owns one word offset of every
+// slot and walks the frames upwards, so it reads slot f+1 before it writes it:
+// the same result as the reference's loop, in one launch for all buffers.
+struct FsSeg {
+    char* base;
+    int64_t slot_bytes, ring;
+    int unit;   // 16, 4 or 1 bytes per word
+};
+constexpr int FS_MAXSEG = 16;
+struct FsArgs {
+    FsSeg seg[FS_MAXSEG];
+    int nseg;
+};
+
+__global__ __launch_bounds__(256) void frame_shift_kernel(FsArgs a, int64_t k, int64_t n)
+{
+    const FsSeg s = a.seg[blockIdx.y];
+    const int64_t words = s.slot_bytes / s.unit;
+    for (int64_t w = blockIdx.x * 256ll + threadIdx.x; w < words; w += (int64_t)gridDim.x * 256) {
+        for (int64_t f = k; f + 1 < n; f++) {
+            const int64_t d = s.ring ? f % s.ring : f, r = s.ring ? (f + 1) % s.ring : f + 1;
+            char* dst = s.base + d * s.slot_bytes + w * s.unit;
+            const char* src = s.base + r * s.slot_bytes + w * s.unit;
+            if (s.unit == 16) *(uint4*)dst = *(const uint4*)src;
+            else if (s.unit == 4) *(uint32_t*)dst = *(const uint32_t*)src;
+            else *dst = *src;
+        }
+    }
+}
+
 }  // namespace dpvo
 
 using namespace dpvo;
@@ -397,6 +506,57 @@ extern "C" int dpvo_motion_mag_ws(const float* poses, const float* patches, int 
                            patches, P, intrinsics, ii, jj, kk, num_edges, i, j, beta, (float*)workspace);
     hipLaunchKernelGGL(motion_mag_final_kernel, dim3(1), dim3(MM2_THREADS), 0, as_stream(stream),
                        (const float*)workspace, nblk, (int64_t)P * P, out);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" size_t dpvo_keyframe_masks_workspace_bytes(int64_t num_edges)
+{
+    (void)num_edges;
+    return (size_t)KM_MAXBLK * 4 * sizeof(int);
+}
+
+extern "C" int dpvo_keyframe_masks(const int64_t* ii, const int64_t* jj, const int64_t* kk, int64_t num_edges,
+                                   const int64_t* ix, int64_t ix_len, int64_t k, int64_t M, int64_t n, int64_t RW,
+                                   const float* mm, const int* ba_fail, const float* pose_k, uint8_t* masks,
+                                   int64_t* idx, double* vals, void* workspace, size_t workspace_bytes, void* stream)
+{
+    DPVO_CHECK_ARG(num_edges >= 0 && ix_len >= 0, "negative size");
+    DPVO_CHECK_ARG(mm && ba_fail && pose_k && vals, "null operand");
+    DPVO_CHECK_ARG(num_edges == 0 || (ii && jj && kk && ix && masks && idx), "null operand");
+    DPVO_CHECK_ARG(workspace && workspace_bytes >= dpvo_keyframe_masks_workspace_bytes(num_edges),
+                   "workspace too small");
+    const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>((num_edges + KM_THREADS - 1) / KM_THREADS,
+                                                                  KM_MAXBLK));
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(kf_masks_kernel, dim3(nblk), dim3(KM_THREADS), 0, st, ii, jj, kk, ix, ix_len, num_edges, k, M,
+                       n, RW, masks, idx, (int*)workspace);
+    hipLaunchKernelGGL(kf_pack_kernel, dim3(1), dim3(64), 0, st, (const int*)workspace, nblk, mm, ba_fail, pose_k,
+                       vals);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_frame_shift(void* const* bases, const int64_t* slot_bytes, const int64_t* rings, int nseg,
+                                int64_t k, int64_t n, void* stream)
+{
+    DPVO_CHECK_ARG(nseg >= 0 && nseg <= FS_MAXSEG, "at most 16 buffers");
+    DPVO_CHECK_ARG(nseg == 0 || (bases && slot_bytes && rings), "null operand");
+    if (nseg == 0 || n - 1 <= k) return 0;
+    DPVO_CHECK_ARG(k >= 0, "k must be >= 0");
+    FsArgs a{};
+    a.nseg = nseg;
+    int64_t most = 0;
+    for (int i = 0; i < nseg; i++) {
+        DPVO_CHECK_ARG(bases[i] && slot_bytes[i] > 0 && rings[i] >= 0, "bad buffer");
+        DPVO_CHECK_ARG(rings[i] == 0 || n - k <= rings[i], "the moved frames must fit in the ring");
+        const uintptr_t b = (uintptr_t)bases[i];
+        const int unit = (b % 16 == 0 && slot_bytes[i] % 16 == 0) ? 16 : (b % 4 == 0 && slot_bytes[i] % 4 == 0) ? 4 : 1;
+        a.seg[i] = {(char*)bases[i], slot_bytes[i], rings[i], unit};
+        most = std::max<int64_t>(most, slot_bytes[i] / unit);
+    }
+    const unsigned gx = (unsigned)std::min<int64_t>((most + 255) / 256, 2048);
+    hipLaunchKernelGGL(frame_shift_kernel, dim3(gx, nseg), dim3(256), 0, as_stream(stream), a, k, n);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

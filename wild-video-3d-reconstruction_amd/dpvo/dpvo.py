@@ -257,16 +257,60 @@ class DPVO:
             index = lambda mask, size: torch.nonzero_static(mask, size=size).squeeze(1)
         if store is not False:
             rem = index(m if store is True else store, counts[1])
-            self.pg.ii_inac = torch.cat((self.pg.ii_inac, self.pg.ii[rem]))
-            self.pg.jj_inac = torch.cat((self.pg.jj_inac, self.pg.jj[rem]))
-            self.pg.kk_inac = torch.cat((self.pg.kk_inac, self.pg.kk[rem]))
-            self.pg.weight_inac = torch.cat((self.pg.weight_inac, self.pg.weight[:, rem]), dim=1)
-            self.pg.target_inac = torch.cat((self.pg.target_inac, self.pg.target[:, rem]), dim=1)
+            for name, src, dim in (("ii_inac", self.pg.ii, 0), ("jj_inac", self.pg.jj, 0), ("kk_inac", self.pg.kk, 0),
+                                   ("weight_inac", self.pg.weight, 1), ("target_inac", self.pg.target, 1)):
+                self._append_inactive(name, src, rem, dim)
         keep = index(~m, counts[0])
         self.pg.weight = self.pg.weight[:, keep]
         self.pg.target = self.pg.target[:, keep]
         self.pg.ii, self.pg.jj, self.pg.kk = self.pg.ii[keep], self.pg.jj[keep], self.pg.kk[keep]
-        self.pg.net = self.pg.net[:, keep]
+        # the kept rows of the edge state go to the front of a buffer with room
+        # for the next frame's edges: its append then zeroes the new rows in
+        # place instead of concatenating the whole state (146 MB at C3)
+        net = self.pg.net
+        n_keep = keep.numel()
+        cap = net.new_empty(1, n_keep + self._edge_slack(), net.shape[2])
+        torch.index_select(net, 1, keep, out=cap[:, :n_keep])
+        self._net_cap = cap
+        self.pg.net = cap[:, :n_keep]
+
+    def _append_inactive(self, name, src, rem, dim):
+        """pg.<name> = cat(pg.<name>, src[rem]) along dim (dpvo.py:353-357), the
+        rows gathered straight into a buffer that doubles when full: the
+        inactive lists grow every frame, and re-concatenating them would copy
+        all of them each time"""
+        cur = getattr(self.pg, name)
+        if cur.dtype != src.dtype:   # torch.cat's type promotion
+            setattr(self.pg, name, torch.cat((cur, src.index_select(dim, rem)), dim=dim))
+            return
+        n0, add = cur.shape[dim], rem.numel()
+        caps = self.__dict__.setdefault("_inac_caps", {})
+        cap = caps.get(name)
+        if cap is None or cur.data_ptr() != cap.data_ptr() or cap.shape[dim] < n0 + add or not cur.is_contiguous():
+            size = list(src.shape)
+            size[dim] = max(2 * (n0 + add), 4096)
+            cap = src.new_empty(size)
+            cap.narrow(dim, 0, n0).copy_(cur)
+            caps[name] = cap
+        torch.index_select(src, dim, rem, out=cap.narrow(dim, n0, add))
+        setattr(self.pg, name, cap.narrow(dim, 0, n0 + add))
+
+    def _edge_slack(self):
+        """rows one frame's append adds at most: forward and backward edges
+        of PATCH_LIFETIME frames (dpvo.py:756-769)"""
+        return 2 * self.M * (self.cfg.PATCH_LIFETIME + 1)
+
+    def _append_net_rows(self, E0, E1):
+        """pg.net grown from E0 to E1 rows of zeros (dpvo.py:341-347): in place
+        when the compaction left room behind it, else one concatenation"""
+        cap = getattr(self, "_net_cap", None)
+        net = self.pg.net
+        if (cap is not None and net.data_ptr() == cap.data_ptr() and net.shape[1] == E0 and E1 <= cap.shape[1]
+                and net.dim() == 3 and net.is_contiguous()):
+            self.pg.net = cap[:, :E1]
+            self.pg.net[:, E0:].zero_()
+        else:
+            self.pg.net = torch.cat([net, net.new_zeros(1, E1 - E0, self.DIM)], dim=1)
 
     def motion_probe(self):
         """median flow of a trial update on the newest frame (dpvo.py:366-381)."""
@@ -468,65 +512,49 @@ class DPVO:
         k = self.n - self.cfg.KEYFRAME_INDEX
         i, j = k - 1, k + 1
         RW = self.cfg.REMOVAL_WINDOW
-        ii, jj, kk = self.pg.ii, self.pg.jj, self.pg.kk
-        # the edge masks of both outcomes, formed before the decision: keep
+        # the edge state of both outcomes, formed before the decision: keep
         # (edges whose patch left the removal window, :654-658) and drop (the
-        # edges of frame k go, :616-617, and the retirement runs after the
-        # frames above k moved down by one); their sizes ride on the one host
-        # read, so the compaction needs no synchronisation of its own
-        old_keep = self.ix[kk] < self.n - RW
-        drop = (ii == k) | (jj == k)
-        later = ii > k
-        kk_d = torch.where(later, kk - self.M, kk)
-        old_d = (self.ix[kk_d] < self.n - 1 - RW) & ~drop
-        rm_d = old_d | drop
-        # one host read for both motion directions (the reference reads each,
-        # :609), the deferred BA status of the update()s since the last one,
-        # the pose-NaN check of the keep path (:647, its own read there) and
-        # the compaction sizes
-        sums = torch.stack([old_keep, old_d, rm_d]).sum(dim=1).double()   # one reduction launch
-        vals = torch.cat([self._motionmag_dev(i, j).double(), self._ba_fail.double(),
-                          torch.isnan(self.pg.poses_[k]).any().double()[None], sums])
+        # edges of frame k go, :616-617, the frames above k move down by one,
+        # then the retirement); with one host read for both motion directions
+        # (the reference reads each, :609), the deferred BA status of the
+        # update()s since the last one, the pose-NaN check of the keep path
+        # (:647, its own read there) and the compaction sizes -- so the
+        # compaction needs no synchronisation of its own.  Four launches.
+        mm = self._motionmag_dev(i, j)
+        masks, idx_d, vals = pops.keyframe_masks(self.pg.ii, self.pg.jj, self.pg.kk, self.ix, k, self.M, self.n, RW,
+                                                 mm, self._ba_fail, self.pg.poses_[k])
         host = getattr(self, "_kf_host", None)
         if host is None:
             host = self._kf_host = torch.empty(7, dtype=torch.float64, pin_memory=True)
         host.copy_(vals, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        return dict(k=k, E=kk.numel(), old_keep=old_keep, old_d=old_d, rm_d=rm_d, later=later, kk_d=kk_d,
+        return dict(k=k, E=self.pg.kk.numel(), old_keep=masks[0], old_d=masks[1], rm_d=masks[2], idx_d=idx_d,
                     thresh=self.cfg.KEYFRAME_THRESH, event=ev)
 
     def _keyframe_finish(self, pd):
         pd["event"].synchronize()
         vals = self._kf_host.tolist()
-        k, E, later, kk_d = pd["k"], pd["E"], pd["later"], pd["kk_d"]
-        ii, jj = self.pg.ii, self.pg.jj
+        k, E = pd["k"], pd["E"]
         self.check_ba(int(vals[2]))
         n_old_keep, n_old_d, n_rm_d = (int(v) for v in vals[4:7])
         m = vals[0] + vals[1]
         if m / 2 < pd["thresh"]:
             t0, t1 = self.pg.tstamps_[k - 1:k + 1].tolist()
             self.pg.delta[t1] = (t0, pops.pose_relative(self.pg.poses_[k], self.pg.poses_[k - 1]))
-            # x[x > k] -= 1 as selects: no mask-size synchronisation
-            self.pg.kk = kk_d
-            self.pg.ii = torch.where(later, ii - 1, ii)
-            self.pg.jj = torch.where(jj > k, jj - 1, jj)
-            # frames k+1 .. n-1 move down by one: one gather per buffer (the
-            # reference's per-frame loop, :626-639, reads each source before
-            # overwriting it, so a simultaneous shift is the same)
+            # x[x > k] -= 1, formed by keyframe_masks: no mask-size synchronisation
+            self.pg.ii, self.pg.jj, self.pg.kk = pd["idx_d"].unbind(0)
+            # frames k+1 .. n-1 move down by one in every per-frame buffer, one
+            # launch (the reference's per-frame loop, :626-639, reads each
+            # source before overwriting it, as the kernel's ascending walk does)
             n = self.n
             if n - 1 > k:
                 self.pg.tstamps_[k:n - 1] = self.pg.tstamps_[k + 1:n].copy()
-                for buf in (self.pg.colors_, self.pg.poses_, self.pg.patches_, self.pg.patches_est_,
-                            self.pg.intrinsics_):
-                    buf[k:n - 1] = buf[k + 1:n].clone()
-                dst = torch.arange(k, n - 1, device=self.device)
-                src = dst + 1
-                for ring, size in ((self.imap_, self.pmem), (self.gmap_, self.pmem)):
-                    ring[dst % size] = ring[src % size]
-                for ring in (self.fmap1_, self.fmap2_):
-                    ring[0, dst % self.pmem] = ring[0, src % self.pmem]
-                self.image_buffer_[dst % self.mem] = self.image_buffer_[src % self.mem]
+                bufs = [(b, 0, 0) for b in (self.pg.colors_, self.pg.poses_, self.pg.patches_, self.pg.patches_est_,
+                                            self.pg.intrinsics_)]
+                bufs += [(self.imap_, 0, self.pmem), (self.gmap_, 0, self.pmem), (self.fmap1_, 1, self.pmem),
+                         (self.fmap2_, 1, self.pmem), (self.image_buffer_, 0, self.mem)]
+                pops.frame_shift(bufs, k, n)
             self.n -= 1
             self.pg.m -= self.M
             self.keyframes_dropped = getattr(self, "keyframes_dropped", 0) + 1
@@ -691,7 +719,7 @@ class DPVO:
         E0 = self.pg.ii.numel()
         self.pg.ii, self.pg.jj, self.pg.kk = update_ops.append_edges(self.pg.ii, self.pg.jj, self.pg.kk, self.ix,
                                                                      self.n, self.M, self.cfg.PATCH_LIFETIME)
-        self.pg.net = torch.cat([self.pg.net, self.pg.net.new_zeros(1, self.pg.ii.numel() - E0, self.DIM)], dim=1)
+        self._append_net_rows(E0, self.pg.ii.numel())
         if self.n == self.warm_up and not self.is_initialized:
             self.is_initialized = True
             for _ in range(12):

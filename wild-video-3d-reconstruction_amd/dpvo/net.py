@@ -289,9 +289,13 @@ class Patchifier(nn.Module):
         the modules' own (the graph's fp16 copies), or "native": both networks
         on the HIP library (encoder_ops, 11 launches), inet only at the centres."""
         if encoders == "native":
-            images = 2 * (image[None, None] / 255.0) - 0.5 if return_color else None
-            fmap, imap_at = self._native_encoders().run(image, x, y)
-            gm, im, patches, clr = self._gather(images, fmap, None, x, y, None, return_color, imap_at=imap_at)
+            nat = self._native_encoders()
+            fmap, imap_at = nat.run(image, x, y)
+            if self.patch_size == 3:   # the four gathers in one launch (bit-identical to _gather)
+                gm, im, patches, clr = nat.gather(image, fmap, imap_at, x, y, return_color)
+            else:
+                images = 2 * (image[None, None] / 255.0) - 0.5 if return_color else None
+                gm, im, patches, clr = self._gather(images, fmap, None, x, y, None, return_color, imap_at=imap_at)
             return fmap, gm, im, patches, clr
         fnet, inet = encoders or (self.fnet, self.inet)
         images = 2 * (image[None, None] / 255.0) - 0.5

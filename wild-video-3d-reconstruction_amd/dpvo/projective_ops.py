@@ -100,6 +100,63 @@ def motion_mag_pair(poses, patches, intrinsics, ii, jj, kk, i, j, beta=0.5):
     return out
 
 
+def keyframe_masks(ii, jj, kk, ix, k, M, n, RW, mm, ba_fail, pose_k):
+    """keyframe()'s device work for both outcomes (dpvo.py:605-658) in two
+    launches: masks bool [3, E] (old_keep, old_d, rm_d), idx int64 [3, E]
+    (ii, jj, kk after the drop's shift) and vals float64 [7] (mm[0], mm[1],
+    ba_fail, any(isnan(pose_k)), the three masks' counts) -- see
+    dpvo_keyframe_masks in include/dpvo_hot.h."""
+    ii, jj, kk, ix = H.idx64(ii), H.idx64(jj), H.idx64(kk), H.idx64(ix)
+    H.on_gpu(ii, jj, kk, ix, mm, ba_fail, pose_k)
+    if mm.dtype != torch.float32 or ba_fail.dtype != torch.int32 or pose_k.dtype != torch.float32:
+        raise RuntimeError("keyframe_masks: mm / pose_k float32, ba_fail int32")
+    E, dev = ii.numel(), ii.device
+    masks = torch.empty(3, E, dtype=torch.bool, device=dev)
+    idx = torch.empty(3, E, dtype=torch.int64, device=dev)
+    vals = torch.empty(7, dtype=torch.float64, device=dev)
+    nb = H.lib().dpvo_keyframe_masks_workspace_bytes(E)
+    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    H.check(H.lib().dpvo_keyframe_masks(H.ptr(ii), H.ptr(jj), H.ptr(kk), E, H.ptr(ix), ix.numel(), int(k), int(M),
+                                        int(n), int(RW), H.ptr(mm.contiguous()), H.ptr(ba_fail),
+                                        H.ptr(pose_k.contiguous()), H.ptr(masks), H.ptr(idx), H.ptr(vals), H.ptr(ws),
+                                        nb, H.stream_of(ii)))
+    return masks, idx, vals
+
+
+def _dense(t):
+    """every element of t's storage span used exactly once (any dim order)"""
+    expect = 1
+    for stride, size in sorted((st, sz) for sz, st in zip(t.shape, t.stride()) if sz != 1):
+        if stride != expect:
+            return False
+        expect *= size
+    return True
+
+
+def frame_shift(buffers, k, n):
+    """Move frames k+1 .. n-1 of every buffer down by one slot in one launch
+    (a keyframe drop, dpvo.py:626-639).  buffers: (tensor, slot_dim, ring)
+    with frame f in slot (f % ring if ring else f) along slot_dim; each slot
+    must be one dense block of memory (the dim's stride = the slot's numel)."""
+    if n - 1 <= k or not buffers:
+        return
+    bases, sizes, rings = [], [], []
+    for t, d, ring in buffers:
+        H.on_gpu(t)
+        slot = t.select(d, 0)
+        if t.stride(d) != slot.numel() or any(t.shape[i] != 1 for i in range(d)) or not _dense(t):
+            raise RuntimeError("frame_shift: each slot must be one dense block")
+        bases.append(t.data_ptr())
+        sizes.append(t.stride(d) * t.element_size())
+        rings.append(int(ring or 0))
+    import ctypes
+    ns = len(bases)
+    H.check(H.lib().dpvo_frame_shift((ctypes.c_void_p * ns)(*bases), (ctypes.c_int64 * ns)(*sizes),
+                                     (ctypes.c_int64 * ns)(*rings), ns, int(k), int(n), H.stream_of(buffers[0][0])))
+    for t, _, _ in buffers:   # written in place: caches keyed on the version counter see it
+        torch.autograd.graph.increment_version(t)
+
+
 def keyframe_flow(poses, patches, intrinsics, n, M, beta=0.5):
     """[n, n] device matrix: dist[a, b] = mean flow_mag of frame a's M patches
     into frame b (projective_ops.py:111-121) -- every pair of

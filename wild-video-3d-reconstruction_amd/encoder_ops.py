@@ -218,3 +218,50 @@ class NativeEncoders:
         H.check(lib.dpvo_encoder_head_at(_ct.byref(g), pk[1].out_dim, H2, W2, _ptr(x), _ptr(y), M, st_))
         fmap = fmap.view(1, 1, H2, W2, 128).permute(0, 1, 4, 2, 3)
         return fmap, imap
+
+    def gather(self, image, fmap, imap, x, y, return_color=True):
+        """The Patchifier's gathers at the patch centres (net.py:301-315) in one
+        launch: fmap / imap as run() returns them, image the uint8 frame ->
+        gmap fp32 [1, M, 128, 3, 3], imap fp32 [1, M, DIM, 1, 1], patches fp32
+        [1, M, 3, 3, 3], clr fp32 [1, M, 3] (None unless return_color) --
+        bit-identical to DPVONet._gather's torch composition."""
+        H.on_gpu(image, fmap, imap, x, y)
+        if fmap.dtype != torch.float16 or fmap.dim() != 5 or fmap.shape[2] != 128:
+            raise RuntimeError("patch gather: fmap must be fp16 [1, 1, 128, h, w]")
+        if imap.dtype != torch.float16 or imap.dim() != 2:
+            raise RuntimeError("patch gather: imap must be fp16 [M, DIM]")
+        x, y = H.idx64(x.reshape(-1)), H.idx64(y.reshape(-1))
+        M, dim = x.numel(), imap.shape[1]
+        if y.numel() != M or imap.shape[0] != M:
+            raise RuntimeError("patch gather: x, y and imap must have M rows")
+        imap = imap.contiguous()
+        dev = fmap.device
+        h, w = fmap.shape[-2:]
+        f = fmap[0, 0]
+        strides = torch.tensor([f.stride(0), f.stride(1), f.stride(2)], dtype=torch.int64)
+        gm = torch.empty(1, M, 128, 3, 3, dtype=torch.float32, device=dev)
+        im = torch.empty(1, M, dim, 1, 1, dtype=torch.float32, device=dev)
+        pt = torch.empty(1, M, 3, 3, 3, dtype=torch.float32, device=dev)
+        clr = lut = img = None
+        Hh = Ww = 0
+        if return_color:
+            if image.dtype != torch.uint8 or image.dim() != 3 or image.shape[0] != 3:
+                raise RuntimeError("patch gather: image must be uint8 [3, H, W]")
+            img = image.contiguous()
+            Hh, Ww = img.shape[1:]
+            lut = self._lut(dev)
+            clr = torch.empty(1, M, 3, dtype=torch.float32, device=dev)
+        H.check(H.lib().dpvo_patch_gather(f.data_ptr(), strides.data_ptr(), h, w, imap.data_ptr(), dim, _ptr(img),
+                                          Hh, Ww, _ptr(lut), x.data_ptr(), y.data_ptr(), M, gm.data_ptr(),
+                                          im.data_ptr(), pt.data_ptr(), _ptr(clr), H.stream_of(fmap)))
+        return gm, im, pt, clr
+
+    def _lut(self, dev):
+        """lut[v] = 2 (v / 255) - 0.5 evaluated by the same torch ops as the
+        frame normalisation of forward() (net.py:116), so each entry is the
+        value that expression gives the pixel"""
+        lut = getattr(self, "_lut_t", None)
+        if lut is None or lut.device != dev:
+            v = torch.arange(256, dtype=torch.int32, device=dev).to(torch.uint8)
+            lut = self._lut_t = (2 * (v[None, None] / 255.0) - 0.5).reshape(256).contiguous()
+        return lut
