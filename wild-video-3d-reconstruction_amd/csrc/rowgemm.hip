@@ -1046,18 +1046,23 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
     // gate pass: the same stage layout, W pieces from Wg ([384][K1] like W1)
     const int64_t gdelta = GATED ? (const half_t*)pg.W - W1 : 0;
     // A pieces advance 32 columns per stage, k-blocked W pieces one 384 x 32 block
+    // WROT (DPVO_RC_DBG=1024, timing only, wrong results): every block walks the
+    // W stages in a k order rotated by its index, so the CUs of an XCD do not
+    // all request the same 24 KB W block from L2 at the same time
+    constexpr bool WROT = (DBG & 1024) != 0;
+    auto wrot = [&](int ks, int nks) { return WROT ? (ks + (int)(blockIdx.x % (unsigned)nks)) % nks : ks; };
     auto issue1 = [&](int ks, int buf, bool gate = false) {
         char* st = smem + RC_Y + buf * RC_STAGE;
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const bool wp = 4 * wave + j >= 8;
-            const int64_t k0 = wp ? (int64_t)ks * (RG_BN * RC_BK) : ks * RC_BK;
+            const int64_t k0 = wp ? (int64_t)wrot(ks, ks1) * (RG_BN * RC_BK) : ks * RC_BK;
             glds16(g1src[j] + k0 + (GATED && gate && wp ? gdelta : 0), st + (4 * wave + j) * 1024);
         }
     };
     auto issue2 = [&](int ks, int buf, int64_t wdelta = 0) {
         char* st = smem + RC_Y + buf * RC_STAGE + RC_A_STAGE;
-        const int64_t k0 = (int64_t)ks * (RG_BN * RC_BK) + wdelta;
+        const int64_t k0 = (int64_t)wrot(ks, ks2) * (RG_BN * RC_BK) + wdelta;
 #pragma unroll
         for (int j = 0; j < 3; j++) glds16(w2src[j] + k0, st + (3 * wave + j) * 1024);
     };
@@ -1330,6 +1335,51 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             __builtin_amdgcn_s_barrier();
         }
     };
+    // DEEP (DPVO_RC_DBG=2048): GEMM1 with four stages in flight instead of one.
+    // The y tile is free until GEMM1's result goes there, so it holds three
+    // more 32 KB stage slots beside the two stage buffers: slot s at
+    // RC_Y + s RC_STAGE (s < 2) or (s - 2) RC_STAGE.  Stage 0 is in slot 0
+    // (issued under the previous tile's epilogue); stage ks + 5 is issued into
+    // the slot of stage ks once every wave has passed step ks's trailing barrier.
+    constexpr bool DEEP = (DBG & 2048) != 0;
+    constexpr int DS = 5, DD = DS - 1;
+    auto slot1 = [](int sl) { return sl < 2 ? RC_Y + sl * RC_STAGE : (sl - 2) * RC_STAGE; };
+    auto issue1o = [&](int ks, int off) {
+        char* st = smem + off;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const bool wp = 4 * wave + j >= 8;
+            const int64_t k0 = wp ? (int64_t)wrot(ks, ks1) * (RG_BN * RC_BK) : ks * RC_BK;
+            glds16(g1src[j] + k0, st + (4 * wave + j) * 1024);
+        }
+    };
+    auto gemm1_deep = [&]() {
+#pragma unroll
+        for (int s2 = 1; s2 <= DD; s2++)
+            if (s2 < ks1) issue1o(s2, slot1(s2));
+#pragma unroll 1
+        for (int ks = 0; ks < ks1; ks++) {
+            // stages ks+1 .. min(ks+DD, ks1-1) may stay in flight, 4 loads each
+            const int ahead = min(DD, ks1 - 1 - ks);
+            if (ahead >= 4) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+            else if (ahead == 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            else if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const char* st = smem + slot1(ks % DS);
+            h8_t a[4], b[6];
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(st + a_off[mt]);
+#pragma unroll
+            for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+            mfma_step(a, b);
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            if (ks + DS < ks1) issue1o(ks + DS, slot1(ks % DS));
+        }
+    };
     auto gemm1 = [&](bool gate) {
         if (PP) {
             pp_loop(ks1, [&](int ks, int buf) { issue1_pp(ks, buf, gate); }, read1);
@@ -1369,6 +1419,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         // ---- GEMM1: A (global, gathered) x W1
         zero_acc();
         if (RING) gemm1_ring();
+        else if (DEEP) gemm1_deep();
         else gemm1(false);
         // ---- intermediate -> y tile; W2's first stage into the released stage 0
         acc_to_y((const half_t*)p1.bias, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
@@ -2507,7 +2558,7 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
         hipLaunchKernelGGL((rowchain_kernel<DPVO_RG_RES, false, (D)>), dim3(grid), dim3(RG_THREADS), 0,            \
                            as_stream(stream), *g1, a2, a2);                                                       \
         break;
-            RCD_CASE(0) RCD_CASE(1) RCD_CASE(2) RCD_CASE(3) RCD_CASE(16) RCD_CASE(32) RCD_CASE(48) RCD_CASE(256) RCD_CASE(257) RCD_CASE(512) RCD_CASE(513)
+            RCD_CASE(0) RCD_CASE(1) RCD_CASE(2) RCD_CASE(3) RCD_CASE(16) RCD_CASE(32) RCD_CASE(48) RCD_CASE(256) RCD_CASE(257) RCD_CASE(512) RCD_CASE(513) RCD_CASE(1024) RCD_CASE(1025) RCD_CASE(2048) RCD_CASE(2049)
 #undef RCD_CASE
         default:
             set_error("DPVO_RC_DBG: unsupported value");
