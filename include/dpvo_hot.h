@@ -585,6 +585,21 @@ int dpvo_keyframe_masks(const int64_t* ii, const int64_t* jj, const int64_t* kk,
 int dpvo_frame_shift(void* const* bases, const int64_t* slot_bytes, const int64_t* rings, int nseg, int64_t k,
                      int64_t n, void* stream);
 
+/* remove_factors (dpvo.py:349-364) as one stable compaction: edges with
+ * rm[e] == 0 go, in order, to the kept outputs (*_k); edges to store
+ * (store_mode 0: none, 1: every removed edge, 2: store[e] != 0, a subset of
+ * the removed ones) are written, in order, to the inactive outputs (*_s: the
+ * tails of the inactive lists).  Fields: ii / jj / kk int64, weight / target
+ * rows of wt_bytes, edge-state rows of row_bytes (a multiple of 16, 16-byte
+ * aligned).  Two launches; the caller sizes the outputs (the counts ride on
+ * keyframe()'s host read, dpvo_keyframe_masks). */
+size_t dpvo_compact_edges_workspace_bytes(int64_t num_edges);
+int dpvo_compact_edges(int64_t num_edges, const uint8_t* rm, const uint8_t* store, int store_mode, const int64_t* ii,
+                       const int64_t* jj, const int64_t* kk, const void* weight, const void* target, int wt_bytes,
+                       const void* net, int64_t row_bytes, int64_t* ii_k, int64_t* jj_k, int64_t* kk_k,
+                       void* weight_k, void* target_k, void* net_k, int64_t* ii_s, int64_t* jj_s, int64_t* kk_s,
+                       void* weight_s, void* target_s, void* workspace, size_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

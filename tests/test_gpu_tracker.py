@@ -503,3 +503,31 @@ def test_keyframe_masks_and_frame_shift_edges():
     assert ring._version > v0
     for a, b in zip((ring, plain, raw), refs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("mode", ["all", "none", "subset"])
+def test_native_compaction_equals_torch_path(mode):
+    """remove_factors with known sizes (dpvo_compact_edges, one stable
+    compaction of the index fields, weights, targets, edge state and the
+    inactive-list appends) == the torch index path, twice in a row (the second
+    call appends to the lists the first one grew)."""
+    from dpvo.synthetic import steady_state_tracker
+    g = torch.Generator(device="cuda").manual_seed(9)
+    with torch.no_grad():
+        a = steady_state_tracker("fast", buffer=96, n=70, seed=4)
+        b = steady_state_tracker("fast", buffer=96, n=70, seed=4)
+        a.NATIVE_COMPACTION = True
+        w, t = torch.rand_like(a.pg.weight), torch.rand_like(a.pg.target)
+        for s in (a, b):
+            s.pg.weight, s.pg.target = w.clone(), t.clone()
+        for _ in range(2):
+            E = a.pg.ii.numel()
+            m = torch.rand(E, generator=g, device="cuda") < 0.3
+            store = {"all": True, "none": False, "subset": m & (torch.rand(E, generator=g, device="cuda") < 0.5)}[mode]
+            n_store = int(m.sum()) if mode == "all" else 0 if mode == "none" else int(store.sum())
+            a.remove_factors(m, store, counts=(E - int(m.sum()), n_store))
+            b.remove_factors(m, store)
+            for name in ("ii", "jj", "kk", "net", "weight", "target", "ii_inac", "jj_inac", "kk_inac", "weight_inac",
+                         "target_inac"):
+                x, y = getattr(a.pg, name), getattr(b.pg, name)
+                assert x.shape == y.shape and torch.equal(x, y), name

@@ -96,6 +96,9 @@ _SIGNATURES = {
     "dpvo_keyframe_masks": (_ip, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp, _sz, _vp]),
     "dpvo_frame_shift": (_ip, [_vp, _vp, _vp, _ip, _i64, _i64, _vp]),
+    "dpvo_compact_edges_workspace_bytes": (_sz, [_i64]),
+    "dpvo_compact_edges": (_ip, [_i64, _vp, _vp, _ip, _vp, _vp, _vp, _vp, _vp, _ip, _vp, _i64, _vp, _vp, _vp, _vp, _vp,
+                                 _vp, _vp, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
     "dpvo_patch_gather": (_ip, [_vp, _vp, _ip, _ip, _vp, _ip, _vp, _ip, _ip, _vp, _vp, _vp, _i64, _vp, _vp, _vp,
                                 _vp, _vp]),
 }

@@ -415,6 +415,170 @@ __global__ __launch_bounds__(256) void frame_shift_kernel(FsArgs a, int64_t k, i
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// Edge-state compaction of keyframe() / remove_factors (dpvo.py:349-364):
+// edges with rm[e] == 0 keep their order at the front of the kept arrays;
+// edges with store[e] != 0 (a subset of the removed ones; store_mode 1: all
+// removed edges) are appended, in order, to the inactive lists.  Two launches:
+// per-block counts, then each block adds up the counts before it, ranks its
+// edges with wave ballots and moves them -- the index fields, the (weight,
+// target) rows and the edge-state rows (row_words 16-byte words each).
+constexpr int CE_THREADS = 256, CE_EDGES = 256;   // one edge per thread: E / 256 blocks
+
+struct CeArgs {
+    int64_t E;
+    const uint8_t* rm; const uint8_t* store; int store_mode;
+    const int64_t* ii; const int64_t* jj; const int64_t* kk;
+    const char* w; const char* t; int wt_bytes;          // weight / target rows, wt_bytes each
+    const uint4* net; int64_t row_words;                  // edge-state rows
+    int64_t* ii_k; int64_t* jj_k; int64_t* kk_k; char* w_k; char* t_k; uint4* net_k;
+    int64_t* ii_s; int64_t* jj_s; int64_t* kk_s; char* w_s; char* t_s;
+    int* part;
+};
+
+__device__ __forceinline__ bool ce_store(const CeArgs& a, int64_t e, bool rm)
+{
+    return a.store_mode == 1 ? rm : a.store_mode == 2 ? a.store[e] != 0 : false;
+}
+
+__device__ __forceinline__ void ce_row(char* d, const char* sp, int bytes)
+{
+    if (bytes % 8 == 0 && ((uintptr_t)d & 7) == 0 && ((uintptr_t)sp & 7) == 0)
+        for (int b = 0; b < bytes; b += 8) *(uint2*)(d + b) = *(const uint2*)(sp + b);
+    else
+        for (int b = 0; b < bytes; b++) d[b] = sp[b];
+}
+
+__global__ __launch_bounds__(CE_THREADS) void ce_count_kernel(CeArgs a)
+{
+    __shared__ int red[2][CE_THREADS / 64];
+    int ck = 0, cs = 0;
+    const int64_t e0 = (int64_t)blockIdx.x * CE_EDGES;
+    for (int i = threadIdx.x; i < CE_EDGES; i += CE_THREADS) {
+        const int64_t e = e0 + i;
+        if (e < a.E) {
+            const bool rm = a.rm[e] != 0;
+            ck += !rm;
+            cs += ce_store(a, e, rm);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        ck += __shfl_xor(ck, o);
+        cs += __shfl_xor(cs, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = ck;
+        red[1][threadIdx.x >> 6] = cs;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        int t = 0;
+        for (int w = 0; w < CE_THREADS / 64; w++) t += red[threadIdx.x][w];
+        a.part[blockIdx.x * 2 + threadIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(CE_THREADS) void ce_move_kernel(CeArgs a)
+{
+    __shared__ int base[2];
+    __shared__ int wsum[2][CE_THREADS / 64];
+    __shared__ int64_t src[CE_EDGES], dst[CE_EDGES];
+    __shared__ int nk_s;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // counts of the blocks before this one
+    {
+        int bk = 0, bs = 0;
+        for (int b = tid; b < (int)blockIdx.x; b += CE_THREADS) {
+            bk += a.part[2 * b];
+            bs += a.part[2 * b + 1];
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            bk += __shfl_xor(bk, o);
+            bs += __shfl_xor(bs, o);
+        }
+        if (lane == 0) { wsum[0][wv] = bk; wsum[1][wv] = bs; }
+        __syncthreads();
+        if (tid < 2) {
+            int t = 0;
+            for (int w = 0; w < CE_THREADS / 64; w++) t += wsum[tid][w];
+            base[tid] = t;
+        }
+        __syncthreads();
+    }
+    const int64_t e0 = (int64_t)blockIdx.x * CE_EDGES;
+    int64_t ok = base[0], os = base[1];   // running output positions (block-uniform)
+    int nk = 0;                           // kept edges of this block so far
+    for (int c = 0; c < CE_EDGES; c += CE_THREADS) {
+        const int64_t e = e0 + c + tid;
+        const bool in = e < a.E;
+        const bool rm = in && a.rm[e] != 0;
+        const bool keep = in && !rm, st = in && ce_store(a, e, rm);
+        const uint64_t bk = __ballot(keep), bs = __ballot(st);
+        const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const int rk = __popcll(bk & below), rs = __popcll(bs & below);
+        if (lane == 0) { wsum[0][wv] = __popcll(bk); wsum[1][wv] = __popcll(bs); }
+        __syncthreads();
+        int pk = 0, ps = 0, tk = 0, ts = 0;
+        for (int w = 0; w < CE_THREADS / 64; w++) {
+            pk += w < wv ? wsum[0][w] : 0;
+            ps += w < wv ? wsum[1][w] : 0;
+            tk += wsum[0][w];
+            ts += wsum[1][w];
+        }
+        if (keep) {
+            const int64_t d = ok + pk + rk;
+            a.ii_k[d] = a.ii[e];
+            a.jj_k[d] = a.jj[e];
+            a.kk_k[d] = a.kk[e];
+            ce_row(a.w_k + d * a.wt_bytes, a.w + e * a.wt_bytes, a.wt_bytes);
+            ce_row(a.t_k + d * a.wt_bytes, a.t + e * a.wt_bytes, a.wt_bytes);
+            src[nk + pk + rk] = e;
+            dst[nk + pk + rk] = d;
+        }
+        if (st) {
+            const int64_t d = os + ps + rs;
+            a.ii_s[d] = a.ii[e];
+            a.jj_s[d] = a.jj[e];
+            a.kk_s[d] = a.kk[e];
+            ce_row(a.w_s + d * a.wt_bytes, a.w + e * a.wt_bytes, a.wt_bytes);
+            ce_row(a.t_s + d * a.wt_bytes, a.t + e * a.wt_bytes, a.wt_bytes);
+        }
+        ok += tk;
+        os += ts;
+        nk += tk;
+        __syncthreads();   // wsum reused by the next chunk
+    }
+    if (tid == 0) nk_s = nk;
+    __syncthreads();
+    // the kept edge-state rows: each wave moves groups of 8 rows as one flat
+    // range of 16-byte words, all of a lane's loads issued before its stores
+    // (12 per lane for 1,536-byte rows: enough bytes in flight for HBM)
+    const int rw = (int)a.row_words;
+    constexpr int G = 8, U = 12;
+    for (int r0 = wv * G; r0 < nk_s; r0 += (CE_THREADS / 64) * G) {
+        const int total = min(G, nk_s - r0) * rw;
+        uint4 v[U];
+        int64_t to[U];
+#pragma unroll
+        for (int j = 0; j < U; j++) {
+            const int q = lane + 64 * j;
+            if (q < total) {
+                const int r = q / rw, wd = q - r * rw;
+                v[j] = a.net[src[r0 + r] * rw + wd];
+                to[j] = dst[r0 + r] * rw + wd;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < U; j++)
+            if (lane + 64 * j < total) a.net_k[to[j]] = v[j];
+        for (int q = lane + 64 * U; q < total; q += 64) {   // rows wider than 96 words
+            const int r = q / rw, wd = q - r * rw;
+            a.net_k[dst[r0 + r] * rw + wd] = a.net[src[r0 + r] * rw + wd];
+        }
+    }
+}
+
 }  // namespace dpvo
 
 using namespace dpvo;
@@ -557,6 +721,38 @@ extern "C" int dpvo_frame_shift(void* const* bases, const int64_t* slot_bytes, c
     }
     const unsigned gx = (unsigned)std::min<int64_t>((most + 255) / 256, 2048);
     hipLaunchKernelGGL(frame_shift_kernel, dim3(gx, nseg), dim3(256), 0, as_stream(stream), a, k, n);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" size_t dpvo_compact_edges_workspace_bytes(int64_t num_edges)
+{
+    return (size_t)std::max<int64_t>(1, (num_edges + CE_EDGES - 1) / CE_EDGES) * 2 * sizeof(int);
+}
+
+extern "C" int dpvo_compact_edges(int64_t num_edges, const uint8_t* rm, const uint8_t* store, int store_mode,
+                                  const int64_t* ii, const int64_t* jj, const int64_t* kk, const void* weight,
+                                  const void* target, int wt_bytes, const void* net, int64_t row_bytes,
+                                  int64_t* ii_k, int64_t* jj_k, int64_t* kk_k, void* weight_k, void* target_k,
+                                  void* net_k, int64_t* ii_s, int64_t* jj_s, int64_t* kk_s, void* weight_s,
+                                  void* target_s, void* workspace, size_t workspace_bytes, void* stream)
+{
+    DPVO_CHECK_ARG(num_edges >= 0 && store_mode >= 0 && store_mode <= 2, "bad size or store mode");
+    if (num_edges == 0) return 0;
+    DPVO_CHECK_ARG(rm && ii && jj && kk && weight && target && net, "null operand");
+    DPVO_CHECK_ARG(ii_k && jj_k && kk_k && weight_k && target_k && net_k, "null kept output");
+    DPVO_CHECK_ARG(store_mode != 2 || store, "store_mode 2 needs the store mask");
+    DPVO_CHECK_ARG(store_mode == 0 || (ii_s && jj_s && kk_s && weight_s && target_s), "null inactive output");
+    DPVO_CHECK_ARG(wt_bytes > 0 && row_bytes > 0 && row_bytes % 16 == 0, "row sizes: edge-state rows of 16-byte words");
+    DPVO_CHECK_ARG(((uintptr_t)net & 15) == 0 && ((uintptr_t)net_k & 15) == 0, "edge-state rows must be 16-byte aligned");
+    DPVO_CHECK_ARG(workspace && workspace_bytes >= dpvo_compact_edges_workspace_bytes(num_edges), "workspace too small");
+    const unsigned nblk = (unsigned)((num_edges + CE_EDGES - 1) / CE_EDGES);
+    CeArgs a{num_edges, rm, store, store_mode, ii, jj, kk, (const char*)weight, (const char*)target, wt_bytes,
+             (const uint4*)net, row_bytes / 16, ii_k, jj_k, kk_k, (char*)weight_k, (char*)target_k, (uint4*)net_k,
+             ii_s, jj_s, kk_s, (char*)weight_s, (char*)target_s, (int*)workspace};
+    hipStream_t st = as_stream(stream);
+    hipLaunchKernelGGL(ce_count_kernel, dim3(nblk), dim3(CE_THREADS), 0, st, a);
+    hipLaunchKernelGGL(ce_move_kernel, dim3(nblk), dim3(CE_THREADS), 0, st, a);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

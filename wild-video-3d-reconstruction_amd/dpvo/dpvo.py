@@ -16,6 +16,7 @@ MI355X-specific choices (all behind the same API):
 import torch
 import torch.nn.functional as F
 
+import _dpvo_hot as H
 import cuda_corr
 import cuda_ba
 import update_ops
@@ -250,6 +251,8 @@ class DPVO:
         host read): the indices then come from nonzero_static, with no
         synchronisation at all."""
         assert self.pg.ii.numel() == self.pg.weight.shape[1]
+        if counts is not None and self.NATIVE_COMPACTION and self._compact_native(m, store, *counts):
+            return
         if counts is None:
             index = lambda mask, _: torch.nonzero(mask).squeeze(1)
             counts = (None, None)
@@ -274,16 +277,13 @@ class DPVO:
         self._net_cap = cap
         self.pg.net = cap[:, :n_keep]
 
-    def _append_inactive(self, name, src, rem, dim):
-        """pg.<name> = cat(pg.<name>, src[rem]) along dim (dpvo.py:353-357), the
-        rows gathered straight into a buffer that doubles when full: the
-        inactive lists grow every frame, and re-concatenating them would copy
-        all of them each time"""
+    def _inactive_reserve(self, name, src, add, dim):
+        """room for `add` more rows of src's kind at the end of pg.<name>, in a
+        buffer that doubles when full: the inactive lists grow every frame,
+        and re-concatenating them would copy all of them each time.  Returns
+        (the tail to write, the grown list)."""
         cur = getattr(self.pg, name)
-        if cur.dtype != src.dtype:   # torch.cat's type promotion
-            setattr(self.pg, name, torch.cat((cur, src.index_select(dim, rem)), dim=dim))
-            return
-        n0, add = cur.shape[dim], rem.numel()
+        n0 = cur.shape[dim]
         caps = self.__dict__.setdefault("_inac_caps", {})
         cap = caps.get(name)
         if cap is None or cur.data_ptr() != cap.data_ptr() or cap.shape[dim] < n0 + add or not cur.is_contiguous():
@@ -292,8 +292,72 @@ class DPVO:
             cap = src.new_empty(size)
             cap.narrow(dim, 0, n0).copy_(cur)
             caps[name] = cap
-        torch.index_select(src, dim, rem, out=cap.narrow(dim, n0, add))
-        setattr(self.pg, name, cap.narrow(dim, 0, n0 + add))
+        return cap.narrow(dim, n0, add), cap.narrow(dim, 0, n0 + add)
+
+    def _append_inactive(self, name, src, rem, dim):
+        """pg.<name> = cat(pg.<name>, src[rem]) along dim (dpvo.py:353-357),
+        the rows gathered straight into the list's spare room"""
+        cur = getattr(self.pg, name)
+        if cur.dtype != src.dtype:   # torch.cat's type promotion
+            setattr(self.pg, name, torch.cat((cur, src.index_select(dim, rem)), dim=dim))
+            return
+        tail, grown = self._inactive_reserve(name, src, rem.numel(), dim)
+        torch.index_select(src, dim, rem, out=tail)
+        setattr(self.pg, name, grown)
+
+    # remove_factors through dpvo_compact_edges when the sizes are known.  Off:
+    # its row move measured slower than torch's gather (102-146 vs ~45 us for
+    # the 146 MB edge state at C3; profiles/r3/NOTES.md), so the two paths end
+    # level; kept for the equality test and further work
+    NATIVE_COMPACTION = False
+
+    _INACTIVE = (("ii_inac", "ii", 0), ("jj_inac", "jj", 0), ("kk_inac", "kk", 0), ("weight_inac", "weight", 1),
+                 ("target_inac", "target", 1))
+
+    def _compact_native(self, m, store, n_keep, n_store):
+        """remove_factors with known sizes as one native compaction
+        (dpvo_compact_edges: two launches for the index fields, weights,
+        targets, the edge state and the inactive-list appends).  False when
+        the edge state's layout does not allow it (the caller then uses the
+        torch path)."""
+        pg = self.pg
+        E = pg.ii.numel()
+        w, t, net = pg.weight, pg.target, pg.net
+        if not (w.dim() == 3 and w.shape[:2] == (1, E) and t.shape == w.shape and t.dtype == w.dtype and
+                w.is_contiguous() and t.is_contiguous() and net.dim() == 3 and net.shape[:2] == (1, E) and
+                net.is_contiguous() and (net.shape[2] * net.element_size()) % 16 == 0 and net.data_ptr() % 16 == 0
+                and all(x.dtype == torch.int64 and x.is_contiguous() for x in (pg.ii, pg.jj, pg.kk))
+                and all(getattr(pg, a).dtype == getattr(pg, b).dtype for a, b, _ in self._INACTIVE)):
+            return False
+        if n_keep == 0 or E == 0:
+            return False
+        mode = 1 if store is True else 0 if store is False else 2
+        if n_store == 0:   # nothing to append (and empty tails have no address)
+            mode = 0
+        rm = m.contiguous().view(torch.uint8)
+        sm = store.contiguous().view(torch.uint8) if mode == 2 else None
+        ii_k, jj_k, kk_k = (torch.empty(n_keep, dtype=torch.int64, device=self.device) for _ in range(3))
+        w_k, t_k = w.new_empty(1, n_keep, w.shape[2]), t.new_empty(1, n_keep, t.shape[2])
+        cap = net.new_empty(1, n_keep + self._edge_slack(), net.shape[2])
+        tails, grown = {}, {}
+        if mode:
+            for name, src, dim in self._INACTIVE:
+                tails[name], grown[name] = self._inactive_reserve(name, getattr(pg, src), n_store, dim)
+        tp = lambda name: tails[name].data_ptr() if mode else None
+        nb = H.lib().dpvo_compact_edges_workspace_bytes(E)
+        ws = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        H.check(H.lib().dpvo_compact_edges(
+            E, rm.data_ptr(), sm.data_ptr() if sm is not None else None, mode, pg.ii.data_ptr(), pg.jj.data_ptr(),
+            pg.kk.data_ptr(), w.data_ptr(), t.data_ptr(), w.shape[2] * w.element_size(), net.data_ptr(),
+            net.shape[2] * net.element_size(), ii_k.data_ptr(), jj_k.data_ptr(), kk_k.data_ptr(), w_k.data_ptr(),
+            t_k.data_ptr(), cap.data_ptr(), tp("ii_inac"), tp("jj_inac"), tp("kk_inac"), tp("weight_inac"),
+            tp("target_inac"), ws.data_ptr(), nb, H.stream_of(net)))
+        for name, g in grown.items():
+            setattr(pg, name, g)
+        pg.ii, pg.jj, pg.kk, pg.weight, pg.target = ii_k, jj_k, kk_k, w_k, t_k
+        self._net_cap = cap
+        pg.net = cap[:, :n_keep]
+        return True
 
     def _edge_slack(self):
         """rows one frame's append adds at most: forward and backward edges
