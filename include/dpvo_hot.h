@@ -31,7 +31,13 @@ extern "C" {
 
 enum { DPVO_F16 = 0, DPVO_F32 = 1, DPVO_F64 = 2 };
 
-#define DPVO_HOT_ABI_VERSION 1
+/* ABI version history:
+ *  1 -- rounds 1-2.
+ *  2 -- dpvo_rowchain / dpvo_rowchain_gated / dpvo_rowchain3 read every W
+ *       k-blocked ([K/32][384][32] instead of [384][K]); dpvo_rowadd_args
+ *       gained c16 / c_idx / c_rows.  A caller built against version 1 must
+ *       not run against this library. */
+#define DPVO_HOT_ABI_VERSION 2
 
 int dpvo_hot_abi_version(void);
 const char* dpvo_hot_last_error(void);

@@ -43,7 +43,7 @@ def test_ctypes_binding_covers_header_and_loads():
     import _dpvo_hot as H
     assert sorted(H.EXPORTED) == declared()
     lib = H.lib()  # dlopen without touching the GPU
-    assert lib.dpvo_hot_abi_version() == 1
+    assert lib.dpvo_hot_abi_version() == 2
     assert lib.dpvo_ba_workspace_bytes(95424, 2048 * 192, 10) > 0
     assert lib.dpvo_neighbors_workspace_bytes(95424) > 0
 

@@ -109,3 +109,20 @@ def test_group_by_large_groups_counting_sort():
     for gg in (0, 1, G - 1):
         members = p[o[gg]:o[gg + 1]]
         assert torch.equal(members, torch.nonzero(inv == gg)[:, 0])
+
+
+def test_out_of_range_index_raises_like_torch_scatter():
+    """torch-scatter 2.1.2 fails on an index outside the output:
+    no member is dropped silently."""
+    ts = _shim()
+    src = torch.randn(10, 4, device="cuda")
+    idx = torch.arange(10, device="cuda")
+    with pytest.raises(IndexError):
+        ts.scatter_sum(src, idx, dim=0, dim_size=5)
+    with pytest.raises(IndexError):
+        ts.scatter_mean(src, idx, dim=0, out=torch.zeros(9, 4, device="cuda"))
+    with pytest.raises(IndexError):
+        ts.scatter_max(src, idx - 1, dim=0)
+    with pytest.raises(IndexError):
+        ts.scatter_softmax(src, idx - 3, dim=0)
+    assert ts.scatter_sum(src, idx, dim=0, dim_size=10).shape == (10, 4)

@@ -94,8 +94,11 @@ def test_window_violation_skips_ba_and_raises():
 
 def test_update_get_corr():
     """dpvo.py:660-687: one update, BA failure reported as a warning, the
-    point cloud of all stored patches and the BA targets returned"""
+    point cloud of all stored patches and the BA targets returned, pg.target /
+    pg.weight left as they were (the reference's update_get_corr never sets
+    them)"""
     a, b = make(seed=9), make(seed=9)
+    t_before, w_before = b.pg.target, b.pg.weight
     with torch.no_grad():
         a.update()
         pts, target = b.update_get_corr()
@@ -104,7 +107,24 @@ def test_update_get_corr():
     assert pts.shape == (m, 3) and target.shape == (1, a.pg.ii.numel(), 2)
     assert torch.equal(pts, a.pg.points_[:m]) and torch.equal(target, a.pg.target)
     assert torch.equal(b.pg.poses_[:b.n], a.pg.poses_[:a.n])
+    assert b.pg.target is t_before and b.pg.weight is w_before
+    orig = b.update
+
+    def failing(word):
+        def f(t0=None):
+            orig(t0)
+            b._ba_fail.fill_(word)   # as if THIS update's BA / window check had set the word
+        return f
     with torch.no_grad():
-        b._ba_fail.fill_(7)                    # as if this update's BA had failed: caught, as in the reference
+        b.update = failing(7)                  # this call's Cholesky failure: caught, as in the reference
         b.update_get_corr()
-    b.check_ba()                               # the failure was consumed by the warning
+        b.check_ba()                           # consumed by the warning
+        b.update = orig
+        b._ba_fail.fill_(7)                    # an EARLIER update's failure is raised, not swallowed
+        with pytest.raises(RuntimeError, match="leading minor of order 7"):
+            b.update_get_corr()
+        b.update = failing(-2)                 # the window-key flag raises
+        with pytest.raises(RuntimeError, match="64-frame key window"):
+            b.update_get_corr()
+        b.update = orig
+    b.check_ba()

@@ -30,7 +30,7 @@
 namespace dpvo {
 
 namespace corr {
-constexpr int R = 3, D = 8, DO = 7, PS = 3, NP = 9, BOX = 10, NPAIR = 5;
+constexpr int R = 3, D = 8, DO = 7, PS = 3, NP = 9, NPAIR = 5;
 // v3's shared box: floor spreads up to 4 px (12 x 12).  At level 1 about 1 edge
 // in 9 of the C3 workload spreads by 3 px (perspective scale ~1.4 between
 // frames up to 35 apart); per-pixel windows would cost it 4x the common pass.
@@ -86,213 +86,6 @@ struct LevelMeta {
     int fast, oy, ox, bw, bh, nslots, first_slot, pad;
     float rbw;   // 1 / bw (v3 decode: exact floor((loc + 0.5) / bw) for loc < 256, bw <= 12)
 };
-
-template <int NLEV, int C8>
-__global__ __launch_bounds__(FastThreads<NLEV>::value) void corr_fast_kernel(CorrFastParams p)
-{
-    using namespace corr;
-    constexpr int NT = FastThreads<NLEV>::value;
-    constexpr int C = C8 * 8;
-    __shared__ __attribute__((aligned(16))) uint32_t f1pk[C * 8];   // (p0,p1)(p2,p3)(p4,p5)(p6,p7)(p8,0) per channel
-    __shared__ half_t raw[NLEV][NP][BOX * BOX];                      // raw 8x8 tiles (inside the shared box)
-    __shared__ LevelMeta meta[NLEV];
-
-    const int bid = xcd_swizzle(blockIdx.x, gridDim.x);
-    const int b = bid / p.E, e = bid - b * p.E;
-    const int tid = threadIdx.x;
-    const int ix = (int)p.ii[e];
-    const int jx = (int)p.jj[e];
-    const bool ix_ok = ix >= 0 && ix < p.N1;
-
-    // ---- per-level floors and shared-box geometry (one thread per level)
-    if (tid < NLEV) {
-        LevelMeta& m = meta[tid];
-        const float sc = p.scale[tid];
-        const float* cb = p.coords + b * p.c_s[0] + (int64_t)e * p.c_s[1];
-        int ymin = 0x7fffffff, ymax = (int)0x80000000u, xmin = 0x7fffffff, xmax = (int)0x80000000u;
-        for (int q = 0; q < NP; q++) {
-            const int64_t o = (q / PS) * p.c_s[3] + (q % PS) * p.c_s[4];
-            const float x = cb[o] / sc, y = cb[p.c_s[2] + o] / sc;
-            m.xs[q] = x; m.ys[q] = y;
-            m.fy[q] = floor_to_int_sat(y);
-            m.fx[q] = floor_to_int_sat(x);
-            ymin = min(ymin, m.fy[q]); ymax = max(ymax, m.fy[q]);
-            xmin = min(xmin, m.fx[q]); xmax = max(xmax, m.fx[q]);
-        }
-        m.fast = ((int64_t)ymax - ymin) <= 2 && ((int64_t)xmax - xmin) <= 2;
-        m.oy = wrap_add(ymin, -R);
-        m.ox = wrap_add(xmin, -R);
-        m.bh = m.fast ? (ymax - ymin) + D : D;
-        m.bw = m.fast ? (xmax - xmin) + D : D;
-        m.nslots = m.fast ? m.bh * m.bw : NP * D * D;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        int acc = 0;
-        for (int l = 0; l < NLEV; l++) { meta[l].first_slot = acc; acc += meta[l].nslots; }
-        meta[0].pad = acc;  // total slots
-    }
-    __syncthreads();
-    const int total = meta[0].pad;
-
-    // slot -> (level, box pixel).  Every lane gets a valid row pointer (out-of-image
-    // lanes read the frame origin and their chains are zeroed afterwards), so the
-    // loads need no branches.
-    struct Slot { int lev, q_only, u; bool act, inb; const uint4* ptr; };
-    auto decode = [&](int slot) {
-        Slot s{0, -1, 0, false, false, nullptr};
-        s.act = slot < total;
-        const int sl = s.act ? slot : 0;
-        s.lev = (NLEV == 2 && sl >= meta[NLEV - 1].first_slot) ? NLEV - 1 : 0;
-        const LevelMeta& m = meta[s.lev];
-        const int loc = sl - m.first_slot;
-        int gy, gx;
-        if (m.fast) {
-            const int uy = loc / m.bw, ux = loc - uy * m.bw;
-            gy = wrap_add(m.oy, uy); gx = wrap_add(m.ox, ux);
-            s.u = loc;
-        } else {
-            const int q = loc / (D * D), u = loc - q * (D * D);
-            const int uy = u / D, ux = u - uy * D;
-            gy = wrap_add(m.fy[q], uy - R); gx = wrap_add(m.fx[q], ux - R);
-            s.q_only = q;
-            s.u = u;
-        }
-        const int lv = s.lev;
-        s.inb = s.act && ix_ok && jx >= 0 && jx < p.N2[lv] && gy >= 0 && gy < p.H2[lv] && gx >= 0 && gx < p.W2[lv];
-        const half_t* base = p.fmap[lv] + b * p.f_s0[lv];
-        s.ptr = reinterpret_cast<const uint4*>(
-            s.inb ? base + (int64_t)jx * p.f_s1[lv] + (int64_t)gy * p.f_s3[lv] + (int64_t)gx * p.f_s4[lv] : base);
-        return s;
-    };
-
-    // ---- the reference's chain, channel 0..C-1, for all nine patch pixels, two per op:
-    //      acc = acc + (W[c], W[c]) * (f1[p][c], f1[p'][c])   (no FMA: exact per-op rounding)
-    // The patch pairs are fetched per 8-channel chunk with inline-asm ds_reads: as
-    // plain loads, LLVM hoists all C x 5 of them to the top and the kernel drops to
-    // 2 waves/SIMD.
-    auto chunk = [&](half2_t (&acc)[NPAIR], const uint4 wq, int k) {
-        lds_u32* fb = (lds_u32*)(f1pk) + k * 64;  // 8 channels x 8 dwords (address-space cast)
-        u32x4 fa[8];
-        uint32_t fc[8];
-#pragma unroll
-        for (int c = 0; c < 8; c++) {
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(fa[c]) : "v"(fb), "i"(c * 32));
-            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(fc[c]) : "v"(fb), "i"(c * 32 + 16));
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t wd[4] = {wq.x, wq.y, wq.z, wq.w};
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const half2_t wv = as_h2(wd[j]);
-#pragma unroll
-            for (int hsel = 0; hsel < 2; hsel++) {
-                const int c = 2 * j + hsel;
-                const half_t ws = hsel ? wv.y : wv.x;
-                const half2_t wb = {ws, ws};
-                acc[0] = acc[0] + wb * as_h2(fa[c].x);
-                acc[1] = acc[1] + wb * as_h2(fa[c].y);
-                acc[2] = acc[2] + wb * as_h2(fa[c].z);
-                acc[3] = acc[3] + wb * as_h2(fa[c].w);
-                acc[4] = acc[4] + wb * as_h2(fc[c]);
-            }
-        }
-        // pin this chunk's arithmetic before the next chunk's (volatile) reads
-#pragma unroll
-        for (int q = 0; q < NPAIR; q++) asm volatile("" : "+v"(acc[q]));
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    // first pass: this lane's first four 16-byte chunks are in flight before the
-    // patch-feature repack and the barrier
-    Slot cur = decode(tid);
-    uint4 a0 = cur.ptr[0], a1 = cur.ptr[1], a2 = cur.ptr[2], a3 = cur.ptr[3];
-
-    // ---- patch features -> channel-major packed pairs, one global round trip
-    if (tid < C) {
-        const half_t* g = p.gmap + b * p.g_s[0] + (int64_t)(ix_ok ? ix : 0) * p.g_s[1] + tid * p.g_s[2];
-        half_t v[NP + 1];
-#pragma unroll
-        for (int q = 0; q < NP; q++) v[q] = g[(q / PS) * p.g_s[3] + (q % PS) * p.g_s[4]];
-        v[NP] = (half_t)0;
-        uint32_t d[NPAIR];
-#pragma unroll
-        for (int q = 0; q < NPAIR; q++) d[q] = __builtin_bit_cast(uint32_t, (half2_t){v[2 * q], v[2 * q + 1]});
-        *reinterpret_cast<uint4*>(f1pk + tid * 8) = make_uint4(d[0], d[1], d[2], d[3]);
-        f1pk[tid * 8 + 4] = d[4];
-    }
-    __syncthreads();
-
-    for (int base = 0; base < total; base += NT) {
-        if (base > 0) {
-            cur = decode(base + tid);
-            a0 = cur.ptr[0]; a1 = cur.ptr[1]; a2 = cur.ptr[2]; a3 = cur.ptr[3];
-        }
-        half2_t acc[NPAIR];
-#pragma unroll
-        for (int q = 0; q < NPAIR; q++) acc[q] = (half2_t){(half_t)0, (half_t)0};
-        // software pipeline: 4 chunks (4 KB per wave) in flight while 4 are consumed
-#pragma unroll 1
-        for (int k = 0; k < C8; k += 8) {
-            const uint4 b0 = cur.ptr[k + 4], b1 = cur.ptr[k + 5], b2 = cur.ptr[k + 6], b3 = cur.ptr[k + 7];
-            chunk(acc, a0, k + 0);
-            chunk(acc, a1, k + 1);
-            chunk(acc, a2, k + 2);
-            chunk(acc, a3, k + 3);
-            if (k + 8 < C8) {
-                a0 = cur.ptr[k + 8]; a1 = cur.ptr[k + 9]; a2 = cur.ptr[k + 10]; a3 = cur.ptr[k + 11];
-            }
-            chunk(acc, b0, k + 4);
-            chunk(acc, b1, k + 5);
-            chunk(acc, b2, k + 6);
-            chunk(acc, b3, k + 7);
-        }
-        if (cur.act) {
-            // out-of-image taps are exactly +0 in the reference (never accumulated)
-            const half_t z = (half_t)0;
-            const half_t sv[NP] = {acc[0].x, acc[0].y, acc[1].x, acc[1].y, acc[2].x,
-                                   acc[2].y, acc[3].x, acc[3].y, acc[4].x};
-            if (cur.q_only < 0) {
-#pragma unroll
-                for (int q = 0; q < NP; q++) raw[cur.lev][q][cur.u] = cur.inb ? sv[q] : z;
-            } else {
-                half_t v = z;
-#pragma unroll
-                for (int q = 0; q < NP; q++) if (q == cur.q_only) v = sv[q];
-                raw[cur.lev][cur.q_only][cur.u] = cur.inb ? v : z;
-            }
-        }
-    }
-    __syncthreads();
-
-    // ---- bilinear epilogue, exact rounding sequence of correlation_kernel.cu:221-232,
-    // outputs enumerated in the stacked layout's memory order (x, y, pixel, level)
-    half_t* ob = p.out + b * p.o_b + (int64_t)e * p.o_e;
-    for (int o = tid; o < NLEV * NP * DO * DO; o += NT) {
-        const int lev = o % NLEV;
-        int r = o / NLEV;
-        const int q = r % NP; r /= NP;
-        const int a = r % DO;
-        const int bx = r / DO;
-        const LevelMeta& m = meta[lev];
-        const int bw = m.fast ? m.bw : D;
-        const int oy = m.fast ? m.fy[q] - (int)wrap_add(m.oy, R) : 0;
-        const int ox = m.fast ? m.fx[q] - (int)wrap_add(m.ox, R) : 0;
-        const half_t* t = &raw[lev][q][(oy + a) * bw + (ox + bx)];
-        const half_t c00 = t[0], c01 = t[1], c10 = t[bw], c11 = t[bw + 1];
-        const float xq = m.xs[q], yq = m.ys[q];
-        const half_t dx = (half_t)(xq - floorf(xq));
-        const half_t dy = (half_t)(yq - floorf(yq));
-        const half_t one = (half_t)1.0f;
-        const half_t omdx = one - dx, omdy = one - dy;
-        half_t v = hmul(hmul(omdx, omdy), c00);
-        v = hadd(v, hmul(hmul(dx, omdy), c01));
-        v = hadd(v, hmul(hmul(omdx, dy), c10));
-        v = hadd(v, hmul(hmul(dx, dy), c11));
-        ob[bx * p.o_x + a * p.o_y + q * p.o_p + lev * p.o_l] = v;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // v3 fast path: the patch features are uniform over the workgroup, so they are
@@ -774,11 +567,7 @@ int launch_fast(int nlev, const void* gmap, const int64_t* gsz, const int64_t* g
     p.o_b = ostr[0]; p.o_e = ostr[1]; p.o_l = ostr[2]; p.o_x = ostr[3]; p.o_y = ostr[4]; p.o_p = ostr[5];
     const int64_t nblk = (int64_t)p.B * p.E;
     if (nblk == 0) return 0;
-    static const int version = [] {
-        const char* v = getenv("DPVO_CORR_KERNEL");
-        return v ? atoi(v) : 3;
-    }();
-    if (version == 3) {
+    {
         // patch features as a scalar-load table: the caller's (dpvo_corr_pack), or
         // packed here into stream-ordered scratch
         void* tab = nullptr;
@@ -799,12 +588,7 @@ int launch_fast(int nlev, const void* gmap, const int64_t* gsz, const int64_t* g
             hipLaunchKernelGGL((corr_sfast_kernel<1, 16>), dim3((unsigned)nblk), dim3(FastThreads<1>::value), 0,
                                stream, p);
         if (tab) (void)hipFreeAsync(tab, stream);
-        return 0;
     }
-    if (nlev == 2)
-        hipLaunchKernelGGL((corr_fast_kernel<2, 16>), dim3((unsigned)nblk), dim3(FastThreads<2>::value), 0, stream, p);
-    else
-        hipLaunchKernelGGL((corr_fast_kernel<1, 16>), dim3((unsigned)nblk), dim3(FastThreads<1>::value), 0, stream, p);
     return 0;
 }
 

@@ -15,9 +15,6 @@ namespace dpvo {
 // error reporting through the C ABI
 // ---------------------------------------------------------------------------
 void set_error(const std::string& msg);
-// once per process: a timing-experiment environment switch that makes results
-// invalid is active (DPVO_CM_DBG, DPVO_BD_DBG, DPVO_RC_DBG, DPVO_RG4_DBG)
-void warn_debug_knob(const char* name);
 
 #define DPVO_CHECK_ARG(cond, msg)                                   \
     do {                                                            \

@@ -568,12 +568,7 @@ extern "C" int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, co
     int64_t g = std::min<int64_t>((E + cm::WAVES - 1) / cm::WAVES, 256 * 3);   // LDS and VGPRs: 3 per CU
     if (g > 8) g &= ~int64_t(7);
     const unsigned grid = (unsigned)g;
-    static const bool nostore = getenv("DPVO_CM_DBG") && std::string(getenv("DPVO_CM_DBG")) == "nostore";
-    if (nostore) warn_debug_knob("DPVO_CM_DBG");
-    if (nostore)
-        hipLaunchKernelGGL(corr_mfma_kernel<false>, dim3(grid), dim3(64 * cm::WAVES), 0, as_stream(stream), p);
-    else
-        hipLaunchKernelGGL(corr_mfma_kernel<true>, dim3(grid), dim3(64 * cm::WAVES), 0, as_stream(stream), p);
+    hipLaunchKernelGGL(corr_mfma_kernel<true>, dim3(grid), dim3(64 * cm::WAVES), 0, as_stream(stream), p);
     DPVO_CHECK_LAUNCH();
     return 0;
 }

@@ -1565,16 +1565,7 @@ constexpr int BD_NMAX = 12;
 constexpr int BD_N6MAX = 6 * BD_NMAX;     // 72
 constexpr int BD_WAVES = 4;
 constexpr int BD_GRID = 512;    // 4 waves each (measured over 256-2048: 512 is fastest at C3 and C2, scripts/exp_bd_grid.sh)
-constexpr int BD_GRID_MAX = 2048;   // workspace sizing (DPVO_BD_GRID timing experiments)
-static int bd_grid()
-{
-    static const int g = [] {
-        const char* e = getenv("DPVO_BD_GRID");
-        const int v = e ? atoi(e) : BD_GRID;
-        return v >= 64 && v <= BD_GRID_MAX ? v : BD_GRID;
-    }();
-    return g;
-}
+static int bd_grid() { return BD_GRID; }
 
 struct BdLayout {
     size_t hdr, gid, offs, perm, groups, gbws, gbws_bytes, Em, Cg, ug, Hpart, H, dX, total;
@@ -1602,7 +1593,7 @@ static BdLayout bd_layout(int64_t E, int64_t num_patches, int N)
     L.Em = take((size_t)L.mu_max * std::max(L.n6, 1) * 4);
     L.Cg = take((size_t)L.mu_max * 4);
     L.ug = take((size_t)L.mu_max * 4);
-    L.Hpart = take((size_t)BD_GRID_MAX * std::max(L.ent, 1) * 4);
+    L.Hpart = take((size_t)BD_GRID * std::max(L.ent, 1) * 4);
     L.H = take((size_t)std::max(L.ent, 1) * 4);
     L.dX = take((size_t)std::max(L.n6, 1) * 4);
     L.total = off;
@@ -1773,10 +1764,7 @@ constexpr int BD_SLOT_IT = 8;                     // wave iterations per flush
 constexpr int BD_SLOTS = BD_SLOT_IT * BD_WAVES;   // 32 listed patches
 constexpr int BD_SLOT_LD = BD_N6MAX + 2;          // E row, Q, Q u
 
-// DBG (timing experiments only, DPVO_BD_DBG; results are wrong): 1 skips the
-// shared-frame / target-frame pose terms, 2 the Schur update, 4 the
-// workgroup partial's write
-template <bool APPLY, bool HESS, int DBG = 0>
+template <bool APPLY, bool HESS>
 __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
 {
     extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -1870,7 +1858,7 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
             const bool jt = o.jv && !o.self;
             for (int q = 0; q < N && !mixed; q++)
                 mixed = __popcll(__ballot(jt && o.jx == q)) > 1;
-            const int passes = (DBG & 1) ? 0 : mixed ? 64 : 1;
+            const int passes = mixed ? 64 : 1;
             for (int ps = 0; ps < passes; ps++) {
                 const bool act = !mixed || lane == ps;
                 const uint64_t ivm = __ballot(act && o.iv);
@@ -1939,7 +1927,7 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
             // slots in order, into wave 0's partial (one thread per entry)
             __syncthreads();
             const int ns = (sit + 1) * BD_WAVES;
-            if (!(DBG & 2)) {
+            {
                 for (int kx = threadIdx.x; kx < ent; kx += blockDim.x) {
                     float acc = sm[kx];
                     if (kx < nup) {
@@ -1965,7 +1953,7 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
     // the workgroup's partial: its waves' partials summed in wave order
     __syncthreads();
     float* dst = p.Hpart + (int64_t)blockIdx.x * ent;
-    for (int i = threadIdx.x; i < ((DBG & 4) ? 0 : ent); i += blockDim.x) {
+    for (int i = threadIdx.x; i < ent; i += blockDim.x) {
         float s = sm[i];
 #pragma unroll
         for (int w = 1; w < BD_WAVES; w++) s += sm[w * ent + i];
@@ -2240,8 +2228,7 @@ __global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
 
 static void bd_solve_launch(const BdParams& p, hipStream_t s)
 {
-    static const bool blocked = getenv("DPVO_BD_BLOCK_SOLVE") != nullptr;   // A/B switch: the workgroup solver
-    if (blocked || p.N > 10) {
+    if (p.N > 10) {   // 11-12 poses: the workgroup solver
         hipLaunchKernelGGL(bd_solve_kernel, dim3(1), dim3(256), 0, s, p);
         return;
     }
@@ -2281,25 +2268,11 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
                        (size_t)(p.N > 0 ? (L.nup + 1) / 2 : 0) * 4 +
                        (size_t)(p.N > 0 ? BD_SLOTS * BD_SLOT_LD : 0) * 4;
     const unsigned gR = (unsigned)((L.ent + 63) / 64);
-    static const int dbg = getenv("DPVO_BD_DBG") ? atoi(getenv("DPVO_BD_DBG")) : 0;
-    if (dbg) warn_debug_knob("DPVO_BD_DBG");
     for (int it = 0; it < iterations; it++) {
-#define BD_HESS(A, D) hipLaunchKernelGGL((bd_patch_kernel<A, true, D>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p)
-#define BD_DBG_CASES(A)                                                                                   \
-        switch (dbg) {                                                                                    \
-        case 1: BD_HESS(A, 1); break;                                                                     \
-        case 2: BD_HESS(A, 2); break;                                                                     \
-        case 3: BD_HESS(A, 3); break;                                                                     \
-        case 7: BD_HESS(A, 7); break;                                                                     \
-        default: BD_HESS(A, 0);                                                                           \
-        }
-        if (it == 0) {
-            BD_DBG_CASES(false)
-        } else {
-            BD_DBG_CASES(true)
-        }
-#undef BD_DBG_CASES
-#undef BD_HESS
+        if (it == 0)
+            hipLaunchKernelGGL((bd_patch_kernel<false, true>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p);
+        else
+            hipLaunchKernelGGL((bd_patch_kernel<true, true>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p);
         if (p.N > 0) {
             hipLaunchKernelGGL(bd_reduce_kernel, dim3(gR), dim3(1024), 0, s, p, bd_grid());
             bd_solve_launch(p, s);
@@ -2401,13 +2374,7 @@ extern "C" int dpvo_ba_forward_ex(float* poses, float* patches, int64_t num_patc
     DPVO_CHECK_ARG(workspace && workspace_bytes >= L.total, "workspace too small");
     p.hdr = (int*)(ws + L.hdr);
     p.status = status ? status : p.hdr + HDR_STATUS;
-    {
-        static const int red = [] {
-            const char* v = getenv("DPVO_BA_WAVE_RED");
-            return v ? atoi(v) : 2;
-        }();
-        p.red_iters = red;
-    }
+    p.red_iters = 2;   // wave-reduction rounds of the atomic path's Hessian (measured best)
     p.bits = (uint32_t*)(ws + L.bits);
     p.wordbase = (int*)(ws + L.wordbase);
     p.kx = (int*)(ws + L.kx);
@@ -2445,8 +2412,7 @@ extern "C" int dpvo_ba_forward_ex(float* poses, float* patches, int64_t num_patc
             hipLaunchKernelGGL((ba_hessian_kernel<false, false>), dim3(gH), dim3(256), 0, s, p);
         if (N > 0) {
             hipLaunchKernelGGL(ba_schur_kernel, dim3(gS), dim3(256), lds_s, s, p);
-            static const bool block_solve = getenv("DPVO_BA_BLOCK_SOLVE") != nullptr;  // A/B switch
-            if (p.n6 <= 64 && !block_solve)
+            if (p.n6 <= 64)
                 hipLaunchKernelGGL(ba_solve_wave_kernel, dim3(1), dim3(64), 0, s, p);
             else
                 hipLaunchKernelGGL(ba_solve_kernel, dim3(1), dim3(256), lds_v, s, p);

@@ -18,14 +18,6 @@ namespace dpvo {
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
-void warn_debug_knob(const char* name)
-{
-    static std::mutex mu;
-    static std::set<std::string> seen;
-    std::lock_guard<std::mutex> lock(mu);
-    if (seen.insert(name).second)
-        fprintf(stderr, "libdpvo_hot: %s is set -- a timing experiment; results are NOT valid\n", name);
-}
 
 using G3 = lie::SE3<float>;
 

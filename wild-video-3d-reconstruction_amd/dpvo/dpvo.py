@@ -159,6 +159,7 @@ class DPVO:
         return points[mask], colors[mask], (intrinsic, self.ht, self.wd)
 
     def get_pose(self, t):
+        self.flush_keyframe()
         if t in self.traj:
             return SE3(self.traj[t])
         t0, dP = self.pg.delta[t]
@@ -467,16 +468,31 @@ class DPVO:
         m stored patches [m, 3], target [1, E, 2]).  The reference stores the
         points into ``self.points_``, which DPVO does not have (its
         AttributeError at :686 makes the method unusable there); they go to
-        ``pg.points_`` here, where update() writes them."""
+        ``pg.points_`` here, where update() writes them.  Like the reference it
+        leaves pg.target / pg.weight as they were.  Only a Cholesky failure of
+        THIS call becomes the warning: failures pending from earlier update()s
+        and the window-key flag (-2) raise, as their next host read would."""
+        defer = getattr(self.cfg, "DEFER_BA_CHECK", True)
+        if defer:
+            self.check_ba()   # earlier updates' status: raised, never swallowed here
+        saved = (self.pg.target, self.pg.weight)
         try:
             self.update()
-            status = int(self._ba_fail.item()) if getattr(self.cfg, "DEFER_BA_CHECK", True) else 0
-        except RuntimeError:
+            status = int(self._ba_fail.item()) if defer else 0
+        except RuntimeError as e:
+            if "cholesky" not in str(e):
+                raise
             status = 1
-        if status:
+        finally:
+            target = self.pg.target
+            self.pg.target, self.pg.weight = saved
+        if status > 0:
             self._ba_fail.zero_()
             print("Warning BA failed...")
-        return self.pg.points_[:self.pg.m], self.pg.target
+        elif status:
+            self._ba_fail.zero_()
+            cuda_ba.raise_for_status(status)
+        return self.pg.points_[:self.pg.m], target
 
     def _window_keys(self):
         """True when every edge of the sliding window has n - 64 <= ii, jj < n
@@ -529,6 +545,9 @@ class DPVO:
         change the key and the next call captures again."""
         if not getattr(self.cfg, "DEFER_BA_CHECK", True):
             raise RuntimeError("update_graphed needs cfg.DEFER_BA_CHECK (no host read inside update())")
+        # a deferred keyframe() decision changes the edges: apply it before the
+        # replay key is formed (the reference's order is keyframe, then update)
+        self.flush_keyframe()
         key = (self.pg.ii.data_ptr(), self.pg.jj.data_ptr(), self.pg.kk.data_ptr(), self.pg.ii.numel(), self.n,
                t0, self.gmap_._version, self.pg.net.data_ptr(), self.pg.net.shape)
         if self._ugraph is not None and self._ugraph[0] == key:
@@ -557,7 +576,10 @@ class DPVO:
         enqueueing its frame's encoders -- the GPU runs them while the host
         waits for the copy and launches the bookkeeping, instead of idling.
         The state is the reference's once the decision is applied: by the next
-        __call__, terminate(), flush_keyframe() or any accessor that reads it."""
+        __call__, update(), update_graphed(), terminate(), terminate_keyframe(),
+        global_bundle_adjustment(), get_pts_clr_intri(), get_pose() or
+        flush_keyframe().  The plain state views (n, m, poses, patches, pg.*)
+        do NOT apply it: call flush_keyframe() before reading them."""
         self.flush_keyframe()
         pend = self._keyframe_begin()
         if getattr(self.cfg, "DEFER_KEYFRAME", False):

@@ -59,6 +59,19 @@ def _dim_size(index, dim_size):
     return int(index.max().item()) + 1 if index.numel() else 0
 
 
+def _check_range(index, dim_size=None):
+    """torch_scatter 2.1.2 fails on an index outside [0, dim_size) (an
+    index-out-of-bounds error); the CSR kernel would skip such members
+    silently, so the range is checked first.  One host read: this module is
+    the compatibility surface, the tracker's SoftAgg does not come through it."""
+    if index.numel() == 0:
+        return
+    lo, hi = torch.stack([index.min(), index.max()]).tolist()
+    if lo < 0 or (dim_size is not None and hi >= dim_size):
+        raise IndexError(f"torch_scatter (HIP): index out of range (min {lo}, max {hi}) for an output of "
+                         f"{dim_size if dim_size is not None else 'inferred'} rows")
+
+
 def _reduce(op, src, index, dim, out, dim_size):
     dim, src3, index, outer, E, inner = _prep(src, index, dim)
     if out is None:
@@ -69,6 +82,7 @@ def _reduce(op, src, index, dim, out, dim_size):
         if out.dtype != src.dtype or not out.is_contiguous():
             raise RuntimeError("torch_scatter (HIP): out must be contiguous and of src's dtype")
         dim_size = out.shape[dim]
+    _check_range(index, dim_size)
     if E:
         U.scatter_csr(op, src3, index, U.group_by(index), out, out_rows=dim_size)
     return out
@@ -94,6 +108,7 @@ def scatter_max(src, index, dim=-1, out=None, dim_size=None):
     shape = _out_shape(src, dim, dim_size)
     out = torch.zeros(shape, dtype=src.dtype, device=src.device)
     arg = torch.full(shape, E, dtype=torch.int64, device=src.device)
+    _check_range(index, dim_size)
     if E:
         U.scatter_csr(U.SCATTER_MAX, src3, index, U.group_by(index), out, out_rows=dim_size, argmax=arg)
     return out, arg
@@ -102,6 +117,7 @@ def scatter_max(src, index, dim=-1, out=None, dim_size=None):
 def scatter_softmax(src, index, dim=-1, eps=1e-12, dim_size=None):
     dim, src3, index, outer, E, inner = _prep(src, index, dim)
     out = torch.empty_like(src3)
+    _check_range(index)
     if E:
         U.scatter_csr(U.SCATTER_SOFTMAX, src3, index, U.group_by(index), out, eps=eps)
     return out.view(src.shape)
