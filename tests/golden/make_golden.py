@@ -276,11 +276,14 @@ def ba_fixtures(ba, lie):
 # ----------------------------------------------------------------------------
 # altcorr: torch-CPU float16 restatement of correlation_kernel.cu
 # ----------------------------------------------------------------------------
-def torch_corr_f16(fmap1, fmap2, coords, ii, jj, radius):
+def torch_corr_f16(fmap1, fmap2, coords, ii, jj, radius, dtype=torch.float16):
     """correlation_kernel.cu:83-135 with c10::Half arithmetic (each product
     and each sum rounded to binary16), then the reference's ATen epilogue
     (:221-232) verbatim on float16 tensors.  Returns the returned view
-    (permuted) as a contiguous tensor [B,E,2r+1(x),2r+1(y),H,W]."""
+    (permuted) as a contiguous tensor [B,E,2r+1(x),2r+1(y),H,W].
+    dtype=torch.float64: the same sums and epilogue in float64 (the exact
+    answer for fp16 inputs)."""
+    fmap1, fmap2 = fmap1.to(dtype), fmap2.to(dtype)
     R, D = radius, 2 * radius + 2
     B, M, _, H, W = coords.shape
     C, H2, W2 = fmap1.shape[2], fmap2.shape[3], fmap2.shape[4]
@@ -292,20 +295,20 @@ def torch_corr_f16(fmap1, fmap2, coords, ii, jj, radius):
     j1 = fx[..., None, None] + (b - R)
     inb = (i1 >= 0) & (i1 < H2) & (j1 >= 0) & (j1 < W2)
     i1c, j1c = i1.clamp(0, H2 - 1), j1.clamp(0, W2 - 1)
-    s = torch.zeros(B, M, H, W, D, D, dtype=torch.float16)
+    s = torch.zeros(B, M, H, W, D, D, dtype=dtype)
     bidx = torch.arange(B).view(B, 1, 1, 1, 1, 1)
     jx = jj.view(1, M, 1, 1, 1, 1)
     f1 = fmap1[torch.arange(B).view(B, 1), ii.view(1, M)]  # [B,M,C,H,W]
     for c in range(C):
         f2 = fmap2[bidx, jx, c, i1c, j1c]  # [B,M,H,W,D,D]
         s = s + f1[:, :, c, :, :, None, None] * f2
-    s = torch.where(inb, s, torch.zeros((), dtype=torch.float16))
+    s = torch.where(inb, s, torch.zeros((), dtype=dtype))
     corr = s.permute(0, 1, 4, 5, 2, 3).contiguous()  # [B,M,D(a),D(b),H,W]
     # --- the reference's ATen epilogue, correlation_kernel.cu:221-232 ---
     xx = coords[:, :, 0, None, None]
     yy = coords[:, :, 1, None, None]
-    dx = xx - xx.floor(); dx = dx.to(torch.float16)
-    dy = yy - yy.floor(); dy = dy.to(torch.float16)
+    dx = xx - xx.floor(); dx = dx.to(dtype)
+    dy = yy - yy.floor(); dy = dy.to(dtype)
     out = (1 - dx) * (1 - dy) * corr[:, :, 0:D - 1, 0:D - 1]
     out += (dx) * (1 - dy) * corr[:, :, 0:D - 1, 1:D]
     out += (1 - dx) * (dy) * corr[:, :, 1:D, 0:D - 1]
@@ -465,10 +468,130 @@ def encoder_fixtures():
     print("encoders: reference BasicEncoder4 vectors saved")
 
 
+def update_step_fixtures(pops, ba, lie, dscale=None, save=True):
+    """One whole DPVO.update() (dpvo.py:711-749) of the reference from the
+    injected steady-state graph of net_inputs.update_step_state(), through the
+    reference's own modules:
+      reproject  = projective_ops.transform (+ the permute of dpvo.py:338),
+      corr       = the CUDA-only altcorr restated (torch_corr_f16, both levels,
+                   coords / 1 and / 4, ring slots kk % (M pmem), jj % pmem,
+                   dpvo.py:326-333),
+      ctx        = imap[:, kk % (M pmem)]  (dpvo.py:718),
+      network    = net.Update on the update_ref.npz weights,
+      target     = coords[..., 1, 1] + delta, weight  (dpvo.py:722-724),
+      BA         = ba.py with the fastba argument mapping, twice,
+                   t0 = n - OPTIMIZATION_WINDOW (dpvo.py:730-734),
+      points     = projective_ops.point_cloud centre / w (dpvo.py:747-749).
+    Run twice: "f64" in float64 throughout (the exact answer for these inputs)
+    and "r16" with the reference's own precisions (fp16 altcorr chain, Update
+    under fp16 autocast, fp32 BA) -- its distance from f64 is the reference's
+    own error at this state.  The C oracle's restatement of ba_cuda.cu is run
+    on the r16 targets as a cross-check of the ba.py mapping."""
+    net_mod = importlib.import_module("dpvo.net")
+    S = NI.update_step_state()
+    C = NI.STEP
+    n, M, pmem = C["n"], C["M"], C["pmem"]
+    m = n * M
+    t0 = n - C["opt_window"]
+    torch.manual_seed(0)
+    upd = net_mod.Update(3)
+    spec = NI.spec_json(upd.state_dict())
+    _load(upd, spec, NI.UPDATE_SEED)
+    dscale = NI.STEP_DSCALE if dscale is None else dscale
+    with torch.no_grad():   # the delta head scaled (net_inputs.STEP_DSCALE): see there
+        upd.d[1].weight.mul_(dscale)
+        upd.d[1].bias.mul_(dscale)
+    upd.eval()
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    ii, jj, kk = T(S["ii"]), T(S["jj"]), T(S["kk"])
+    E = len(ii)
+    gmap = T(S["gmap"]).view(1, pmem * M, 128, 3, 3)
+    fmap1, fmap2 = T(S["fmap1"])[None], T(S["fmap2"])[None]
+    imap = T(S["imap"]).view(1, pmem * M, 384)
+    ix = torch.arange(C["N"]).repeat_interleave(M)
+    rows = NI.update_rows(E)[::4]
+    crow = rows[::3]
+    cx, cy = C["intrinsics"][2], C["intrinsics"][3]
+    bounds = [-64, -64, 2 * cx + 64, 2 * cy + 64]
+    out = dict(seed=np.int64(NI.STEP_SEED), dscale=np.float64(dscale), update_seed=np.int64(NI.UPDATE_SEED), spec=np.array(spec),
+               t0=np.int64(t0), n=np.int64(n), rows=rows, corr_rows=crow,
+               state_checksum=np.stack([NI.checksum(S[k]) for k in sorted(S)]))
+    touched = np.unique(S["kk"])
+    out["touched"] = touched
+    res = {}
+    for mode, dt, cdt in (("f64", torch.float64, torch.float64), ("r16", torch.float32, torch.float16)):
+        poses = T(S["poses"]).to(dt)[None]
+        patches = T(S["patches"]).to(dt)[None]
+        intr = T(S["intrinsics"]).to(dt)[None]
+        with torch.no_grad():
+            coords = pops.transform(lie.SE3(poses), patches, intr, ii, jj, kk)
+            coords = coords.permute(0, 1, 4, 2, 3).contiguous()          # DPVO.reproject
+            ii1, jj1 = kk % (M * pmem), jj % pmem
+            corr1 = torch_corr_f16(gmap, fmap1, coords / 1, ii1, jj1, 3, dtype=cdt)
+            corr2 = torch_corr_f16(gmap, fmap2, coords / 4, ii1, jj1, 3, dtype=cdt)
+            corr = torch.stack([corr1, corr2], -1).view(1, E, -1)
+            ctx = imap[:, kk % (M * pmem)]
+            net = T(S["net"])[None]
+            if mode == "f64":
+                u64 = copy.deepcopy(upd).double()
+                net_o, (delta, weight, _) = u64(net.double(), ctx.double(), corr, None, ii, jj, kk)
+            else:
+                with torch.autocast("cpu", dtype=torch.float16):
+                    net_o, (delta, weight, _) = upd(net, ctx, corr, None, ii, jj, kk)
+            weight = weight.to(dt)
+            target = coords[..., 1, 1] + delta.to(dt)
+            Gs, pt = lie.SE3(poses.clone()), patches.clone()
+            est = torch.zeros_like(pt)
+            for _ in range(2):
+                Gs, pt = ba.BA(Gs, pt, intr, target, weight, 1e-4, ii, jj, kk, bounds, ep=1.0, fixedp=t0,
+                               structure_only=False, patches_est=est)
+                dep = pt[0, touched, 2].numpy()
+                print(f"update_step {mode}: touched depths in [{dep.min():.4g}, {dep.max():.4g}]")
+                assert dep.min() > 1e-3 and dep.max() < 10.0, (mode, dep.min(), dep.max())   # SURVEY 8c (i)
+            pc = pops.point_cloud(Gs, pt[:, :m], intr, ix[:m])
+            points = (pc[..., 1, 1, :3] / pc[..., 1, 1, 3:]).reshape(-1, 3)
+        r = dict(poses=Gs.data[0].numpy().astype(np.float64), depth=pt[0, touched, 2, 1, 1].numpy().astype(np.float64),
+                 points=points.numpy().astype(np.float64), net=net_o[0].float().numpy()[rows].astype(np.float64),
+                 delta=delta[0].float().numpy().astype(np.float64),
+                 weight=weight[0].float().numpy().astype(np.float64),
+                 target=target[0].numpy().astype(np.float64), corr=corr[0].numpy()[crow])
+        res[mode] = r
+        for k in ("poses", "depth", "points", "net", "delta", "weight", "target"):
+            small = k in ("poses", "depth", "points") and mode == "f64"
+            out[f"{mode}_{k}"] = r[k] if small else r[k].astype(np.float32)
+        if mode == "r16":
+            # the C restatement of ba_cuda.cu on the same fp32 targets / weights
+            rp, rq, st = oracle.ba_forward(S["poses"], S["patches"], S["intrinsics"], target.numpy(),
+                                           weight.numpy(), 1e-4, S["ii"], S["jj"], S["kk"], t0, n, 2)
+            assert st == 0
+            dpose = np.abs(rp[t0:n] - r["poses"][t0:n]).max()
+            ddep = np.abs(rq[touched, 2, 1, 1] - r["depth"]).max()
+            print(f"update_step: ba.py vs the oracle's ba_cuda restatement: poses {dpose:.3g}, depths {ddep:.3g}")
+            assert dpose < 1e-4 and ddep < 1e-4
+    out["f64_corr"] = res["f64"]["corr"].astype(np.float32)   # exact corr rows (fp16 inputs, fp64 sums)
+    for k in ("poses", "depth", "points", "net", "delta", "weight", "target"):
+        a, b = res["r16"][k], res["f64"][k]
+        if k == "poses":
+            a, b = a[t0:n], b[t0:n]
+        rel = np.abs(a - b) / (np.abs(b) + 1e-12)
+        nrm = np.linalg.norm(a - b) / np.linalg.norm(b)
+        extra = ""
+        if k == "points":
+            pp = np.linalg.norm(a - b, axis=1) / np.linalg.norm(b, axis=1)
+            extra = f", per point max {pp.max():.3g}"
+        print(f"update_step: reference fp16 path vs float64, {k}: max abs {np.abs(a - b).max():.3g}, "
+              f"max rel (|x| > 1e-3) {rel[np.abs(b) > 1e-3].max():.3g}, norm-wise {nrm:.3g}{extra}")
+        out[f"r16_err_{k}"] = _err_stats(a, b)
+    moved = np.abs(res["f64"]["poses"][t0:n] - S["poses"][t0:n]).max()
+    print(f"update_step: E = {E}, window poses moved by up to {moved:.3g}; fixture saved")
+    if save:
+        np.savez_compressed(os.path.join(HERE, "update_step_ref.npz"), **out)
+
+
 if __name__ == "__main__":
-    # python make_golden.py [part ...]: parts lietorch, pops, ba, altcorr, neighbors, update, encoder
+    # python make_golden.py [part ...]: parts lietorch, pops, ba, altcorr, neighbors, update, encoder, step
     torch.set_num_threads(8)
-    parts = set(sys.argv[1:]) or {"lietorch", "pops", "ba", "altcorr", "neighbors", "update", "encoder"}
+    parts = set(sys.argv[1:]) or {"lietorch", "pops", "ba", "altcorr", "neighbors", "update", "encoder", "step"}
     pops, ba, lie = import_reference()
     if "lietorch" in parts:
         lietorch_fixtures(lie)
@@ -484,3 +607,5 @@ if __name__ == "__main__":
         update_fixtures()
     if "encoder" in parts:
         encoder_fixtures()
+    if "step" in parts:
+        update_step_fixtures(pops, ba, lie)

@@ -121,3 +121,90 @@ def encoder_rows(h):
 def checksum(a):
     a = np.asarray(a, np.float64)
     return np.array([a.sum(), np.abs(a).sum(), (a * np.arange(a.size).reshape(a.shape) % 7).sum()])
+
+
+# ----------------------------------------------------------------------------
+# one whole DPVO.update() (dpvo.py:711-749) from an injected steady-state
+# patch graph: update_step_ref.npz
+# ----------------------------------------------------------------------------
+STEP_SEED = 51
+# the Update's delta head (d.1, net.py:66) scaled by this factor for the
+# update_step fixture: seeded random weights put ~1 px of incoherent noise on
+# every target, and two Gauss-Newton steps then drive a few poorly observed
+# patches' inverse depths into fastba's / ba.py's different clamps (SURVEY 8c
+# (i)), where the reference's two BA implementations disagree by design
+STEP_DSCALE = 0.25
+# default.yaml (REMOVAL_WINDOW 22, OPTIMIZATION_WINDOW 10, PATCH_LIFETIME 13)
+# with M = 12 patches per frame, a 48-frame buffer, n = 40 keyframes (the
+# 36-slot feature rings wrap), 128 x 96 frames (32 x 24 feature maps)
+STEP = dict(n=40, M=12, N=48, pmem=36, ht=96, wd=128, lifetime=13, removal=22, opt_window=10,
+            intrinsics=(20.0, 20.0, 16.0, 12.0))
+
+
+def _qmul(a, b):
+    """Hamilton product of [x, y, z, w] quaternions"""
+    ax, ay, az, aw = a
+    bx, by, bz, bw = b
+    return np.array([aw * bx + ax * bw + ay * bz - az * by, aw * by - ax * bz + ay * bw + az * bx,
+                     aw * bz + ax * by - ay * bx + az * bw, aw * bw - ax * bx - ay * by - az * bz])
+
+
+def step_edges(n, M, lifetime, removal):
+    """the edge set update() sees at n keyframes in steady state: the append
+    rules of dpvo.py:756-769 for the recent frames, then the removal rule of
+    dpvo.py:657 as of the previous keyframe (dpvo/synthetic.py restated)"""
+    ii, jj, kk = [], [], []
+    for t in range(max(1, n - removal - 2), n + 1):
+        for k in range(M * max(t - lifetime, 0), M * max(t - 1, 0)):
+            ii.append(k // M); jj.append(t - 1); kk.append(k)
+        for k in range(M * (t - 1), M * t):
+            for j in range(max(t - lifetime, 0), t):
+                ii.append(k // M); jj.append(j); kk.append(k)
+    ii, jj, kk = (np.asarray(a, np.int64) for a in (ii, jj, kk))
+    keep = ii >= n - 1 - removal
+    return ii[keep], jj[keep], kk[keep]
+
+
+def update_step_state(seed=STEP_SEED):
+    """Every input of one update(): poses [N][7] (rows >= n zero), patches
+    [N*M][3][3][3], intrinsics [N][4] (all fp32), the fp16 rings fmap1
+    [pmem][128][h][w], fmap2 [pmem][128][h/4][w/4] (4x4 average of fmap1),
+    gmap [pmem][M][128][3][3] (3x3 windows of fmap1 at the patch centres, the
+    Patchifier's patchify), imap [pmem][M][384], the edges ii / jj / kk and the
+    fp32 edge state net [E][384]."""
+    S = STEP
+    n, M, N, pmem = S["n"], S["M"], S["N"], S["pmem"]
+    h, w = S["ht"] // 4, S["wd"] // 4
+    g = np.random.default_rng(seed)
+    poses = np.zeros((N, 7), np.float64)
+    poses[0, 6] = 1.0
+    for i in range(1, n):
+        dq = np.concatenate([0.5 * g.normal(0, 0.01, 3), [1.0]])
+        q = _qmul(dq / np.linalg.norm(dq), poses[i - 1, 3:])
+        poses[i, 3:] = q / np.linalg.norm(q)
+        poses[i, :3] = poses[i - 1, :3] + g.normal(0, 0.05, 3)
+    xs = g.integers(1, w - 1, size=(n, M)).astype(np.float64)
+    ys = g.integers(1, h - 1, size=(n, M)).astype(np.float64)
+    d = g.uniform(0.2, 1.0, size=(n, M))
+    patches = np.zeros((N, M, 3, 3, 3))
+    off = np.arange(3) - 1.0
+    patches[:n, :, 0] = xs[:, :, None, None] + off[None, None, None, :]
+    patches[:n, :, 1] = ys[:, :, None, None] + off[None, None, :, None]
+    patches[:n, :, 2] = d[:, :, None, None]
+    intrinsics = np.zeros((N, 4))
+    intrinsics[:n] = S["intrinsics"]
+    fmap1 = (0.25 * g.standard_normal((pmem, 128, h, w))).astype(np.float16)
+    fmap2 = fmap1.astype(np.float32).reshape(pmem, 128, h // 4, 4, w // 4, 4).mean((3, 5)).astype(np.float16)
+    gmap = np.zeros((pmem, M, 128, 3, 3), np.float16)
+    imap = np.zeros((pmem, M, 384), np.float16)
+    for f in range(n - pmem, n):
+        s = f % pmem
+        for p in range(M):
+            x, y = int(xs[f, p]), int(ys[f, p])
+            gmap[s, p] = fmap1[s, :, y - 1:y + 2, x - 1:x + 2]
+        imap[s] = g.standard_normal((M, 384)).astype(np.float16)
+    ii, jj, kk = step_edges(n, M, S["lifetime"], S["removal"])
+    net = (0.1 * g.standard_normal((len(ii), 384))).astype(np.float32)
+    return dict(poses=poses.astype(np.float32), patches=patches.reshape(N * M, 3, 3, 3).astype(np.float32),
+                intrinsics=intrinsics.astype(np.float32), fmap1=fmap1, fmap2=fmap2, gmap=gmap, imap=imap,
+                ii=ii, jj=jj, kk=kk, net=net)

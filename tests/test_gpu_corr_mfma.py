@@ -131,3 +131,35 @@ def test_edge_order_is_a_grouped_permutation_and_changes_nothing():
     a = cuda_corr.forward_pyramid_mfma(*args)
     b = cuda_corr.forward_pyramid_mfma(*args, order=order)
     assert torch.equal(a, b)
+
+
+def test_tracker_corr_c3_window_order_vs_oracle_exact():
+    """DPVO.corr at C3 (2048-KF buffer, n = 2040, E = 95,424) exactly as
+    update() calls it -- ring slots and the visiting order from the per-update
+    window group-by (dpvo_window_group_by, jj_order) -- against the oracle's
+    exact mode (fp16 inputs, fp64 sums) on a 480-edge sample, at the
+    small-size bound: every output within the final fp16 rounding, RMS no
+    worse than the reference's fp16 chain."""
+    import update_ops
+    from dpvo.synthetic import steady_state_tracker
+    slam = steady_state_tracker("dpvo_2k", buffer=2048, seed=4)
+    E = slam.pg.ii.numel()
+    assert E == 95424
+    with torch.no_grad():
+        coords = slam.reproject()
+        ctx, jslot, _, _, order = update_ops.window_group_by(
+            slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M, slam.n - 64, slam.M * slam.pmem, slam.pmem,
+            flag=slam._ba_status, jj_order=True)
+        corr = slam.corr(coords, slots=(ctx, jslot), order=order)
+    torch.cuda.synchronize()
+    assert int(slam._ba_status.item()) == 0
+    o = order.cpu().numpy()
+    assert np.array_equal(np.sort(o), np.arange(E))
+    sel = np.unique(np.concatenate([np.linspace(0, E - 1, 400).astype(np.int64), o[:40], o[-40:]]))
+    c = coords[0].cpu().numpy()[sel][None]
+    fm = [slam.fmap1_.contiguous().cpu().numpy(), slam.fmap2_.contiguous().cpu().numpy()]
+    args = (slam.gmap.cpu().numpy(), fm, c, ctx.cpu().numpy()[sel], jslot.cpu().numpy()[sel])
+    exact = oracle.corr_pyramid(*args, mode=oracle.F16_ACC64)
+    ref16 = oracle.corr_pyramid(*args)
+    mine, ref = check(corr[0].cpu().numpy()[sel][None], exact, ref16)
+    print(f"C3 tracker order, {len(sel)} edges: rms vs exact {mine:.3g} (reference fp16 chain {ref:.3g})")

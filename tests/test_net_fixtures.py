@@ -122,3 +122,61 @@ def test_encoder_mirror_float64_matches_reference(frame):
     np.testing.assert_allclose(fmap[:, f[f"f{frame}_rows"]], f[f"f{frame}_fmap"], rtol=1e-5, atol=1e-6)
     xs, ys = f[f"f{frame}_xs"], f[f"f{frame}_ys"]
     np.testing.assert_allclose(imap[:, ys, xs].T, f[f"f{frame}_imap"], rtol=1e-5, atol=1e-6)
+
+
+def test_update_step_inputs_regenerate():
+    """update_step_ref.npz's inputs come back bit for bit from their seed
+    (the GPU test regenerates them instead of loading 20 MB of state), and the
+    fixture's edge set is the steady state the tracker sees (497 M edges)"""
+    f = np.load(os.path.join(GOLDEN, "update_step_ref.npz"))
+    S = NI.update_step_state(int(f["seed"]))
+    got = np.stack([NI.checksum(S[k]) for k in sorted(S)])
+    np.testing.assert_allclose(got, f["state_checksum"], rtol=1e-12, atol=0)
+    assert len(S["ii"]) == 497 * NI.STEP["M"]
+    assert np.array_equal(f["touched"], np.unique(S["kk"]))
+
+
+def test_update_step_oracle_chain_matches_reference(monkeypatch):
+    """the CPU restatement of the whole update() -- oracle.transform, the
+    oracle's exact altcorr (F16_ACC64), the mirror Update in float64, the
+    oracle's ba_cuda.cu restatement, the oracle's point cloud -- reproduces the
+    reference modules' float64 update_step fixture: the oracle chain the GPU
+    kernels are tested against is itself pinned end to end."""
+    from oracle import oracle
+    from dpvo import fastba
+    from dpvo.net import Update
+    f = np.load(os.path.join(GOLDEN, "update_step_ref.npz"))
+    S = NI.update_step_state(int(f["seed"]))
+    C = NI.STEP
+    n, M, pmem, t0 = C["n"], C["M"], C["pmem"], int(f["t0"])
+    m = n * M
+    ii, jj, kk = S["ii"], S["jj"], S["kk"]
+    E = len(ii)
+    coords = oracle.transform(S["poses"], S["patches"], S["intrinsics"], ii, jj, kk)[0].transpose(0, 3, 1, 2)
+    corr = oracle.corr_pyramid(S["gmap"].reshape(1, pmem * M, 128, 3, 3), [S["fmap1"][None], S["fmap2"][None]],
+                               coords[None], kk % (M * pmem), jj % pmem, mode=oracle.F16_ACC64)[0]
+    np.testing.assert_allclose(corr[f["corr_rows"]], f["f64_corr"], rtol=1e-5, atol=1e-5)
+    upd = Update(3)
+    _load(upd, str(f["spec"]), int(f["update_seed"]))
+    with torch.no_grad():
+        upd.d[1].weight.mul_(float(f["dscale"]))
+        upd.d[1].bias.mul_(float(f["dscale"]))
+    upd = upd.double()
+    monkeypatch.setattr(fastba, "neighbors", _neighbors_cpu)
+    ctx = S["imap"].reshape(pmem * M, 384)[kk % (M * pmem)]
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a))
+    # the torch path with autograd on (the inference path's SoftAgg is the HIP kernel)
+    net0 = T(S["net"]).double()[None].requires_grad_(True)
+    net, (d, w, _) = upd(net0, T(ctx).double()[None], T(corr).double()[None], None, T(ii), T(jj), T(kk))
+    net, d, w = net.detach(), d.detach(), w.detach()
+    np.testing.assert_allclose(net[0].numpy()[f["rows"]], f["f64_net"], rtol=1e-5, atol=1e-5)
+    target = coords[:, :, 1, 1] + d[0].numpy()
+    np.testing.assert_allclose(target, f["f64_target"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(w[0].numpy(), f["f64_weight"], rtol=1e-5, atol=1e-6)
+    poses, patches, st = oracle.ba_forward(S["poses"], S["patches"], S["intrinsics"], target, w[0].numpy(), 1e-4,
+                                           ii, jj, kk, t0, n, 2)
+    assert st == 0
+    np.testing.assert_allclose(poses[t0:n], f["f64_poses"][t0:n], rtol=1e-4, atol=2e-6)
+    np.testing.assert_allclose(patches[f["touched"], 2, 1, 1], f["f64_depth"], rtol=1e-4)
+    pts = oracle.point_cloud_centre(poses, patches[:m], S["intrinsics"], np.arange(m) // M)
+    np.testing.assert_allclose(pts, f["f64_points"], rtol=1e-4, atol=1e-5)
