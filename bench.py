@@ -208,12 +208,25 @@ class CorrProbe:
         return float(np.mean(ts)) if ts else 0.0
 
 
+def _gpu_head_start(ms=2.0):
+    """Keep the device busy for ~ms so the host enqueues the launches that
+    follow ahead of it: event gaps then measure back-to-back device time, not
+    the host's launch pace (small phases otherwise read as Python + ctypes
+    enqueue time whenever the GPU has drained)."""
+    try:
+        torch.cuda._sleep(int(ms * 2.0e6))   # ~2 GHz shader clock
+    except (AttributeError, RuntimeError):
+        pass
+
+
 def phase_breakdown(slam, reps=5):
     """Per-phase device time of one update, measured with events outside the
     timed loop.  The phases follow DPVO.update() (dpvo/dpvo.py) step by step,
-    with the same arguments: reproject; the window keys and both group-bys;
-    altcorr (edge ordering + the fused kernel); the update operator; the BA
-    targets + fastba; the point cloud."""
+    with the same arguments: reproject; the window keys, both group-bys and
+    altcorr's visiting order (dpvo_window_group_by, jj_order); altcorr (the
+    fused matrix-core kernel in that order); the update operator; the BA
+    targets + fastba; the point cloud.  Each rep starts behind a device-side
+    delay, so the phases run back to back as in the timed loop."""
     import update_ops
     from dpvo import fastba
     from dpvo import projective_ops as pops
@@ -225,15 +238,16 @@ def phase_breakdown(slam, reps=5):
     for _ in range(reps):
         slam._ba_status.zero_()
         e = [ev() for _ in range(len(names) + 1)]
+        _gpu_head_start()
         e[0].record()
         coords = slam.reproject()
         e[1].record()
-        ctx_idx, jslot, kk_groups, ij_groups = update_ops.window_group_by(
+        ctx_idx, jslot, kk_groups, ij_groups, order = update_ops.window_group_by(
             slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M, slam.n - 64, slam.M * slam.pmem, slam.pmem,
-            flag=slam._ba_status)
+            flag=slam._ba_status, jj_order=True)
         e[2].record()
         with torch.autocast("cuda", enabled=True):
-            corr = slam.corr(coords, slots=(ctx_idx, jslot))
+            corr = slam.corr(coords, slots=(ctx_idx, jslot), order=order)
             e[3].record()
             net, (delta, weight, _) = slam.network.update(slam.pg.net, slam.imap, corr, None, slam.pg.ii, slam.pg.jj,
                                                           slam.pg.kk, inp_idx=ctx_idx,
@@ -253,7 +267,50 @@ def phase_breakdown(slam, reps=5):
         for k, (a, b) in zip(acc, zip(e[:-1], e[1:])):
             acc[k].append(a.elapsed_time(b))
     slam.check_ba(int(slam._ba_status.item()))
-    return {k: round(float(np.median(v)), 4) for k, v in acc.items()}
+    out = {k: round(float(np.median(v)), 4) for k, v in acc.items()}
+    return out
+
+
+def gmap_pack_ms(slam, reps=5):
+    """The matrix-core altcorr's gmap table (dpvo_corr_pack_mfma): packed once
+    per NEW keyframe by DPVO.corr (the ring's version changed), so it belongs
+    to the frame ingest, not to update(); timed here for the end-to-end
+    account."""
+    import cuda_corr
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        _gpu_head_start(0.5)
+        a.record()
+        cuda_corr.pack_mfma(slam.gmap, out=slam._gtab)
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b))
+    return round(float(np.median(ts)), 4)
+
+
+def host_cost(slam, reps=6):
+    """Host CPU per eager update(): the Python thread's CPU time (launches,
+    ctypes, torch dispatch) against the GPU time of the same update, from
+    updates run back to back behind a device-side delay (so the host never
+    waits for the device inside the measured span).  Decides whether several
+    ranks sharing this host would be launch-bound (8 ranks: > 1/8 of the
+    step)."""
+    slam.update()
+    torch.cuda.synchronize()
+    _gpu_head_start(20.0)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    c0 = time.thread_time()
+    a.record()
+    for _ in range(reps):
+        slam.update()
+    b.record()
+    c1 = time.thread_time()
+    torch.cuda.synchronize()
+    thread_ms = (c1 - c0) / reps * 1e3
+    gpu_ms = a.elapsed_time(b) / reps
+    return {"thread_ms": round(thread_ms, 4), "gpu_ms": round(gpu_ms, 4),
+            "ranks_per_host_before_launch_bound": round(gpu_ms / max(thread_ms, 1e-6), 1)}
 
 
 def load_counters(path, edges):
@@ -290,7 +347,8 @@ def roofline_lines(slam, corr_ms, order_ms, breakdown, counters, path):
     phase_ms = corr_ms + order_ms
     alg = CORR_BYTES_PER_EDGE * E
     corr = {"kernel": ("corr_sfast_kernel<2,16> (bit-exact fp16-chain altcorr)" if slam.cfg.EXACT_CORR
-                       else "corr_mfma_kernel (2-level altcorr on the matrix cores) + edge_order"),
+                       else "corr_mfma_kernel (2-level altcorr on the matrix cores, edges in the window "
+                            "group-by's target-frame order)"),
             "unit": "GB/s", "peak": HBM_PEAK_GBS, "avg_launch_ms": round(phase_ms, 5),
             "kernel_ms": round(corr_ms, 5), "edge_order_ms": round(order_ms, 5),
             "algorithmic_bytes": alg, "algorithmic_GBs": round(alg / (phase_ms * 1e-3) / 1e9, 1),
@@ -534,30 +592,40 @@ def main():
     # warmup and replays it (the patch graph does not change between steps);
     # measured no faster on one GPU (2.78 vs 2.71 ms/step at C3), so eager is
     # the default and the corr events below time every launch live
-    upd = slam.update_graphed if args.graph else slam.update
     with torch.no_grad():
-        for _ in range(max(args.warmup, 2 if args.graph else 0)):
+        host = host_cost(slam)
+    # several ranks share one host: when one eager update() costs the host more
+    # than 1/8 of its GPU time, 8 ranks would be launch-bound -- replay it from
+    # a HIP graph instead (one launch per step)
+    graph = args.graph or (world > 1 and host["thread_ms"] > host["gpu_ms"] / 8)
+    upd = slam.update_graphed if graph else slam.update
+    with torch.no_grad():
+        for _ in range(max(args.warmup, 2 if graph else 0)):
             upd()
         probe.clear()
         barrier(world)
         torch.cuda.synchronize()
+        c0, p0 = time.thread_time(), time.process_time()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             upd()
         torch.cuda.synchronize()
         barrier(world)
         elapsed = time.perf_counter() - t0
+        c1, p1 = time.thread_time(), time.process_time()
         # every timed launch (eager); with --graph the captured launches are
         # not evented (ROCm torch has no event-record nodes), so the probe
         # falls back to a short eager pass after the loop
         corr_ms, order_ms = probe.mean_ms("corr"), probe.mean_ms("order")
-        if args.graph:
+        if graph:
             for _ in range(3):
                 slam.update()
             torch.cuda.synchronize()
             corr_ms, order_ms = probe.mean_ms("corr"), probe.mean_ms("order")
         slam.check_ba()
         breakdown = phase_breakdown(slam)
+        if not slam.cfg.EXACT_CORR:
+            breakdown["ingest_gmap_pack"] = gmap_pack_ms(slam)
 
     gather_ms = None
     if world > 1:
@@ -578,7 +646,7 @@ def main():
             "metric": metric, "value": round(value, 3), "unit": "keyframes/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f16+f32",
-            "launch": "hip-graph replay of update()" if args.graph else "eager",
+            "launch": "hip-graph replay of update()" if graph else "eager",
             "data": "synthetic (seeded steady-state patch graph, random-init VONet weights)",
             "config": {"workload": f"{cfgd['name']}: M={slam.M}, {args.buffer}-KF buffer, n={slam.n} keyframes, "
                                    f"E={E} edges, 512x384, {slam.cfg.BA_ITERATIONS} BA iterations",
@@ -590,6 +658,9 @@ def main():
             "breakdown_ms": breakdown,
             "fastba_us_per_iteration": round(breakdown["fastba"] * 1e3 / slam.cfg.BA_ITERATIONS, 2),
             "host_cores": {"rank0": _core_str(args.cores), "cpu_model": _cpu_model()},
+            "host_ms_per_step": round((c1 - c0) / args.steps * 1e3, 4),
+            "host_process_ms_per_step": round((p1 - p0) / args.steps * 1e3, 4),
+            "host_calibration": host,
         }
         if gather_ms is not None:
             line["gather_ms"] = gather_ms
