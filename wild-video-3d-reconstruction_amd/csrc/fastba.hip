@@ -30,6 +30,8 @@
 
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace dpvo {
 
 // ---------------------------------------------------------------------------
@@ -1564,11 +1566,12 @@ static size_t nb_sort_temp_bytes(int64_t E)
 constexpr int BD_NMAX = 12;
 constexpr int BD_N6MAX = 6 * BD_NMAX;     // 72
 constexpr int BD_WAVES = 4;
+constexpr int BD_HD_LD = 64;   // row pitch of the dense lower-triangle system the wave solver loads
 constexpr int BD_GRID = 512;    // 4 waves each (measured over 256-2048: 512 is fastest at C3 and C2, scripts/exp_bd_grid.sh)
 static int bd_grid() { return BD_GRID; }
 
 struct BdLayout {
-    size_t hdr, gid, offs, perm, groups, gbws, gbws_bytes, Em, Cg, ug, Hpart, H, dX, total;
+    size_t hdr, gid, offs, perm, groups, gbws, gbws_bytes, Em, Cg, ug, Hpart, H, Hd, dX, total;
     int64_t mu_max;
     int n6, nup, ent;
 };
@@ -1595,6 +1598,7 @@ static BdLayout bd_layout(int64_t E, int64_t num_patches, int N)
     L.ug = take((size_t)L.mu_max * 4);
     L.Hpart = take((size_t)BD_GRID * std::max(L.ent, 1) * 4);
     L.H = take((size_t)std::max(L.ent, 1) * 4);
+    L.Hd = take((size_t)64 * BD_HD_LD * 4);
     L.dX = take((size_t)std::max(L.n6, 1) * 4);
     L.total = off;
     return L;
@@ -1616,7 +1620,7 @@ struct BdParams {
     const int* perm;
     const int64_t* groups;
     int* status;
-    float *Em, *Cg, *ug, *Hpart, *H, *dX;
+    float *Em, *Cg, *ug, *Hpart, *H, *Hd, *dX;
 };
 
 // row-major upper triangle of the n6 x n6 system, a <= b
@@ -1961,7 +1965,9 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
     }
 }
 
-// H = sum of the patch kernel's workgroup partials, fixed order
+// H = sum of the patch kernel's workgroup partials, fixed order.  Also stored
+// as dense rows for the wave solver: Hd[b][a] = H(a, b) (a <= b, the lower
+// triangle, row pitch BD_HD_LD) and row n6 = g.
 __global__ __launch_bounds__(1024) void bd_reduce_kernel(BdParams p, int nparts)
 {
     __shared__ float red[16][64];
@@ -1980,6 +1986,20 @@ __global__ __launch_bounds__(1024) void bd_reduce_kernel(BdParams p, int nparts)
 #pragma unroll
         for (int w = 0; w < 16; w++) t += red[w][lane];
         p.H[i] = t;
+        const int n = p.n6;
+        int a = 0, b;
+        if (i < p.nup) {   // (a, b) of the packed upper entry i
+            int k = i;
+            while (k >= n - a) { k -= n - a; a++; }
+            b = a + k;
+        } else {
+            a = i - p.nup;
+            b = n;
+        }
+        // the wave solver's rows: the damped lower triangle (S += diag(1e-4 S
+        // + 1), ba_cuda.cu:517-518), zeros above it, the g row
+        p.Hd[b * BD_HD_LD + a] = a == b ? t + (1e-4f * t + 1.0f) : t;
+        if (a < b && b < n) p.Hd[a * BD_HD_LD + b] = 0.f;
     }
 }
 
@@ -2143,77 +2163,116 @@ __global__ __launch_bounds__(256) void bd_solve_kernel(BdParams p)
     }
 }
 
-// The same damping / factor / solve / retraction in ONE wave with the system
-// in registers, for windows of up to 10 poses (DPVO's OPTIMIZATION_WINDOW):
-// lane i holds row i of the lower triangle of the augmented [S; g^T] (lane
-// n = 6 NN holds g^T), NN compile-time so every loop unrolls onto registers.
-// Right-looking Cholesky: per column k the pivot comes from lane k and the
-// column's entries L[c][k] from lanes c by readlane -- no LDS, no barriers;
-// the g row rides along as row n, ending as z = L^-1 g.  Back substitution
-// L^T x = z: lane i owns x_i, each x_j is (z_j - sum_{i > j} L[i][j] x_i) /
-// L[j][j] with the sum a wave reduction.  Status: the first failing leading
+// The same damping / factor / solve / retraction in ONE wave, for windows of
+// up to 10 poses (DPVO's OPTIMIZATION_WINDOW; n = 6 NN <= 60), NN compile-time
+// so every loop unrolls onto registers.  Lane i holds row i of the lower
+// triangle of the augmented [S; g^T] (lane n holds g^T), loaded as 16-byte
+// vectors from the reduce kernel's dense rows.
+// Right-looking Cholesky, per column k: the pivot by readlane, lane k's
+// sqrt and the column scaled by 1/L[k][k]; the next column's entries updated
+// through a readlane of L[k+1][k] (the critical path: no LDS round trip),
+// every later column through the broadcast of column k from LDS (one
+// ds_write per lane, 16-byte broadcast reads, packed FMAs).  The g row rides
+// along as row n and ends as z = L^-1 g.  Back substitution L^T x = z on the
+// transposed factor (LDS transpose once): lane r then holds column r, and
+// every x_j, broadcast by readlane, is one FMA into the running sums --
+// no cross-lane reduction per unknown.  Status: the first failing leading
 // minor, as torch::linalg::cholesky reports it.
 __device__ __forceinline__ float rdl(float v, int lane) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane)); }
+
+typedef float bd_f2 __attribute__((ext_vector_type(2)));
+// f(integral_constant<int, K>) for K = B .. E-1, expanded at compile time
+template <int B, int E>
+struct bd_unroll {
+    template <class F>
+    __device__ __forceinline__ static void run(F&& f)
+    {
+        if constexpr (B < E) {
+            f(std::integral_constant<int, B>{});
+            bd_unroll<B + 1, E>::run(f);
+        }
+    }
+};
+typedef float bd_f4 __attribute__((ext_vector_type(4)));
+constexpr int BD_T_LD = 68;   // transpose rows: 272 B, 16-byte aligned, column reads conflict-free
 
 template <int NN>
 __global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
 {
     constexpr int n = 6 * NN;
-    static_assert(n < 64, "one lane per row plus the g row");
+    constexpr int NV = (n + 3) / 4;   // 16-byte vectors per row
+    static_assert(n < 64 && n % 2 == 0, "one lane per row plus the g row; columns in pairs");
+    __shared__ __attribute__((aligned(16))) float col[n][64];              // column k of the factor, by row
+    __shared__ __attribute__((aligned(16))) float tr[(n + 1) * BD_T_LD];   // the factor, row-major, for the transpose
     __shared__ float xs[64];
     const int status = *(volatile int*)p.status;   // checked once the system loads below are in flight
     const int lane = threadIdx.x;
-    const int nup = p.nup;
-    float a[n];
-    // every load issued before any is used: row `lane` of the upper-stored
-    // system, column c at tri_up(c, lane) (lane < n), the g row at nup + c;
-    // other lanes / entries read entry 0 and are zeroed after the loads
-    const bool rowv = lane < n, grow = lane == n;
-    // tri_up(c, lane, n) = c (2n - c + 1) / 2 + lane - c: per-c constant + lane
-    const int base = rowv ? lane : grow ? nup : 0;
+    // rows 0 .. n (lanes past n load row 0: a harmless copy, never read)
+    const float* src = p.Hd + (lane <= n ? lane : 0) * BD_HD_LD;
+    float a[4 * NV];
 #pragma unroll
-    for (int c = 0; c < n; c++) {
-        const int off = grow ? c : rowv ? c * (2 * n - c + 1) / 2 - c : 0;
-        a[c] = __builtin_nontemporal_load(p.H + (base + off));
+    for (int v = 0; v < NV; v++) {
+        const bd_f4 x = __builtin_nontemporal_load((const bd_f4*)src + v);
+        a[4 * v + 0] = x[0]; a[4 * v + 1] = x[1]; a[4 * v + 2] = x[2]; a[4 * v + 3] = x[3];
     }
     if (status != 0) return;
-#pragma unroll
-    for (int c = 0; c < n; c++) {
-        const bool keep = (rowv && c <= lane) || grow;
-        a[c] = keep ? a[c] : 0.f;
-        if (c == lane) a[c] += 1e-4f * a[c] + 1.0f;   // S += diag(1e-4 S + 1), ba_cuda.cu:517-518
-    }
     int fail = 0;
-#pragma unroll
-    for (int k = 0; k < n; k++) {
+    // one column step per k, k a compile-time constant (bd_unroll): every a[]
+    // index is static, so the system stays in registers at any NN
+    bd_unroll<0, n>::run([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
         const float d = rdl(a[k], k);
-        if (!(d > 0.f)) {
-            fail = k + 1;
-            break;
-        }
-        const float l = sqrtf(d), il = 1.0f / l;
-        a[k] = lane == k ? l : a[k] * il;
+        fail = (fail == 0 && !(d > 0.f)) ? k + 1 : fail;
+        // lane k: d / sqrt(d) = L[k][k]; lanes below it: L[r][k]; lane n: z_k
+        a[k] *= __builtin_amdgcn_rsqf(d);
+        if constexpr (k + 1 < n) {
+            col[k][lane] = a[k];
+            a[k + 1] -= a[k] * rdl(a[k], k + 1);   // the next pivot's column: no LDS latency
+            // columns k + 2 .. n - 1 from the LDS broadcast of column k: aligned
+            // pairs by packed FMAs, an odd leading column alone
 #pragma unroll
-        for (int c = k + 1; c < n; c++) a[c] -= a[k] * rdl(a[k], c);
-    }
+            for (int c = 0; c < n; c += 2) {
+                if (c >= k + 2) {
+                    const bd_f2 lc = *(const bd_f2*)&col[k][c];
+                    const bd_f2 r = __builtin_elementwise_fma(-bd_f2{a[k], a[k]}, lc, bd_f2{a[c], a[c + 1]});
+                    a[c] = r[0];
+                    a[c + 1] = r[1];
+                } else if (c + 1 >= k + 2) {
+                    a[c + 1] -= a[k] * col[k][c + 1];
+                }
+            }
+        }
+    });
     if (fail) {
         if (lane == 0) atomicExch(p.status, fail);
         return;
     }
-    float x = 0.f;
+    // transpose through LDS: lane r reads column r -- L[i][r] for i >= r (zero
+    // above the diagonal), z_r from row n
+#pragma unroll
+    for (int v = 0; v < NV; v++)
+        *(bd_f4*)&tr[lane * BD_T_LD + 4 * v] = bd_f4{a[4 * v], a[4 * v + 1], a[4 * v + 2], a[4 * v + 3]};
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0); one wave: its LDS accesses stay in order
+    const int rc = lane < n ? lane : 0;
+    float lt[n + 1];
+#pragma unroll
+    for (int i = 0; i <= n; i++) lt[i] = tr[i * BD_T_LD + rc];
+    const float rinv = 1.0f / tr[rc * BD_T_LD + rc];
+    // L^T x = z, j = n-1 .. 0: x_j = (z_j - s_j) / L[j][j], s_r = sum_{i > r} L[i][r] x_i.
+    // Lanes r > j add lt[j] = 0 (above the diagonal), so after the loop every
+    // lane's s is final and (z - s) / L[r][r] is x_r, the value broadcast at step r.
+    float sacc = 0.f;
 #pragma unroll
     for (int j = n - 1; j >= 0; j--) {
-        const float zj = rdl(a[j], n), ljj = rdl(a[j], j);
-        const float sj = wave64_allsum(lane > j && lane < n ? a[j] * x : 0.f);
-        const float xj = (zj - sj) / ljj;
-        x = lane == j ? xj : x;
+        const float xj = rdl((lt[n] - sacc) * rinv, j);
+        sacc += lt[j] * xj;
     }
+    const float x = (lt[n] - sacc) * rinv;
     if (lane < n) {
         xs[lane] = x;
         p.dX[lane] = x;
     }
-    __builtin_amdgcn_s_barrier();   // one wave: orders the LDS write before the reads below
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    __builtin_amdgcn_s_waitcnt(0xc07f);
     if (lane < NN) {
         float* P = p.poses + (int64_t)(p.t0 + lane) * 7;
         const float t0v[3] = {P[0], P[1], P[2]}, q0v[4] = {P[3], P[4], P[5], P[6]};
@@ -2263,6 +2322,7 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
     p.ug = (float*)(ws + L.ug);
     p.Hpart = (float*)(ws + L.Hpart);
     p.H = (float*)(ws + L.H);
+    p.Hd = (float*)(ws + L.Hd);
     p.dX = (float*)(ws + L.dX);
     const size_t lds = (size_t)(BD_WAVES * (p.N > 0 ? L.ent : 0) + BD_WAVES * BD_N6MAX) * 4 +
                        (size_t)(p.N > 0 ? (L.nup + 1) / 2 : 0) * 4 +
