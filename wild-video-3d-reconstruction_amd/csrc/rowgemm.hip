@@ -468,6 +468,15 @@ constexpr int RC_Y = RG_BM * 768;                  // 96 KB
 constexpr int RC_LDS = RC_Y + 2 * RC_STAGE;        // 160 KB
 
 
+// chunk swizzle of the BK = 32 stage rows (64 B = four 16-byte chunks): the
+// physical chunk p of row r holds logical chunk p ^ rc_sw(r), with rc_sw =
+// [0, 2, 3, 1][(r >> 2) & 3].  Each ds_read_b128 lane group ({0-3, 12-15,
+// 20-27}, ...) reads rows fr = lane & 15 at chunk fq = lane >> 4; with this
+// permutation its 16 lanes hit 16 distinct 16-byte bank slots (the plain
+// (r >> 2) & 3 xor put two lanes on each slot: 2-way conflicts on every
+// fragment read, 46 % of the chain kernels' LDS cycles).
+__device__ __forceinline__ int rc_sw(int r) { return (0x78 >> (((r >> 2) & 3) << 1)) & 3; }
+
 struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflict-free
     // ds_read_b128 fragment reads down 16 rows and 256-byte row sweeps
     __device__ int off(int r, int byte) const { return r * 768 + (((byte >> 4) ^ (r & 15)) << 4) + (byte & 15); }
@@ -508,7 +517,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
     const int64_t w3delta = TRI ? (const half_t*)p.W - W2 : 0;
     const YMapChunk ym;
     // piece (1 KB = 16 rows x 64 B) lane mapping: row base + L/4, physical chunk
-    // L%4 holding logical chunk (L%4) ^ ((row>>2)&3)
+    // L%4 holding logical chunk (L%4) ^ rc_sw(row)
     const int srow = lane >> 2, pch = lane & 3;
     // GEMM1 stage: pieces 4 wave .. 4 wave + 3 of 32 (0-7 A rows, 8-31 W1 rows)
     const half_t* g1src[4];
@@ -524,7 +533,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
                     const int64_t s = p1.a_idx ? p1.a_idx[m] : m;
                     if (s >= 0 && s < p1.a_rows) row = (const half_t*)p1.A + s * p1.lda;
                 }
-                g1src[j] = row + 8 * (pch ^ ((r >> 2) & 3));
+                g1src[j] = row + 8 * (pch ^ rc_sw(r));
             }
         }
     };
@@ -533,7 +542,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         const int pc = 4 * wave + j;   // A pieces then W pieces, contiguous within the stage
         if (pc >= 8) {   // W1 k-blocked [K1/32][384][32]: a stage's 384 rows are one contiguous block
             const int n = (pc - 8) * 16 + srow;
-            g1src[j] = W1 + (int64_t)n * RC_BK + 8 * (pch ^ ((n >> 2) & 3));
+            g1src[j] = W1 + (int64_t)n * RC_BK + 8 * (pch ^ rc_sw(n));
         }
     }
     // GEMM2 stage: W2 pieces 3 wave .. 3 wave + 2 of 24
@@ -541,7 +550,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
 #pragma unroll
     for (int j = 0; j < 3; j++) {
         const int n = (3 * wave + j) * 16 + srow;
-        w2src[j] = W2 + (int64_t)n * RC_BK + 8 * (pch ^ ((n >> 2) & 3));   // k-blocked like W1
+        w2src[j] = W2 + (int64_t)n * RC_BK + 8 * (pch ^ rc_sw(n));   // k-blocked like W1
     }
     // gate pass: the same stage layout, W pieces from Wg ([384][K1] like W1)
     const int64_t gdelta = GATED ? (const half_t*)pg.W - W1 : 0;
@@ -571,12 +580,12 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
 #pragma unroll
     for (int mt = 0; mt < 4; mt++) {
         const int row = wm * 64 + mt * 16 + fr;
-        a_off[mt] = row * 64 + 16 * (fq ^ ((row >> 2) & 3));
+        a_off[mt] = row * 64 + 16 * (fq ^ rc_sw(row));
     }
 #pragma unroll
     for (int nt = 0; nt < 6; nt++) {
         const int n = wn * 96 + nt * 16 + fr;
-        w_off[nt] = RC_A_STAGE + n * 64 + 16 * (fq ^ ((n >> 2) & 3));
+        w_off[nt] = RC_A_STAGE + n * 64 + 16 * (fq ^ rc_sw(n));
     }
     auto zero_acc = [&]() {
 #pragma unroll
