@@ -2247,8 +2247,9 @@ __global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
         if (lane == 0) atomicExch(p.status, fail);
         return;
     }
-    // transpose through LDS: lane r reads column r -- L[i][r] for i >= r (zero
-    // above the diagonal), z_r from row n
+    // transpose through LDS: lane r reads column r -- L[i][r] for i >= r, z_r
+    // from row n; the entries above the diagonal (which the right-looking
+    // updates leave as garbage) read as zero
 #pragma unroll
     for (int v = 0; v < NV; v++)
         *(bd_f4*)&tr[lane * BD_T_LD + 4 * v] = bd_f4{a[4 * v], a[4 * v + 1], a[4 * v + 2], a[4 * v + 3]};
@@ -2256,7 +2257,10 @@ __global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
     const int rc = lane < n ? lane : 0;
     float lt[n + 1];
 #pragma unroll
-    for (int i = 0; i <= n; i++) lt[i] = tr[i * BD_T_LD + rc];
+    for (int i = 0; i <= n; i++) {
+        const float v = tr[i * BD_T_LD + rc];
+        lt[i] = (i >= lane || i == n) ? v : 0.f;
+    }
     const float rinv = 1.0f / tr[rc * BD_T_LD + rc];
     // L^T x = z, j = n-1 .. 0: x_j = (z_j - s_j) / L[j][j], s_r = sum_{i > r} L[i][r] x_i.
     // Lanes r > j add lt[j] = 0 (above the diagonal), so after the loop every
