@@ -2247,9 +2247,9 @@ __global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
         if (lane == 0) atomicExch(p.status, fail);
         return;
     }
-    // transpose through LDS: lane r reads column r -- L[i][r] for i >= r, z_r
-    // from row n; the entries above the diagonal (which the right-looking
-    // updates leave as garbage) read as zero
+    // transpose through LDS: lane r reads column r -- L[i][r] for i > r, z_r
+    // from row n; the diagonal and the entries above it (which the
+    // right-looking updates leave as garbage) read as zero
 #pragma unroll
     for (int v = 0; v < NV; v++)
         *(bd_f4*)&tr[lane * BD_T_LD + 4 * v] = bd_f4{a[4 * v], a[4 * v + 1], a[4 * v + 2], a[4 * v + 3]};
@@ -2259,12 +2259,12 @@ __global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
 #pragma unroll
     for (int i = 0; i <= n; i++) {
         const float v = tr[i * BD_T_LD + rc];
-        lt[i] = (i >= lane || i == n) ? v : 0.f;
+        lt[i] = (i > lane || i == n) ? v : 0.f;   // L[i][r], i > r (the diagonal: rinv)
     }
     const float rinv = 1.0f / tr[rc * BD_T_LD + rc];
     // L^T x = z, j = n-1 .. 0: x_j = (z_j - s_j) / L[j][j], s_r = sum_{i > r} L[i][r] x_i.
-    // Lanes r > j add lt[j] = 0 (above the diagonal), so after the loop every
-    // lane's s is final and (z - s) / L[r][r] is x_r, the value broadcast at step r.
+    // Lanes r >= j add lt[j] = 0, so after the loop every lane's s is final and
+    // (z - s) / L[r][r] is x_r, the value broadcast at step r.
     float sacc = 0.f;
 #pragma unroll
     for (int j = n - 1; j >= 0; j--) {
