@@ -7,7 +7,7 @@ from collections import defaultdict
 acc = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(f"{sys.argv[1]}/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        acc[r["Kernel_Name"][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        acc[r["Kernel_Name"][:96]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in acc.items():
     print(k)
     for c, v in sorted(cs.items()):
