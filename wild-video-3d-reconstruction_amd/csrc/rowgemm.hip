@@ -496,16 +496,32 @@ struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflic
 // then a third GEMM on that tile with p's W and bias feeds p's epilogue.
 // Bit-identical to rowchain (corr0, corr1, LN|LN_RELU) -> fp16 rows ->
 // rowgemm (corr2, RES|LN): the same MFMA k order and the same epilogue code.
+// Roles (round 4): waves 0-3 issue every LDS-DMA stage (loaders: GEMM1 stages
+// 8 pieces each -- 2 A + 6 W --, W-only stages 6), so only they wait on the
+// stage vmcnt; all eight waves read fragments and issue MFMAs.
+// OVL (every chain but the heads chain): the row epilogue of tile t is
+// deferred into the next tile's GEMM1 k-loop -- GEMM1 does not touch the y
+// tile, which still holds tile t's output -- where waves 4-7 run it in
+// row-pair batches after each k-step's MFMAs (16 batches of 2 rows per wave,
+// spread over the k-steps, the next batch's residual loads in flight while one
+// is finished).  Their loads and stores never enter the loaders' vmcnt, and
+// the epilogue's HBM traffic overlaps the k-loops instead of following them.
+// The last tile's epilogue runs after the loop on all eight waves.  The
+// arithmetic per row is epi2_finish's either way: bit-identical results.
 template <int F2, bool GATED = false, int FMID = 0>
 __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
                                                                  dpvo_rowgemm_args pg)
 {
     constexpr bool TRI = FMID != 0;
+    constexpr bool OVL = !(F2 & RG_HEADS);
     static_assert(!(TRI && GATED), "a chain is either gated or three GEMMs long");
     __shared__ __attribute__((aligned(16))) char smem[RC_LDS];
     typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave & 1, wn = wave >> 1;
+    const bool ldw = wave < 4;   // loader waves
+    const int lw = wave & 3;
     const int K1 = p1.K, ks1 = K1 / RC_BK, ks2 = RG_BN / RC_BK;
     const int64_t Mrows = p1.M_dev ? min(*p1.M_dev, p1.M) : p1.M;
     const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
@@ -517,57 +533,41 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
     const int64_t w3delta = TRI ? (const half_t*)p.W - W2 : 0;
     const YMapChunk ym;
     // piece (1 KB = 16 rows x 64 B) lane mapping: row base + L/4, physical chunk
-    // L%4 holding logical chunk (L%4) ^ rc_sw(row)
+    // L%4 holding logical chunk (L%4) ^ rc_sw(row); rc_sw(16 q + srow) = rc_sw(srow)
     const int srow = lane >> 2, pch = lane & 3;
-    // GEMM1 stage: pieces 4 wave .. 4 wave + 3 of 32 (0-7 A rows, 8-31 W1 rows)
-    const half_t* g1src[4];
+    // loader lw: A pieces 2 lw, 2 lw + 1 (rows 16 piece + srow) and, in the
+    // k-blocked W ([K/32][384][32]: a stage is one contiguous 384 x 32 block),
+    // W pieces 6 lw .. 6 lw + 5, 512 elements apart
+    const half_t* a1src[2];
     auto set_tile = [&](int64_t tile) {
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int pc = 4 * wave + j;
-            if (pc < 8) {
-                const int r = pc * 16 + srow;
-                const int64_t m = tile * RG_BM + r;
-                const half_t* row = zero;
-                if (m < Mrows) {
-                    const int64_t s = p1.a_idx ? p1.a_idx[m] : m;
-                    if (s >= 0 && s < p1.a_rows) row = (const half_t*)p1.A + s * p1.lda;
-                }
-                g1src[j] = row + 8 * (pch ^ rc_sw(r));
+        for (int j = 0; j < 2; j++) {
+            const int r = (2 * lw + j) * 16 + srow;
+            const int64_t m = tile * RG_BM + r;
+            const half_t* row = zero;
+            if (m < Mrows) {
+                const int64_t s = p1.a_idx ? p1.a_idx[m] : m;
+                if (s >= 0 && s < p1.a_rows) row = (const half_t*)p1.A + s * p1.lda;
             }
+            a1src[j] = row + 8 * (pch ^ rc_sw(r));
         }
     };
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int pc = 4 * wave + j;   // A pieces then W pieces, contiguous within the stage
-        if (pc >= 8) {   // W1 k-blocked [K1/32][384][32]: a stage's 384 rows are one contiguous block
-            const int n = (pc - 8) * 16 + srow;
-            g1src[j] = W1 + (int64_t)n * RC_BK + 8 * (pch ^ rc_sw(n));
-        }
-    }
-    // GEMM2 stage: W2 pieces 3 wave .. 3 wave + 2 of 24
-    const half_t* w2src[3];
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int n = (3 * wave + j) * 16 + srow;
-        w2src[j] = W2 + (int64_t)n * RC_BK + 8 * (pch ^ rc_sw(n));   // k-blocked like W1
-    }
+    const int wq = (6 * lw * 16 + srow) * RC_BK + 8 * (pch ^ rc_sw(srow));
     // gate pass: the same stage layout, W pieces from Wg ([384][K1] like W1)
     const int64_t gdelta = GATED ? (const half_t*)pg.W - W1 : 0;
-    auto issue1 = [&](int ks, int buf, bool gate = false) {
+    auto issue1 = [&](int ks, int buf, bool gate = false) {   // loaders only
         char* st = smem + RC_Y + buf * RC_STAGE;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const bool wp = 4 * wave + j >= 8;
-            const int64_t k0 = wp ? (int64_t)ks * (RG_BN * RC_BK) : ks * RC_BK;
-            glds16(g1src[j] + k0 + (GATED && gate && wp ? gdelta : 0), st + (4 * wave + j) * 1024);
-        }
-    };
-    auto issue2 = [&](int ks, int buf, int64_t wdelta = 0) {
-        char* st = smem + RC_Y + buf * RC_STAGE + RC_A_STAGE;
-        const int64_t k0 = (int64_t)ks * (RG_BN * RC_BK) + wdelta;
+        for (int j = 0; j < 2; j++) glds16(a1src[j] + ks * RC_BK, st + (2 * lw + j) * 1024);
+        const half_t* w = W1 + wq + (int64_t)ks * (RG_BN * RC_BK) + (GATED && gate ? gdelta : 0);
 #pragma unroll
-        for (int j = 0; j < 3; j++) glds16(w2src[j] + k0, st + (3 * wave + j) * 1024);
+        for (int j = 0; j < 6; j++) glds16(w + 512 * j, st + (8 + 6 * lw + j) * 1024);
+    };
+    auto issue2 = [&](int ks, int buf, int64_t wdelta = 0) {   // loaders only
+        char* st = smem + RC_Y + buf * RC_STAGE + RC_A_STAGE;
+        const half_t* w = W2 + wq + (int64_t)ks * (RG_BN * RC_BK) + wdelta;
+#pragma unroll
+        for (int j = 0; j < 6; j++) glds16(w + 512 * j, st + (6 * lw + j) * 1024);
     };
     auto sync_lds = [&]() {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -599,6 +599,16 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
 #pragma unroll
             for (int nt = 0; nt < 6; nt++)
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
+    };
+    // one GEMM1 k-step's fragment reads and MFMAs from stage buffer buf
+    auto step1 = [&](int buf) {
+        const char* st = smem + RC_Y + buf * RC_STAGE;
+        h8_t a[4], b[6];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(st + a_off[mt]);
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
+        mfma_step(a, b);
     };
     // acc + bias -> act -> fp16 -> y tile (row mt*16+fr, columns 4 fq.. of block nt)
     // (called before any stage prefetch is in flight: its bias loads would
@@ -661,20 +671,92 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             }
         }
     };
+    // ---- the row epilogue in batches of 4 rows (two row pairs): local rows
+    // lr .. lr + 3 of tile `et`
+    auto epi_issue = [&](int64_t et, int lr, EpiOps2<4>& o) {
+        epi2_load<F2, 4>(p, Mrows, et * RG_BM + lr, lane, o);
+    };
+    auto epi_done = [&](int64_t et, int lr, const EpiConsts2& kc, const EpiOps2<4>& o) {
+        const int hh = lane >> 5, ss = lane & 31;
+        epi2_finish<F2, 4>(
+            p, Mrows,
+            [&](int i, int j) { return *(const ep_h4*)(smem + ym.off(lr + 2 * i + hh, (128 * j + 4 * ss) * 2)); },
+            et * RG_BM + lr, lane, kc, o);
+    };
+    int64_t etile = -1;   // OVL: the tile whose row epilogue is still pending
+    // GEMM1 (A gathered x W1); OVL: waves 4-7 run the pending epilogue meanwhile
     auto gemm1 = [&](bool gate) {
-        for (int ks = 0; ks < ks1; ks++) {
-            if (ks + 1 < ks1) {
-                issue1(ks + 1, (ks + 1) & 1, gate);
-                asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (ldw) {
+            for (int ks = 0; ks < ks1; ks++) {
+                if (ks + 1 < ks1) {
+                    issue1(ks + 1, (ks + 1) & 1, gate);
+                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                step1(ks & 1);
+                __builtin_amdgcn_s_barrier();
+            }
+        } else if (OVL && !gate && etile >= 0) {
+            // rows 32 e .. 32 e + 31 (e = wave - 4) in 8 batches of 4: batch b's
+            // residual loads issued after k-step L(b) = b (ks1 - 1) / 8, the batch
+            // finished after k-step L(b) + 1 (one k-step of load latency hidden;
+            // one batch of loads live at a time)
+            const int lr0 = 32 * (wave - 4);
+            EpiOps2<4> st;
+            int bi = 0, bd = 0;   // next batch to issue / to finish
+            for (int ks = 0; ks < ks1; ks++) {
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                step1(ks & 1);
+                if (bd < bi) {
+                    // LayerNorm constants per batch (L1 hits), not held across the
+                    // k-steps: the register budget is the accumulators' here
+                    EpiConsts2 kc;
+                    load_consts2<F2>(p, lane, kc);
+                    epi_done(etile, lr0 + 4 * bd, kc, st);
+                    bd++;
+                }
+                // (the next batch's loads may not move above this batch's
+                // arithmetic: both would be live at once)
+                __builtin_amdgcn_sched_barrier(0);
+                if (bi < 8 && (bi * (ks1 - 1)) / 8 == ks) {
+                    epi_issue(etile, lr0 + 4 * bi, st);
+                    bi++;
+                }
+                __builtin_amdgcn_s_barrier();
+            }
+        } else {
+            for (int ks = 0; ks < ks1; ks++) {
+                __builtin_amdgcn_s_barrier();
+                asm volatile("" ::: "memory");
+                step1(ks & 1);
+                __builtin_amdgcn_s_barrier();
+            }
+        }
+    };
+    // GEMM over the y tile (stage 0 already issued); wdelta selects W3
+    auto gemm_y = [&](int64_t wdelta) {
+        zero_acc();
+#pragma unroll 1
+        for (int ks = 0; ks < ks2; ks++) {
+            if (ldw) {
+                if (ks + 1 < ks2) {
+                    issue2(ks + 1, (ks + 1) & 1, wdelta);
+                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
             }
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
             const char* st = smem + RC_Y + (ks & 1) * RC_STAGE;
             h8_t a[4], b[6];
 #pragma unroll
-            for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(st + a_off[mt]);
+            for (int mt = 0; mt < 4; mt++)
+                a[mt] = *(const h8_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, (ks * 4 + fq) * 16));
 #pragma unroll
             for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
             mfma_step(a, b);
@@ -682,47 +764,25 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         }
     };
     int64_t tile = blockIdx.x;
-    set_tile(tile);
-    issue1(0, 0);
+    if (ldw) {
+        set_tile(tile);
+        issue1(0, 0);
+    }
     for (; tile < ntiles; tile += gridDim.x) {
         const bool more = tile + gridDim.x < ntiles;
-        // ---- GEMM1: A (global, gathered) x W1
         zero_acc();
         gemm1(false);
+        etile = -1;
         // ---- intermediate -> y tile; W2's first stage into the released stage 0
         acc_to_y((const half_t*)p1.bias, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
-        issue2(0, 0);
+        if (ldw) issue2(0, 0);
         sync_lds();
-        // ---- GEMM2: y tile x W2 (stage 0 already issued); wdelta selects W3
-        auto gemm_y = [&](int64_t wdelta) {
-            zero_acc();
-#pragma unroll 1
-            for (int ks = 0; ks < ks2; ks++) {
-                if (ks + 1 < ks2) {
-                    issue2(ks + 1, (ks + 1) & 1, wdelta);
-                    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-                const char* st = smem + RC_Y + (ks & 1) * RC_STAGE;
-                h8_t a[4], b[6];
-#pragma unroll
-                for (int mt = 0; mt < 4; mt++)
-                    a[mt] = *(const h8_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, (ks * 4 + fq) * 16));
-#pragma unroll
-                for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
-                mfma_step(a, b);
-                __builtin_amdgcn_s_barrier();
-            }
-        };
         gemm_y(0);
         if (TRI) {
             // the middle Linear's output -> its row epilogue (LayerNorm, ReLU) in
             // place on the y tile -> the third GEMM's A operand
             acc_to_y((const half_t*)pg.bias, false, false);
-            issue2(0, 0, w3delta);   // stage 0 of W3 loads under the row pass
+            if (ldw) issue2(0, 0, w3delta);   // stage 0 of W3 loads under the row pass
             sync_lds();
             mid_rows(pg);
             sync_lds();
@@ -731,7 +791,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         acc_to_y((const half_t*)p.bias, F2 & RG_RELU, F2 & RG_SIGMOID);
         if (GATED) {
             // ---- gate: A x Wg -> sigmoid (rowgemm's SIGMOID rounding) -> y = fp16(gate * y)
-            issue1(0, 0, true);
+            if (ldw) issue1(0, 0, true);
             zero_acc();
             gemm1(true);
 #pragma unroll
@@ -752,19 +812,26 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             }
         }
         // ---- the next tile's first GEMM1 stage loads under this epilogue
-        if (more) {
+        if (more && ldw) {
             set_tile(tile + gridDim.x);
             issue1(0, 0);
         }
         sync_lds();
-        // LayerNorm / head constants loaded per tile, not held across the GEMMs
-        // (the gated chain's gate already holds 48 VGPRs there)
-        EpiConsts2 kc;
-        load_consts2<F2>(p, lane, kc);
-        constexpr int RB = (F2 & (RG_RES | RG_GATE | RG_LN)) ? 4 : 8;
+        if (OVL && more) {
+            etile = tile;   // run during the next tile's GEMM1
+            continue;
+        }
+        // the row epilogue now, on every wave: rows 16 wave .. 16 wave + 15
+        {
+            EpiConsts2 kc;
+            load_consts2<F2>(p, lane, kc);
 #pragma unroll 1
-        for (int q0 = 0; q0 < 16; q0 += RB)   // one batch live at a time (register budget)
-            epilogue_rows2<F2, RB>(p, Mrows, smem, ym, wave * 16 + q0, tile * RG_BM + wave * 16 + q0, lane, kc);
+            for (int q0 = 0; q0 < 16; q0 += 4) {   // one batch live at a time (register budget)
+                EpiOps2<4> st;
+                epi_issue(tile, 16 * wave + q0, st);
+                epi_done(tile, 16 * wave + q0, kc, st);
+            }
+        }
         sync_lds();
     }
 }
