@@ -499,7 +499,7 @@ struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflic
 // Roles (round 4): waves 0-3 issue every LDS-DMA stage (loaders: GEMM1 stages
 // 8 pieces each -- 2 A + 6 W --, W-only stages 6), so only they wait on the
 // stage vmcnt; all eight waves read fragments and issue MFMAs.
-// OVL (every chain but the heads chain): the row epilogue of tile t is
+// OVL (the residual-only chains c1 / c2): the row epilogue of tile t is
 // deferred into the next tile's GEMM1 k-loop -- GEMM1 does not touch the y
 // tile, which still holds tile t's output -- where waves 4-7 run it in
 // row-pair batches after each k-step's MFMAs (16 batches of 2 rows per wave,
@@ -508,12 +508,17 @@ struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflic
 // the epilogue's HBM traffic overlaps the k-loops instead of following them.
 // The last tile's epilogue runs after the loop on all eight waves.  The
 // arithmetic per row is epi2_finish's either way: bit-identical results.
+// (Measured at C3: c1 / c2 137 -> 129 us.  With the LayerNorm epilogues the
+// deferred batch's state spills beside the accumulators, and a variant whose
+// GEMM1 runs on the loader waves alone -- 8 x 6 accumulators each, waves 4-7
+// free -- spills ~700 B per lane.)
 template <int F2, bool GATED = false, int FMID = 0>
 __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
                                                                  dpvo_rowgemm_args pg)
 {
     constexpr bool TRI = FMID != 0;
-    constexpr bool OVL = !(F2 & RG_HEADS);
+    // (the LayerNorm chains' epilogue state does not fit beside the accumulators: spills)
+    constexpr bool OVL = F2 == RG_RES;
     static_assert(!(TRI && GATED), "a chain is either gated or three GEMMs long");
     __shared__ __attribute__((aligned(16))) char smem[RC_LDS];
     typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
