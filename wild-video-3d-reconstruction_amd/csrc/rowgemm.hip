@@ -477,6 +477,23 @@ constexpr int RC_LDS = RC_Y + 2 * RC_STAGE;        // 160 KB
 // fragment read, 46 % of the chain kernels' LDS cycles).
 __device__ __forceinline__ int rc_sw(int r) { return (0x78 >> (((r >> 2) & 3) << 1)) & 3; }
 
+#ifdef DPVO_STAMPS
+// Diagnostic build only (never the product library): per-wave cycle sums of
+// the chain kernels' k-loop segments, s_memtime stamps (cdna guide, In-kernel
+// stamps).  dpvo_stamps[block][wave][segment].
+constexpr int ST_SEGS = 12;
+__device__ unsigned long long dpvo_stamps[1024 * 8 * ST_SEGS];
+#define RC_STAMP(v)                                                                            \
+    unsigned long long v;                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");                  \
+    __builtin_amdgcn_sched_barrier(0);
+#define RC_ACC(seg, a, b) st_sum[seg] += (b) - (a);
+#else
+#define RC_STAMP(v)
+#define RC_ACC(seg, a, b)
+#endif
+
 struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflict-free
     // ds_read_b128 fragment reads down 16 rows and 256-byte row sweeps
     __device__ int off(int r, int byte) const { return r * 768 + (((byte >> 4) ^ (r & 15)) << 4) + (byte & 15); }
@@ -688,21 +705,30 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             [&](int i, int j) { return *(const ep_h4*)(smem + ym.off(lr + 2 * i + hh, (128 * j + 4 * ss) * 2)); },
             et * RG_BM + lr, lane, kc, o);
     };
+#ifdef DPVO_STAMPS
+    unsigned long long st_sum[ST_SEGS] = {};
+#endif
     int64_t etile = -1;   // OVL: the tile whose row epilogue is still pending
     // GEMM1 (A gathered x W1); OVL: waves 4-7 run the pending epilogue meanwhile
     auto gemm1 = [&](bool gate) {
         if (ldw) {
             for (int ks = 0; ks < ks1; ks++) {
+                RC_STAMP(t0)
                 if (ks + 1 < ks1) {
                     issue1(ks + 1, (ks + 1) & 1, gate);
                     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
                 } else {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
+                RC_STAMP(t1)
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
+                RC_STAMP(t2)
                 step1(ks & 1);
+                RC_STAMP(t3)
                 __builtin_amdgcn_s_barrier();
+                RC_STAMP(t4)
+                RC_ACC(0, t0, t1) RC_ACC(1, t1, t2) RC_ACC(2, t2, t3) RC_ACC(3, t3, t4)
             }
         } else if (OVL && !gate && etile >= 0) {
             // rows 32 e .. 32 e + 31 (e = wave - 4) in 8 batches of 4: batch b's
@@ -713,9 +739,13 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             EpiOps2<4> st;
             int bi = 0, bd = 0;   // next batch to issue / to finish
             for (int ks = 0; ks < ks1; ks++) {
+                RC_STAMP(t1)
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
+                RC_STAMP(t2)
                 step1(ks & 1);
+                RC_STAMP(t3)
+                RC_ACC(1, t1, t2) RC_ACC(2, t2, t3)
                 if (bd < bi) {
                     // LayerNorm constants per batch (L1 hits), not held across the
                     // k-steps: the register budget is the accumulators' here
@@ -731,14 +761,22 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
                     epi_issue(etile, lr0 + 4 * bi, st);
                     bi++;
                 }
+                RC_STAMP(t35)
                 __builtin_amdgcn_s_barrier();
+                RC_STAMP(t4)
+                RC_ACC(4, t3, t35) RC_ACC(3, t35, t4)
             }
         } else {
             for (int ks = 0; ks < ks1; ks++) {
+                RC_STAMP(t1)
                 __builtin_amdgcn_s_barrier();
                 asm volatile("" ::: "memory");
+                RC_STAMP(t2)
                 step1(ks & 1);
+                RC_STAMP(t3)
                 __builtin_amdgcn_s_barrier();
+                RC_STAMP(t4)
+                RC_ACC(1, t1, t2) RC_ACC(2, t2, t3) RC_ACC(3, t3, t4)
             }
         }
     };
@@ -747,6 +785,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
         zero_acc();
 #pragma unroll 1
         for (int ks = 0; ks < ks2; ks++) {
+            RC_STAMP(t0)
             if (ldw) {
                 if (ks + 1 < ks2) {
                     issue2(ks + 1, (ks + 1) & 1, wdelta);
@@ -755,8 +794,10 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 }
             }
+            RC_STAMP(t1)
             __builtin_amdgcn_s_barrier();
             asm volatile("" ::: "memory");
+            RC_STAMP(t2)
             const char* st = smem + RC_Y + (ks & 1) * RC_STAGE;
             h8_t a[4], b[6];
 #pragma unroll
@@ -765,10 +806,14 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
 #pragma unroll
             for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
             mfma_step(a, b);
+            RC_STAMP(t3)
             __builtin_amdgcn_s_barrier();
+            RC_STAMP(t4)
+            RC_ACC(5, t0, t1) RC_ACC(6, t1, t2) RC_ACC(7, t2, t3) RC_ACC(8, t3, t4)
         }
     };
     int64_t tile = blockIdx.x;
+    RC_STAMP(t_begin)
     if (ldw) {
         set_tile(tile);
         issue1(0, 0);
@@ -827,6 +872,7 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             continue;
         }
         // the row epilogue now, on every wave: rows 16 wave .. 16 wave + 15
+        RC_STAMP(te0)
         {
             EpiConsts2 kc;
             load_consts2<F2>(p, lane, kc);
@@ -838,7 +884,16 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             }
         }
         sync_lds();
+        RC_STAMP(te1)
+        RC_ACC(9, te0, te1)
     }
+#ifdef DPVO_STAMPS
+    RC_STAMP(t_end)
+    st_sum[10] += t_end - t_begin;
+    st_sum[11] += 1;
+    if (lane == 0)
+        for (int k = 0; k < ST_SEGS; k++) dpvo_stamps[((int64_t)blockIdx.x * 8 + wave) * ST_SEGS + k] = st_sum[k];
+#endif
 }
 
 // v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16
@@ -1151,6 +1206,14 @@ extern "C" int dpvo_rowchain_gated(const dpvo_rowgemm_args* gate, const dpvo_row
     DPVO_CHECK_ARG(gate != nullptr, "rowchain_gated: gate args missing");
     return rowchain_launch(g1, g2, gate, stream);
 }
+
+#ifdef DPVO_STAMPS
+extern "C" int dpvo_diag_stamps(void* host, size_t bytes)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(dpvo_stamps), std::min(bytes, sizeof(dpvo_stamps)), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int dpvo_rowadd_ln(const dpvo_rowadd_args* a, void* stream)
 {
