@@ -481,7 +481,7 @@ __device__ __forceinline__ int rc_sw(int r) { return (0x78 >> (((r >> 2) & 3) <<
 // Diagnostic build only (never the product library): per-wave cycle sums of
 // the chain kernels' k-loop segments, s_memtime stamps (cdna guide, In-kernel
 // stamps).  dpvo_stamps[block][wave][segment].
-constexpr int ST_SEGS = 12;
+constexpr int ST_SEGS = 16;
 __device__ unsigned long long dpvo_stamps[1024 * 8 * ST_SEGS];
 #define RC_STAMP(v)                                                                            \
     unsigned long long v;                                                                      \
@@ -820,14 +820,19 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
     }
     for (; tile < ntiles; tile += gridDim.x) {
         const bool more = tile + gridDim.x < ntiles;
+        RC_STAMP(tt0)
         zero_acc();
         gemm1(false);
+        RC_STAMP(tt1)
         etile = -1;
         // ---- intermediate -> y tile; W2's first stage into the released stage 0
         acc_to_y((const half_t*)p1.bias, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
         if (ldw) issue2(0, 0);
         sync_lds();
+        RC_STAMP(tt2)
         gemm_y(0);
+        RC_STAMP(tt3)
+        RC_ACC(11, tt1, tt2)
         if (TRI) {
             // the middle Linear's output -> its row epilogue (LayerNorm, ReLU) in
             // place on the y tile -> the third GEMM's A operand
@@ -866,7 +871,10 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
             set_tile(tile + gridDim.x);
             issue1(0, 0);
         }
+        RC_STAMP(tt4)
         sync_lds();
+        RC_STAMP(tt5)
+        RC_ACC(12, tt3, tt4) RC_ACC(13, tt4, tt5) RC_ACC(14, tt0, tt5)
         if (OVL && more) {
             etile = tile;   // run during the next tile's GEMM1
             continue;
@@ -890,7 +898,6 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_ar
 #ifdef DPVO_STAMPS
     RC_STAMP(t_end)
     st_sum[10] += t_end - t_begin;
-    st_sum[11] += 1;
     if (lane == 0)
         for (int k = 0; k < ST_SEGS; k++) dpvo_stamps[((int64_t)blockIdx.x * 8 + wave) * ST_SEGS + k] = st_sum[k];
 #endif
