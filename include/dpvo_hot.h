@@ -382,10 +382,14 @@ int dpvo_scatter_csr(int op, int dtype, const void* src, int64_t outer, int64_t 
  * K must be a multiple of 64 (pad W with zero columns; A's pad columns must
  * be finite); A, W, zero_row 16-byte aligned; zero_row holds >= K zeros.
  * Supported flag sets: 0, RELU, SIGMOID, LN|LN_RELU, RES, RES|LN, GATE,
- * GATE|LN, GATE|HEADS. */
+ * GATE|LN, GATE|HEADS; and WKB, WKB|RELU, WKB|SIGMOID (k-blocked W, K a
+ * multiple of 32). */
 enum {
     DPVO_RG_RELU = 1, DPVO_RG_SIGMOID = 2, DPVO_RG_RES = 4, DPVO_RG_GATE = 8, DPVO_RG_LN = 16, DPVO_RG_LN_RELU = 32,
-    DPVO_RG_HEADS = 64
+    DPVO_RG_HEADS = 64,
+    /* W is k-blocked, [K/32][384][32] (as dpvo_rowchain reads it); with flag
+     * sets 0 / RELU / SIGMOID only (and in both args of dpvo_rowgemm_pair) */
+    DPVO_RG_WKB = 128
 };
 typedef struct dpvo_rowgemm_args {
     const void* A; int64_t lda; const int64_t* a_idx; int64_t a_rows;

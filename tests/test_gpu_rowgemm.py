@@ -138,6 +138,34 @@ def test_rowgemm_pair_equals_two_launches(M):
     assert torch.equal(f2[:M // 2], f[:M // 2]) and torch.equal(g2[:M // 2], g[:M // 2])
 
 
+@pytest.mark.parametrize("M", [1, 127, 3000, 40000])
+@pytest.mark.parametrize("flags", [0, 1, 2])
+def test_kblocked_w_is_bit_identical(M, flags):
+    """W read k-blocked ([K/32][384][32], update_ops.kblock; the SoftAgg
+    GEMMs' layout) == the [384][K] kernel bit for bit: single GEMM with a
+    padded K, a gathered A with idx < 0 rows, a device row count, and the pair."""
+    import update_ops as U
+    K = 882
+    buf = torch.zeros(M, 896, device="cuda", dtype=torch.float16)
+    buf[:, :K] = torch.randn(M, K, device="cuda").half()
+    W16, b16 = U.pack_linear(*lin(K, 7))
+    idx = torch.randint(-1, M, (M + 37,), device="cuda")
+    want = U.rowgemm(buf, W16, b16, flags=flags, a_idx=idx)[1]
+    got = U.rowgemm(buf, U.kblock(W16), b16, flags=flags, a_idx=idx)[1]
+    assert torch.equal(got, want)
+    Md = torch.tensor([(M + 1) // 2], dtype=torch.int64, device="cuda")
+    out = torch.full_like(want, 7.0)
+    U.rowgemm(buf, U.kblock(W16), b16, flags=flags, a_idx=idx, out16=out, M_dev=Md)
+    h = (M + 1) // 2
+    assert torch.equal(out[:h], want[:h]) and bool((out[h:] == 7.0).all())
+    A = torch.randn(M, D, device="cuda").half()
+    (Wa, ba), (Wb, bb) = U.pack_linear(*lin(D, 8)), U.pack_linear(*lin(D, 9))
+    f, g = U.rowgemm_pair(A, U.kblock(Wa), ba, U.kblock(Wb), bb)
+    assert torch.equal(f, U.rowgemm(A, Wa, ba)[1]) and torch.equal(g, U.rowgemm(A, Wb, bb)[1])
+    with pytest.raises(RuntimeError):
+        U.rowgemm(A, U.kblock(Wa), ba, flags=U.RES, res32=torch.zeros(M, D, device="cuda"))
+
+
 def test_rowadd_ln():
     import update_ops as U
     M = 3000

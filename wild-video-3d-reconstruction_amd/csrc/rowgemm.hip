@@ -513,6 +513,204 @@ struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflic
 // then a third GEMM on that tile with p's W and bias feeds p's epilogue.
 // Bit-identical to rowchain (corr0, corr1, LN|LN_RELU) -> fp16 rows ->
 // rowgemm (corr2, RES|LN): the same MFMA k order and the same epilogue code.
+// ---------------------------------------------------------------------------
+// v5 (round 4): the plain GEMM (flags 0 / RELU / SIGMOID) with a k-blocked W
+// and no LDS-DMA:
+//   * 8 waves as 2 (M) x 4 (N), wave tile 64 x 96 (4 x 6 accumulators), BK 32;
+//   * W ([K/32][384][32]: a fragment = one contiguous 1 KB, whole lines)
+//     streams from L2 straight into registers, two k-steps ahead -- no LDS
+//     traffic for W;
+//   * A (128 rows x 64 B per k-step) goes global -> registers -> a 2-slot LDS
+//     ring (register staging, three k-steps ahead; rc_sw chunk swizzle,
+//     conflict-free fragment reads);
+//   * one barrier per k-step; every wait is the compiler's exact count of the
+//     wave's own loads and stores (nothing is in flight that it cannot see);
+//   * the row epilogue stages y16 through a 96 KB LDS tile and stores whole
+//     rows, with the next tile's first loads already in flight ahead of it.
+// Persistent blocks walk a flat (tile, pass, k-step) sequence; DUAL runs a
+// second GEMM (p2's W, bias, out16) on the same A tile right after the first.
+// Per output element the MFMA k order is rowgemm3's: the same bits.
+// ---------------------------------------------------------------------------
+constexpr int R5_THREADS = 512, R5_BK = 32;
+constexpr int R5_Y = RG_BM * 768;                  // 96 KB
+constexpr int R5_ASLOT = RG_BM * R5_BK * 2;        // 8 KB
+constexpr int R5_LDS = R5_Y + 2 * R5_ASLOT;        // 112 KB
+
+// (tile, pass, k-step) of a flat step, advanced one step at a time (no
+// 64-bit divisions); past the end it stays on the last step
+struct R5Cursor {
+    int64_t f, t;
+    int k, q;
+    __device__ __forceinline__ void next(int64_t total, int nks, int np, unsigned grid)
+    {
+        if (f + 1 >= total) return;
+        f++;
+        if (++k == nks) {
+            k = 0;
+            if (++q == np) {
+                q = 0;
+                t += grid;
+            }
+        }
+    }
+};
+
+template <int FLAGS, bool DUAL>
+__global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_args p, dpvo_rowgemm_args p2)
+{
+    static_assert((FLAGS & ~(RG_RELU | RG_SIGMOID)) == 0, "v5: plain GEMMs only");
+    __shared__ __attribute__((aligned(16))) char smem[R5_LDS];
+    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = w & 1, wn = w >> 1;
+    const int K = p.K, nks = K / R5_BK;
+    const int64_t Mrows = p.M_dev ? min(*p.M_dev, p.M) : p.M;
+    const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
+    if ((int64_t)blockIdx.x >= ntiles) return;
+    constexpr int NP = DUAL ? 2 : 1;
+    const int64_t my_tiles = (ntiles - 1 - blockIdx.x) / gridDim.x + 1;
+    const int64_t total = my_tiles * NP * nks;   // flat k-steps of this block
+    const YMapChunk ym;
+    const int fr = lane & 15, fq = lane >> 4;
+    const half_t* __restrict__ zero = (const half_t*)p.zero_row;
+    // ---- A staging: lane holds row 16 w + (lane >> 2), logical chunk lane & 3
+    const int ar = 16 * w + (lane >> 2), ac = lane & 3;
+    int64_t a_tile = -1;
+    const half_t* arow = zero;
+    auto a_row = [&](int64_t t) __attribute__((always_inline)) {
+        if (t == a_tile) return;
+        a_tile = t;
+        const int64_t m = t * RG_BM + ar;
+        const half_t* row = zero;
+        if (m < Mrows) {
+            const int64_t src = p.a_idx ? p.a_idx[m] : m;
+            if (src >= 0 && src < p.a_rows) row = (const half_t*)p.A + src * p.lda;
+        }
+        arow = row + 8 * ac;
+    };
+    h8_t areg[2];
+    auto load_a = [&](const R5Cursor& c) __attribute__((always_inline)) -> h8_t {
+        a_row(c.t);
+        return *(const h8_t*)(arow + c.k * R5_BK);
+    };
+    // slot image: row r, physical chunk ac ^ rc_sw(r) holds logical chunk ac
+    const int aw_off = ar * 64 + 16 * (ac ^ rc_sw(ar));
+    // ---- W fragments: column 96 wn + 16 nt + fr, k 8 fq .. 8 fq + 7 of the step
+    h8_t wreg[2][6];
+    const half_t* W1 = (const half_t*)p.W;
+    const half_t* W2 = DUAL ? (const half_t*)p2.W : W1;
+    const int wcol = (96 * wn + fr) * R5_BK + 8 * fq;
+    auto load_w = [&](const R5Cursor& c, h8_t (&r)[6]) __attribute__((always_inline)) {
+        const half_t* src = (DUAL && c.q ? W2 : W1) + (int64_t)c.k * (RG_BN * R5_BK) + wcol;
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) r[nt] = *(const h8_t*)(src + nt * 16 * R5_BK);
+    };
+    // ---- biases of this wave's columns, both passes
+    h4_t bias[NP][6];
+#pragma unroll
+    for (int q = 0; q < NP; q++)
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++)
+            bias[q][nt] = *(const h4_t*)((const half_t*)(q ? p2.bias : p.bias) + 96 * wn + 16 * nt + 4 * fq);
+    f4_t acc[4][6];
+#pragma unroll
+    for (int mt = 0; mt < 4; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+    const int ar_off = (64 * wm + fr) * 64 + 16 * (fq ^ rc_sw(fr));   // + 1024 mt: row 64 wm + 16 mt + fr
+
+    auto epilogue = [&](int64_t t, auto qc) __attribute__((always_inline)) {
+        constexpr int q = decltype(qc)::value;
+        const dpvo_rowgemm_args& pe = q ? p2 : p;
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++) {
+            const int col = 96 * wn + 16 * nt + 4 * fq;
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++) {
+                h4_t y;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    half_t v = (half_t)(acc[mt][nt][r] + (float)bias[q][nt][r]);
+                    if (FLAGS & RG_RELU) v = v > (half_t)0 ? v : (half_t)0;
+                    if (FLAGS & RG_SIGMOID) v = (half_t)fast_sigmoid((float)v);
+                    y[r] = v;
+                }
+                acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+                *(h4_t*)(smem + ym.off(64 * wm + 16 * mt + fr, col * 2)) = y;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+        // whole rows out: wave w stores rows 16 w .. 16 w + 15, two per pass
+        // (lane half h: row 2 i + h, lane s: columns 4 s + 128 j)
+        const int h = lane >> 5, s = lane & 31;
+        half_t* out = (half_t*)pe.out16;
+#pragma unroll 2
+        for (int i = 0; i < 8; i++) {
+            const int lr = 16 * w + 2 * i + h;
+            const int64_t row = t * RG_BM + lr;
+            ep_h4 v[3];
+#pragma unroll
+            for (int j = 0; j < 3; j++) v[j] = *(const ep_h4*)(smem + ym.off(lr, (128 * j + 4 * s) * 2));
+            if (row < Mrows) {
+#pragma unroll
+                for (int j = 0; j < 3; j++) *(ep_h4*)(out + row * pe.ldo16 + 128 * j + 4 * s) = v[j];
+            }
+        }
+    };
+
+    // ---- prologue: stage 0 into slot 0; stages 1, 2 in registers; W stages 0, 1
+    const unsigned G = gridDim.x;
+    R5Cursor cur{0, (int64_t)blockIdx.x, 0, 0};   // step f
+    R5Cursor cw = cur, ca = cur;                   // W / A prefetch cursors
+    load_w(cw, wreg[0]);
+    cw.next(total, nks, NP, G);
+    load_w(cw, wreg[1]);
+    cw.next(total, nks, NP, G);                    // at f + 2
+    {
+        const h8_t a0 = load_a(ca);
+        *(h8_t*)(smem + R5_Y + aw_off) = a0;
+    }
+    ca.next(total, nks, NP, G);
+    areg[1] = load_a(ca);
+    ca.next(total, nks, NP, G);
+    areg[0] = load_a(ca);
+    ca.next(total, nks, NP, G);                    // at f + 3
+    // one k-step; PH = f mod 2 (register sets): stage f + 1 waits in
+    // areg[(f + 1) % 2], stage f + 2 in areg[f % 2]
+    auto step = [&](auto ph) __attribute__((always_inline)) {
+        constexpr int PH = decltype(ph)::value;
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_s_barrier();   // slot f & 1 holds stage f; slot (f + 1) & 1 was last read at f - 1
+        const char* sa = smem + R5_Y + PH * R5_ASLOT;
+        h8_t a[4];
+#pragma unroll
+        for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(sa + ar_off + 1024 * mt);
+        *(h8_t*)(smem + R5_Y + (PH ^ 1) * R5_ASLOT + aw_off) = areg[PH ^ 1];   // stage f + 1
+        areg[PH ^ 1] = load_a(ca);                                             // stage f + 3
+        ca.next(total, nks, NP, G);
+#pragma unroll
+        for (int nt = 0; nt < 6; nt++)
+#pragma unroll
+            for (int mt = 0; mt < 4; mt++)
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wreg[PH][nt], a[mt], acc[mt][nt], 0, 0, 0);
+        load_w(cw, wreg[PH]);                                                  // stage f + 2
+        cw.next(total, nks, NP, G);
+        if (cur.k == nks - 1) {
+            if (DUAL && cur.q)
+                epilogue(cur.t, std::integral_constant<int, DUAL ? 1 : 0>{});
+            else
+                epilogue(cur.t, std::integral_constant<int, 0>{});
+        }
+        cur.next(total, nks, NP, G);
+    };
+    for (int64_t f = 0; f < total; f += 2) {
+        step(std::integral_constant<int, 0>{});
+        if (f + 1 < total) step(std::integral_constant<int, 1>{});
+    }
+}
+
 // Roles (round 4): waves 0-3 issue every LDS-DMA stage (loaders: GEMM1 stages
 // 8 pieces each -- 2 A + 6 W --, W-only stages 6), so only they wait on the
 // stage vmcnt; all eight waves read fragments and issue MFMAs.
@@ -1009,7 +1207,15 @@ static int validate_rowgemm(const dpvo_rowgemm_args* a)
 {
     DPVO_CHECK_ARG(a != nullptr, "null args");
     DPVO_CHECK_ARG(a->N == RG_BN, "rowgemm: output width must be 384");
-    DPVO_CHECK_ARG(a->K > 0 && a->K % RG_BK == 0, "rowgemm: K must be a positive multiple of 64 (pad W with zeros)");
+    if (a->flags & DPVO_RG_WKB) {
+        DPVO_CHECK_ARG((a->flags & ~(DPVO_RG_WKB | DPVO_RG_RELU | DPVO_RG_SIGMOID)) == 0,
+                       "rowgemm: k-blocked W (WKB) takes only RELU / SIGMOID");
+        DPVO_CHECK_ARG(a->K > 0 && a->K % R5_BK == 0, "rowgemm: K must be a positive multiple of 32 with WKB");
+        DPVO_CHECK_ARG(a->out16 && a->ldo16 % 4 == 0 && ((uintptr_t)a->out16 & 7) == 0 && !a->out32,
+                       "rowgemm: WKB writes out16 only (8-byte aligned rows)");
+    } else {
+        DPVO_CHECK_ARG(a->K > 0 && a->K % RG_BK == 0, "rowgemm: K must be a positive multiple of 64 (pad W with zeros)");
+    }
     // (v2 stages K in steps of 32; every multiple of 64 is one)
     DPVO_CHECK_ARG(a->A && a->W && a->bias && a->zero_row, "rowgemm: A, W, bias and zero_row are required");
     DPVO_CHECK_ARG(a->lda >= a->K && a->lda % 8 == 0, "rowgemm: lda must be >= K and a multiple of 8");
@@ -1042,7 +1248,8 @@ static int ensure_num_cus()
 extern "C" int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_args* b, void* stream)
 {
     if (validate_rowgemm(a) || validate_rowgemm(b)) return -1;
-    DPVO_CHECK_ARG(a->flags == 0 && b->flags == 0, "rowgemm_pair: plain GEMMs only (flags 0)");
+    DPVO_CHECK_ARG((a->flags == 0 && b->flags == 0) || (a->flags == DPVO_RG_WKB && b->flags == DPVO_RG_WKB),
+                   "rowgemm_pair: plain GEMMs only (flags 0, or WKB on both)");
     DPVO_CHECK_ARG(a->A == b->A && a->lda == b->lda && a->a_idx == b->a_idx && a->a_rows == b->a_rows &&
                        a->K == b->K && a->M == b->M && a->M_dev == b->M_dev,
                    "rowgemm_pair: both GEMMs must share A, K and M");
@@ -1050,7 +1257,10 @@ extern "C" int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_
     if (ensure_num_cus()) return -1;
     const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
     const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
-    hipLaunchKernelGGL((rowgemm3_kernel<0, true>), dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, *b);
+    if (a->flags & DPVO_RG_WKB)
+        hipLaunchKernelGGL((rowgemm5_kernel<0, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b);
+    else
+        hipLaunchKernelGGL((rowgemm3_kernel<0, true>), dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, *b);
     DPVO_CHECK_LAUNCH();
     return 0;
 }
@@ -1064,6 +1274,15 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
     const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
     const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
     switch (f) {
+#define R5_CASE(F)                                                                                                  \
+    case (F) | DPVO_RG_WKB:                                                                                         \
+        hipLaunchKernelGGL((rowgemm5_kernel<(F), false>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, \
+                           *a);                                                                                     \
+        break;
+        R5_CASE(0)
+        R5_CASE(DPVO_RG_RELU)
+        R5_CASE(DPVO_RG_SIGMOID)
+#undef R5_CASE
 #define R3_CASE(F)                                                                                            \
     case (F):                                                                                                 \
         hipLaunchKernelGGL(rowgemm3_kernel<(F)>, dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, *a); \

@@ -48,9 +48,9 @@ class Update(nn.Module):
             return self._pk[1]
         P = update_ops.pack_linear
         ln = lambda m: (m.weight.detach().float().contiguous(), m.bias.detach().float().contiguous(), m.eps)
-        agg = lambda a: (P(a.f.weight, a.f.bias), P(a.g.weight, a.g.bias), P(a.h.weight, a.h.bias))
-        # chain operands (rowchain reads its W k-blocked: update_ops.kblock)
+        # chain operands and the plain GEMMs read their W k-blocked (update_ops.kblock)
         KB = lambda wb: (update_ops.kblock(wb[0]), wb[1])
+        agg = lambda a: (KB(P(a.f.weight, a.f.bias)), KB(P(a.g.weight, a.g.bias)), KB(P(a.h.weight, a.h.bias)))
         gr = lambda g: (KB(P(g.gate[0].weight, g.gate[0].bias)), KB(P(g.res[0].weight, g.res[0].bias)),
                         KB(P(g.res[2].weight, g.res[2].bias)))
         pk = {

@@ -287,7 +287,7 @@ def gather_rows(x, idx, dtype=None):
 # ---------------------------------------------------------------------------
 import ctypes as _ct  # noqa: E402
 
-RELU, SIGMOID, RES, GATE, LN, LN_RELU, HEADS = 1, 2, 4, 8, 16, 32, 64
+RELU, SIGMOID, RES, GATE, LN, LN_RELU, HEADS, WKB = 1, 2, 4, 8, 16, 32, 64, 128
 WIDTH = 384
 
 
@@ -364,9 +364,17 @@ def rowgemm(A, W16, b16, flags=0, a_idx=None, M=None, res32=None, res16=None, re
     H.on_gpu(A, W16, b16)
     if A.dtype != torch.float16 or W16.dtype != torch.float16 or b16.dtype != torch.float16:
         raise RuntimeError("rowgemm: A, W and bias must be fp16")
-    if A.dim() != 2 or A.stride(1) != 1 or W16.shape[0] != WIDTH or not W16.is_contiguous():
-        raise RuntimeError("rowgemm: A must be [rows, K] row-contiguous and W [384, Kp] contiguous")
-    Kp = W16.shape[1]
+    if W16.dim() == 3:   # k-blocked W (kblock): the plain-GEMM kernel without LDS-DMA (flags 0 / RELU / SIGMOID)
+        if flags & ~(RELU | SIGMOID) or want32 or out32 is not None:
+            raise RuntimeError("rowgemm: a k-blocked W takes only RELU / SIGMOID and writes out16")
+        Kp = _kb_K(W16)
+        flags |= WKB
+    elif W16.shape[0] != WIDTH or not W16.is_contiguous():
+        raise RuntimeError("rowgemm: W must be [384, Kp] contiguous (or k-blocked)")
+    else:
+        Kp = W16.shape[1]
+    if A.dim() != 2 or A.stride(1) != 1:
+        raise RuntimeError("rowgemm: A must be [rows, K] row-contiguous")
     if A.stride(0) < Kp:
         raise RuntimeError(f"rowgemm: A's row stride {A.stride(0)} < padded K {Kp}")
     dev = A.device
@@ -415,11 +423,15 @@ def rowgemm_pair(A, Wa, ba, Wb, bb, M_dev=None):
     H.on_gpu(A, Wa, ba, Wb, bb)
     if any(t.dtype != torch.float16 for t in (A, Wa, ba, Wb, bb)):
         raise RuntimeError("rowgemm_pair: A, weights and biases must be fp16")
-    if Wa.shape != Wb.shape or Wa.shape[0] != WIDTH or not (Wa.is_contiguous() and Wb.is_contiguous()):
-        raise RuntimeError("rowgemm_pair: Wa and Wb must be contiguous [384, Kp] of one shape")
-    if A.dim() != 2 or A.stride(1) != 1 or A.stride(0) < Wa.shape[1]:
+    if Wa.shape != Wb.shape or not (Wa.is_contiguous() and Wb.is_contiguous()):
+        raise RuntimeError("rowgemm_pair: Wa and Wb must be contiguous, of one shape")
+    kb = Wa.dim() == 3   # k-blocked (kblock): the plain-GEMM kernel without LDS-DMA
+    Kp = _kb_K(Wa) if kb else Wa.shape[1]
+    if not kb and Wa.shape[0] != WIDTH:
+        raise RuntimeError("rowgemm_pair: Wa and Wb must be [384, Kp] or k-blocked")
+    if A.dim() != 2 or A.stride(1) != 1 or A.stride(0) < Kp:
         raise RuntimeError("rowgemm_pair: A must be [rows, >=Kp] row-contiguous")
-    M, Kp, dev = A.shape[0], Wa.shape[1], A.device
+    M, dev = A.shape[0], A.device
     outs = []
     args = []
     for W, b in ((Wa, ba), (Wb, bb)):
@@ -427,7 +439,7 @@ def rowgemm_pair(A, Wa, ba, Wb, bb, M_dev=None):
         a = RowGemmArgs()
         a.A, a.lda, a.a_idx, a.a_rows = _p(A), A.stride(0), None, M
         a.W, a.K, a.N, a.bias, a.zero_row = _p(W), Kp, WIDTH, _p(b), _p(zero_row(dev, Kp))
-        a.M, a.flags = M, 0
+        a.M, a.flags = M, WKB if kb else 0
         a.out16, a.ldo16 = _p(o), o.stride(0)
         if M_dev is not None:
             if M_dev.dtype != torch.int64 or not M_dev.is_cuda:
