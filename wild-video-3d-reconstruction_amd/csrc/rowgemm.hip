@@ -563,7 +563,6 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = w & 1, wn = w >> 1;
     const int K = p.K, nks = K / R5_BK;
     const int64_t Mrows = p.M_dev ? min(*p.M_dev, p.M) : p.M;
     const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
@@ -596,38 +595,38 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     };
     // slot image: row r, physical chunk ac ^ rc_sw(r) holds logical chunk ac
     const int aw_off = ar * 64 + 16 * (ac ^ rc_sw(ar));
-    // ---- W fragments: column 96 wn + 16 nt + fr, k 8 fq .. 8 fq + 7 of the step
-    h8_t wreg[2][6];
+    // ---- W fragments: column 48 w + 16 nt + fr, k 8 fq .. 8 fq + 7 of the step
+    h8_t wreg[2][3];
     const half_t* W1 = (const half_t*)p.W;
     const half_t* W2 = DUAL ? (const half_t*)p2.W : W1;
-    const int wcol = (96 * wn + fr) * R5_BK + 8 * fq;
-    auto load_w = [&](const R5Cursor& c, h8_t (&r)[6]) __attribute__((always_inline)) {
+    const int wcol = (48 * w + fr) * R5_BK + 8 * fq;
+    auto load_w = [&](const R5Cursor& c, h8_t (&r)[3]) __attribute__((always_inline)) {
         const half_t* src = (DUAL && c.q ? W2 : W1) + (int64_t)c.k * (RG_BN * R5_BK) + wcol;
 #pragma unroll
-        for (int nt = 0; nt < 6; nt++) r[nt] = *(const h8_t*)(src + nt * 16 * R5_BK);
+        for (int nt = 0; nt < 3; nt++) r[nt] = *(const h8_t*)(src + nt * 16 * R5_BK);
     };
     // ---- biases of this wave's columns, both passes
-    h4_t bias[NP][6];
+    h4_t bias[NP][3];
 #pragma unroll
     for (int q = 0; q < NP; q++)
 #pragma unroll
-        for (int nt = 0; nt < 6; nt++)
-            bias[q][nt] = *(const h4_t*)((const half_t*)(q ? p2.bias : p.bias) + 96 * wn + 16 * nt + 4 * fq);
-    f4_t acc[4][6];
+        for (int nt = 0; nt < 3; nt++)
+            bias[q][nt] = *(const h4_t*)((const half_t*)(q ? p2.bias : p.bias) + 48 * w + 16 * nt + 4 * fq);
+    f4_t acc[8][3];
 #pragma unroll
-    for (int mt = 0; mt < 4; mt++)
+    for (int mt = 0; mt < 8; mt++)
 #pragma unroll
-        for (int nt = 0; nt < 6; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
-    const int ar_off = (64 * wm + fr) * 64 + 16 * (fq ^ rc_sw(fr));   // + 1024 mt: row 64 wm + 16 mt + fr
+        for (int nt = 0; nt < 3; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+    const int ar_off = fr * 64 + 16 * (fq ^ rc_sw(fr));   // + 1024 mt: row 16 mt + fr
 
     auto epilogue = [&](int64_t t, auto qc) __attribute__((always_inline)) {
         constexpr int q = decltype(qc)::value;
         const dpvo_rowgemm_args& pe = q ? p2 : p;
 #pragma unroll
-        for (int nt = 0; nt < 6; nt++) {
-            const int col = 96 * wn + 16 * nt + 4 * fq;
+        for (int nt = 0; nt < 3; nt++) {
+            const int col = 48 * w + 16 * nt + 4 * fq;
 #pragma unroll
-            for (int mt = 0; mt < 4; mt++) {
+            for (int mt = 0; mt < 8; mt++) {
                 h4_t y;
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
@@ -637,7 +636,7 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
                     y[r] = v;
                 }
                 acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
-                *(h4_t*)(smem + ym.off(64 * wm + 16 * mt + fr, col * 2)) = y;
+                *(h4_t*)(smem + ym.off(16 * mt + fr, col * 2)) = y;
             }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
@@ -684,16 +683,16 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_s_barrier();   // slot f & 1 holds stage f; slot (f + 1) & 1 was last read at f - 1
         const char* sa = smem + R5_Y + PH * R5_ASLOT;
-        h8_t a[4];
+        h8_t a[8];
 #pragma unroll
-        for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(sa + ar_off + 1024 * mt);
+        for (int mt = 0; mt < 8; mt++) a[mt] = *(const h8_t*)(sa + ar_off + 1024 * mt);
         *(h8_t*)(smem + R5_Y + (PH ^ 1) * R5_ASLOT + aw_off) = areg[PH ^ 1];   // stage f + 1
         areg[PH ^ 1] = load_a(ca);                                             // stage f + 3
         ca.next(total, nks, NP, G);
 #pragma unroll
-        for (int nt = 0; nt < 6; nt++)
+        for (int nt = 0; nt < 3; nt++)
 #pragma unroll
-            for (int mt = 0; mt < 4; mt++)
+            for (int mt = 0; mt < 8; mt++)
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wreg[PH][nt], a[mt], acc[mt][nt], 0, 0, 0);
         load_w(cw, wreg[PH]);                                                  // stage f + 2
         cw.next(total, nks, NP, G);
@@ -708,6 +707,342 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     for (int64_t f = 0; f < total; f += 2) {
         step(std::integral_constant<int, 0>{});
         if (f + 1 < total) step(std::integral_constant<int, 1>{});
+    }
+}
+
+// ---------------------------------------------------------------------------
+// v5 chains (round 4): rowchain_kernel's dataflow -- GEMM1 -> y tile -> GEMM2
+// [-> LayerNorm -> GEMM3 (TRI) | gate GEMM (GATED)] -> row epilogue -- on
+// rowgemm5's machinery: every W (k-blocked) streams from L2 into registers two
+// W-steps ahead over one flat per-block sequence (W1, then W2, then W3 / Wg),
+// A goes through registers into the 2-slot ring three A-steps ahead (GEMM1
+// and the gate pass), the GEMMs over the y tile read it in place and need no
+// barrier at all.  8 waves as 1 (M) x 8 (N), wave tile 128 x 48.  K1 % 64 == 0
+// keeps the register-set parities of both sequences equal to the k-step's.
+// OVL (residual-only epilogues): tile t's row epilogue runs inside tile
+// t + 1's GEMM1 k-loop on every wave (4 batches of 4 rows, the batch's loads
+// one k-step ahead of its arithmetic) -- GEMM1 never touches the y tile.
+// Per output element the MFMA k order and the epilogue arithmetic are
+// rowchain_kernel's: the same bits.
+// ---------------------------------------------------------------------------
+struct R5WCursor {   // (tile, segment, k-step) of the flat W-step sequence
+    int64_t f, t;
+    int s, k;
+    __device__ __forceinline__ void next(int64_t total, int n0, int n1, int n2, int nseg, unsigned grid)
+    {
+        if (f + 1 >= total) return;
+        f++;
+        if (++k == (s == 0 ? n0 : s == 1 ? n1 : n2)) {
+            k = 0;
+            if (++s == nseg) {
+                s = 0;
+                t += grid;
+            }
+        }
+    }
+};
+
+template <int F2, bool GATED = false, int FMID = 0>
+__global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
+                                                                  dpvo_rowgemm_args pg)
+{
+    constexpr bool TRI = FMID != 0;
+    static_assert(!(TRI && GATED), "a chain is either gated or three GEMMs long");
+    constexpr bool OVL = F2 == RG_RES;
+    constexpr int NSEG = (TRI || GATED) ? 3 : 2;
+    constexpr int NPA = GATED ? 2 : 1;   // A passes per tile
+    constexpr int nk2 = RG_BN / R5_BK;
+    constexpr int BIAS_OFF = R5_LDS;   // the three biases, 768 B each, after the A ring
+    __shared__ __attribute__((aligned(16))) char smem[R5_LDS + 3 * RG_BN * 2];
+    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int fr = lane & 15, fq = lane >> 4;
+    const int nk1 = p1.K / R5_BK;
+    const int64_t Mrows = p1.M_dev ? min(*p1.M_dev, p1.M) : p1.M;
+    const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
+    if ((int64_t)blockIdx.x >= ntiles) return;
+    const unsigned G = gridDim.x;
+    const int64_t my_tiles = (ntiles - 1 - blockIdx.x) / G + 1;
+    const int64_t total_a = my_tiles * NPA * nk1;
+    const int n2 = TRI ? nk2 : nk1;
+    const int64_t total_w = my_tiles * (nk1 + nk2 + (NSEG == 3 ? n2 : 0));
+    const YMapChunk ym;
+    const half_t* __restrict__ zero = (const half_t*)p1.zero_row;
+    // ---- A staging (rowgemm5's): lane holds row 16 w + (lane >> 2), chunk lane & 3
+    const int ar = 16 * w + (lane >> 2), ac = lane & 3;
+    int64_t a_tile = -1;
+    const half_t* arow = zero;
+    auto a_row = [&](int64_t t) __attribute__((always_inline)) {
+        if (t == a_tile) return;
+        a_tile = t;
+        const int64_t m = t * RG_BM + ar;
+        const half_t* row = zero;
+        if (m < Mrows) {
+            const int64_t src = p1.a_idx ? p1.a_idx[m] : m;
+            if (src >= 0 && src < p1.a_rows) row = (const half_t*)p1.A + src * p1.lda;
+        }
+        arow = row + 8 * ac;
+    };
+    h8_t areg[2];
+    auto load_a = [&](const R5Cursor& c) __attribute__((always_inline)) -> h8_t {
+        a_row(c.t);
+        return *(const h8_t*)(arow + c.k * R5_BK);
+    };
+    const int aw_off = ar * 64 + 16 * (ac ^ rc_sw(ar));
+    // ---- W: segment 0 = W1, 1 = the middle (TRI) or second Linear, 2 = the
+    // last (TRI) or the gate (GATED); fragments at column 48 w + 16 nt + fr
+    const half_t* Ws0 = (const half_t*)p1.W;
+    const half_t* Ws1 = (const half_t*)(TRI ? pg.W : p.W);
+    const half_t* Ws2 = (const half_t*)(TRI ? p.W : pg.W);
+    h8_t wreg[2][3];
+    const int wcol = (48 * w + fr) * R5_BK + 8 * fq;
+    auto load_w = [&](const R5WCursor& c, h8_t (&r)[3]) __attribute__((always_inline)) {
+        const half_t* base = c.s == 0 ? Ws0 : (c.s == 1 ? Ws1 : Ws2);
+        const half_t* src = base + (int64_t)c.k * (RG_BN * R5_BK) + wcol;
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) r[nt] = *(const h8_t*)(src + nt * 16 * R5_BK);
+    };
+    // ---- the biases (GEMM1, GEMM2, GEMM3 / gate) into LDS: read at the
+    // y-tile writes without waiting behind the W / A prefetch's vmcnt
+    if (threadIdx.x < 3 * 96) {
+        const int b = threadIdx.x / 96, c = 4 * (threadIdx.x % 96);
+        const void* src = b == 0 ? p1.bias : (b == 1 ? (TRI ? pg.bias : p.bias) : (TRI ? p.bias : pg.bias));
+        if (b < NSEG) *(h4_t*)(smem + BIAS_OFF + b * RG_BN * 2 + 2 * c) = *(const h4_t*)((const half_t*)src + c);
+    }
+    f4_t acc[8][3];
+    auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int mt = 0; mt < 8; mt++)
+#pragma unroll
+            for (int nt = 0; nt < 3; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+    };
+    const int ar_off = fr * 64 + 16 * (fq ^ rc_sw(fr));   // + 1024 mt: row 16 mt + fr
+    auto sync = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+    };
+    // acc + bias (LDS copy bi) -> act -> fp16 -> y tile
+    auto acc_to_y = [&](int bi, bool relu, bool sigm) __attribute__((always_inline)) {
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+            const int col = 48 * w + 16 * nt + 4 * fq;
+            const h4_t b = *(const h4_t*)(smem + BIAS_OFF + bi * RG_BN * 2 + 2 * col);
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) {
+                h4_t y;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    half_t v = (half_t)(acc[mt][nt][r] + (float)b[r]);
+                    if (relu) v = v > (half_t)0 ? v : (half_t)0;
+                    if (sigm) v = (half_t)fast_sigmoid((float)v);
+                    y[r] = v;
+                }
+                *(h4_t*)(smem + ym.off(16 * mt + fr, col * 2)) = y;
+            }
+        }
+    };
+    const unsigned bid = blockIdx.x;
+    R5Cursor ca{0, (int64_t)bid, 0, 0};
+    R5WCursor cw{0, (int64_t)bid, 0, 0};
+    auto wnext = [&]() __attribute__((always_inline)) { cw.next(total_w, nk1, nk2, n2, NSEG, G); };
+    auto anext = [&]() __attribute__((always_inline)) { ca.next(total_a, nk1, NPA, G); };
+    // one A-step (GEMM1 or the gate pass): stage g in slot g & 1, g + 1 in
+    // areg[(g + 1) & 1], g + 2 in areg[g & 1]; PH = g & 1 = the W-step's parity
+    auto step_a = [&](auto ph) __attribute__((always_inline)) {
+        constexpr int PH = decltype(ph)::value;
+        sync();
+        const char* sa = smem + R5_Y + PH * R5_ASLOT;
+        h8_t a[8];
+#pragma unroll
+        for (int mt = 0; mt < 8; mt++) a[mt] = *(const h8_t*)(sa + ar_off + 1024 * mt);
+        *(h8_t*)(smem + R5_Y + (PH ^ 1) * R5_ASLOT + aw_off) = areg[PH ^ 1];
+        areg[PH ^ 1] = load_a(ca);
+        anext();
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++)
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++)
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wreg[PH][nt], a[mt], acc[mt][nt], 0, 0, 0);
+        load_w(cw, wreg[PH]);
+        wnext();
+    };
+    // one k-step of a GEMM over the y tile (read in place; no barrier)
+    auto step_y = [&](auto ph, int ks) __attribute__((always_inline)) {
+        constexpr int PH = decltype(ph)::value;
+        h8_t a[8];
+#pragma unroll
+        for (int mt = 0; mt < 8; mt++) a[mt] = *(const h8_t*)(smem + ym.off(16 * mt + fr, (ks * 4 + fq) * 16));
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++)
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++)
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wreg[PH][nt], a[mt], acc[mt][nt], 0, 0, 0);
+        load_w(cw, wreg[PH]);
+        wnext();
+    };
+    auto gemm_y = [&]() __attribute__((always_inline)) {
+        zero_acc();
+#pragma unroll 1
+        for (int ks = 0; ks < nk2; ks += 2) {
+            step_y(std::integral_constant<int, 0>{}, ks);
+            step_y(std::integral_constant<int, 1>{}, ks + 1);
+        }
+    };
+    // TRI: LayerNorm (+ ReLU) of the y tile's rows in place, rounded to fp16
+    // (rowchain_kernel's mid_rows: epi2_finish's LN arithmetic)
+    auto mid_rows = [&](const dpvo_rowgemm_args& pm) __attribute__((always_inline)) {
+        EpiConsts2 km;
+        load_consts2<FMID>(pm, lane, km);
+        const int h = lane >> 5, s = lane & 31;
+#pragma unroll 1
+        for (int i = 0; i < 8; i++) {
+            const int r = w * 16 + 2 * i + h;
+            ep_f4 v[3];
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const ep_h4 y = *(const ep_h4*)(smem + ym.off(r, (128 * j + 4 * s) * 2));
+                v[j] = ep_f4{(float)y[0], (float)y[1], (float)y[2], (float)y[3]};
+            }
+            float sm = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; j++) sm += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
+            const float mean = half_sum(sm) * (1.f / RG_BN);
+            float sq = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                const ep_f4 d = v[j] - mean;
+                sq += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+            }
+            const float rstd = rsqrtf(half_sum(sq) * (1.f / RG_BN) + pm.ln_eps);
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                v[j] = (v[j] - mean) * rstd * km.g[j] + km.b[j];
+                if (FMID & RG_LN_RELU)
+#pragma unroll
+                    for (int t = 0; t < 4; t++) v[j][t] = fmaxf(v[j][t], 0.f);
+                *(ep_h4*)(smem + ym.off(r, (128 * j + 4 * s) * 2)) =
+                    ep_h4{(half_t)v[j][0], (half_t)v[j][1], (half_t)v[j][2], (half_t)v[j][3]};
+            }
+        }
+    };
+    // the row epilogue in batches of R rows: local rows lr .. lr + R - 1 of tile et
+    auto epi_issue = [&](int64_t et, int lr, auto& o) __attribute__((always_inline)) {
+        constexpr int R = sizeof(o.add) / sizeof(o.add[0][0]) / 3 * 2;
+        epi2_load<F2, R>(p, Mrows, et * RG_BM + lr, lane, o);
+    };
+    auto epi_done = [&](int64_t et, int lr, const EpiConsts2& kc, const auto& o) __attribute__((always_inline)) {
+        constexpr int R = sizeof(o.add) / sizeof(o.add[0][0]) / 3 * 2;
+        const int hh = lane >> 5, ss = lane & 31;
+        epi2_finish<F2, R>(
+            p, Mrows,
+            [&](int i, int j) { return *(const ep_h4*)(smem + ym.off(lr + 2 * i + hh, (128 * j + 4 * ss) * 2)); },
+            et * RG_BM + lr, lane, kc, o);
+    };
+
+    // ---- prologue: W-steps 0, 1 in registers; A stage 0 in slot 0, 1 and 2 in registers
+    load_w(cw, wreg[0]);
+    wnext();
+    load_w(cw, wreg[1]);
+    wnext();
+    {
+        const h8_t a0 = load_a(ca);
+        *(h8_t*)(smem + R5_Y + aw_off) = a0;
+    }
+    anext();
+    areg[1] = load_a(ca);
+    anext();
+    areg[0] = load_a(ca);
+    anext();
+    int64_t etile = -1;   // OVL: the tile whose row epilogue is still pending
+    for (int64_t tile = bid; tile < ntiles; tile += G) {
+        const bool more = tile + G < ntiles;
+        // ---- GEMM1 (+ OVL: the previous tile's row epilogue, rows 16 w .. 16 w + 15
+        // in 8 batches of 2: batch b's loads after k-step L(b) = b (nk1 - 3) / 7,
+        // its arithmetic after k-step L(b) + 1 <= nk1 - 2, before the last
+        // k-step's barrier)
+        {
+            EpiOps2<2> st;
+            int bi = 0, bd = 0;
+            auto ovl = [&](int ks) __attribute__((always_inline)) {
+                if (!OVL || etile < 0) return;
+                if (bd < bi) {
+                    EpiConsts2 kc;
+                    load_consts2<F2>(p, lane, kc);
+                    epi_done(etile, 16 * w + 2 * bd, kc, st);
+                    bd++;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                if (bi < 8 && (bi * (nk1 - 3)) / 7 == ks) {
+                    epi_issue(etile, 16 * w + 2 * bi, st);
+                    bi++;
+                }
+            };
+            zero_acc();
+#pragma unroll 1
+            for (int ks = 0; ks < nk1; ks += 2) {
+                step_a(std::integral_constant<int, 0>{});
+                ovl(ks);
+                step_a(std::integral_constant<int, 1>{});
+                ovl(ks + 1);
+            }
+        }
+        etile = -1;
+        acc_to_y(0, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
+        sync();
+        gemm_y();
+        sync();   // every wave is done reading the y tile
+        if (TRI) {
+            acc_to_y(1, false, false);
+            sync();
+            mid_rows(pg);
+            sync();
+            gemm_y();
+            sync();
+            acc_to_y(2, F2 & RG_RELU, F2 & RG_SIGMOID);
+        } else {
+            acc_to_y(1, F2 & RG_RELU, F2 & RG_SIGMOID);
+        }
+        if (GATED) {
+            // gate = sigmoid(A Wg^T + bg) (rowgemm's SIGMOID rounding); y = fp16(gate * y)
+            zero_acc();
+#pragma unroll 1
+            for (int ks = 0; ks < nk1; ks += 2) {
+                step_a(std::integral_constant<int, 0>{});
+                step_a(std::integral_constant<int, 1>{});
+            }
+#pragma unroll
+            for (int nt = 0; nt < 3; nt++) {
+                const int col = 48 * w + 16 * nt + 4 * fq;
+                const h4_t b = *(const h4_t*)(smem + BIAS_OFF + 2 * RG_BN * 2 + 2 * col);
+#pragma unroll
+                for (int mt = 0; mt < 8; mt++) {
+                    h4_t* yp = (h4_t*)(smem + ym.off(16 * mt + fr, col * 2));
+                    h4_t y = *yp;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const half_t g = (half_t)fast_sigmoid((float)(half_t)(acc[mt][nt][r] + (float)b[r]));
+                        y[r] = (half_t)((float)g * (float)y[r]);
+                    }
+                    *yp = y;
+                }
+            }
+        }
+        sync();
+        if (OVL && more && nk1 >= 12) {   // (12 k-steps fit the 8 batches' schedule)
+            etile = tile;   // runs inside the next tile's GEMM1
+            continue;
+        }
+        // the row epilogue now: rows 16 w .. 16 w + 15 (the next tile's y
+        // tile writes follow its GEMM1 k-steps' barriers)
+        EpiConsts2 kc;
+        load_consts2<F2>(p, lane, kc);
+#pragma unroll 1
+        for (int q0 = 0; q0 < 16; q0 += 4) {
+            EpiOps2<4> st;
+            epi_issue(tile, 16 * w + q0, st);
+            epi_done(tile, 16 * w + q0, kc, st);
+        }
     }
 }
 
@@ -1310,7 +1645,7 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
 {
     DPVO_CHECK_ARG(g1 != nullptr && g2 != nullptr, "null args");
     DPVO_CHECK_ARG(g1->N == RG_BN && g2->N == RG_BN, "rowchain: output widths must be 384");
-    DPVO_CHECK_ARG(g1->K > 0 && g1->K % RC_BK == 0, "rowchain: K1 must be a positive multiple of 32");
+    DPVO_CHECK_ARG(g1->K > 0 && g1->K % 64 == 0, "rowchain: K1 must be a positive multiple of 64");
     DPVO_CHECK_ARG(g2->K == RG_BN, "rowchain: the second GEMM's K must be 384 (the intermediate width)");
     DPVO_CHECK_ARG(g1->A && g1->W && g1->bias && g1->zero_row && g2->W && g2->bias,
                    "rowchain: A, W1, W2, both biases and zero_row are required");
@@ -1348,7 +1683,7 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
         switch (f) {
 #define RCG_CASE(F)                                                                                                   \
     case (F):                                                                                                         \
-        hipLaunchKernelGGL((rowchain_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES, true>), dim3(grid), dim3(RG_THREADS), \
+        hipLaunchKernelGGL((rowchain5_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES, true>), dim3(grid), dim3(R5_THREADS), \
                            0, as_stream(stream), *g1, a2, *gate);                                                     \
         break;
             RCG_CASE(DPVO_RG_GATE | DPVO_RG_LN)
@@ -1364,7 +1699,7 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
     switch (f) {
 #define RCH_CASE(F)                                                                                                   \
     case (F):                                                                                                         \
-        hipLaunchKernelGGL(rowchain_kernel<(F)>, dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *g1, a2, a2); \
+        hipLaunchKernelGGL(rowchain5_kernel<(F)>, dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, a2); \
         break;
         RCH_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
         RCH_CASE(DPVO_RG_RES)
@@ -1396,7 +1731,7 @@ extern "C" int dpvo_rowchain3(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_ar
                    "rowchain3: the middle epilogue must be LN | LN_RELU with 16-byte aligned LayerNorm parameters");
     DPVO_CHECK_ARG(g3->flags == (DPVO_RG_RES | DPVO_RG_LN), "rowchain3: the last epilogue must be RES | LN");
     DPVO_CHECK_ARG(g1->N == RG_BN && g3->N == RG_BN, "rowchain3: output widths must be 384");
-    DPVO_CHECK_ARG(g1->K > 0 && g1->K % RC_BK == 0, "rowchain3: K1 must be a positive multiple of 32");
+    DPVO_CHECK_ARG(g1->K > 0 && g1->K % 64 == 0, "rowchain3: K1 must be a positive multiple of 64");
     DPVO_CHECK_ARG(g3->K == RG_BN, "rowchain3: the last GEMM's K must be 384");
     DPVO_CHECK_ARG(g1->A && g1->W && g1->bias && g1->zero_row && g3->W && g3->bias,
                    "rowchain3: A, the three W, the biases and zero_row are required");
@@ -1420,8 +1755,8 @@ extern "C" int dpvo_rowchain3(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_ar
     dpvo_rowgemm_args a3 = *g3;
     a3.M = g1->M;
     a3.M_dev = g1->M_dev;
-    hipLaunchKernelGGL((rowchain_kernel<DPVO_RG_RES | DPVO_RG_LN, false, DPVO_RG_LN | DPVO_RG_LN_RELU>), dim3(grid),
-                       dim3(RG_THREADS), 0, as_stream(stream), *g1, a3, *g2);
+    hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | DPVO_RG_LN, false, DPVO_RG_LN | DPVO_RG_LN_RELU>), dim3(grid),
+                       dim3(R5_THREADS), 0, as_stream(stream), *g1, a3, *g2);
     DPVO_CHECK_LAUNCH();
     return 0;
 }
