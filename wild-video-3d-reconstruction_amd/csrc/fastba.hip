@@ -1568,6 +1568,7 @@ constexpr int BD_N6MAX = 6 * BD_NMAX;     // 72
 constexpr int BD_WAVES = 4;
 constexpr int BD_HD_LD = 64;   // row pitch of the dense lower-triangle system the wave solver loads
 constexpr int BD_GRID = 512;    // 4 waves each (measured over 256-2048: 512 is fastest at C3 and C2, scripts/exp_bd_grid.sh)
+static_assert(BD_GRID % 16 == 0, "bd_reduce_kernel: 16 waves split the partials evenly");
 static int bd_grid() { return BD_GRID; }
 
 struct BdLayout {
@@ -1968,17 +1969,21 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
 // H = sum of the patch kernel's workgroup partials, fixed order.  Also stored
 // as dense rows for the wave solver: Hd[b][a] = H(a, b) (a <= b, the lower
 // triangle, row pitch BD_HD_LD) and row n6 = g.
-__global__ __launch_bounds__(1024) void bd_reduce_kernel(BdParams p, int nparts)
+__global__ __launch_bounds__(1024) void bd_reduce_kernel(BdParams p)
 {
     __shared__ float red[16][64];
     if (*(volatile int*)p.status != 0) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int i = blockIdx.x * 64 + lane;
+    // all of this wave's partials in flight at once (one HBM round trip, not
+    // eight), then summed in partial order: the same bits as a running sum
+    constexpr int PER = BD_GRID / 16;
+    float v[PER];
+#pragma unroll
+    for (int j = 0; j < PER; j++) v[j] = i < p.ent ? p.Hpart[(int64_t)(wave + 16 * j) * p.ent + i] : 0.f;
     float s = 0.f;
-    if (i < p.ent) {
-#pragma unroll 4
-        for (int b = wave; b < nparts; b += 16) s += p.Hpart[(int64_t)b * p.ent + i];
-    }
+#pragma unroll
+    for (int j = 0; j < PER; j++) s += v[j];
     red[wave][lane] = s;
     __syncthreads();
     if (wave == 0 && i < p.ent) {
@@ -2338,7 +2343,7 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
         else
             hipLaunchKernelGGL((bd_patch_kernel<true, true>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p);
         if (p.N > 0) {
-            hipLaunchKernelGGL(bd_reduce_kernel, dim3(gR), dim3(1024), 0, s, p, bd_grid());
+            hipLaunchKernelGGL(bd_reduce_kernel, dim3(gR), dim3(1024), 0, s, p);   // (BD_GRID partials)
             bd_solve_launch(p, s);
         }
         DPVO_CHECK_LAUNCH();

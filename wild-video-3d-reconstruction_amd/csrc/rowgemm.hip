@@ -456,16 +456,9 @@ __global__ __launch_bounds__(RG_THREADS, 1) void rowgemm3_kernel(dpvo_rowgemm_ar
 // intermediate kept in LDS -- the update operator's Linear -> ReLU -> Linear
 // pairs (corr0/corr1, c1, c2, the GRU res branches; net.py:53-56,
 // blocks.py:27-30), whose 73 MB intermediates otherwise round-trip HBM.
-// LDS: the y tile (96 KB; GEMM2's A operand, then its output for the row
-// epilogue) + two 32 KB stages (BK = 32: A 8 KB | W 24 KB for GEMM1, W only
-// for GEMM2).  Transposed accumulators as in v3.
+// (rowchain5_kernel below; the y tile is GEMM2's A operand, then its output
+// for the row epilogue.)
 // ---------------------------------------------------------------------------
-constexpr int RC_BK = 32;
-constexpr int RC_A_STAGE = RG_BM * RC_BK * 2;      // 8 KB
-constexpr int RC_W_STAGE = RG_BN * RC_BK * 2;      // 24 KB
-constexpr int RC_STAGE = RC_A_STAGE + RC_W_STAGE;  // 32 KB
-constexpr int RC_Y = RG_BM * 768;                  // 96 KB
-constexpr int RC_LDS = RC_Y + 2 * RC_STAGE;        // 160 KB
 
 
 // chunk swizzle of the BK = 32 stage rows (64 B = four 16-byte chunks): the
@@ -516,25 +509,43 @@ struct YMapChunk {   // 128 rows x 768 B, 16-byte chunks XOR (row & 15): conflic
 // ---------------------------------------------------------------------------
 // v5 (round 4): the plain GEMM (flags 0 / RELU / SIGMOID) with a k-blocked W
 // and no LDS-DMA:
-//   * 8 waves as 2 (M) x 4 (N), wave tile 64 x 96 (4 x 6 accumulators), BK 32;
+//   * 8 waves as 1 (M) x 8 (N), wave tile 128 x 48 (8 x 3 accumulators), BK 32:
+//     every W fragment is read by one wave only (24 KB per k-step and CU from
+//     L2; the 2 x 4 layout read each twice: 93 -> 85 us for the SoftAgg pair);
 //   * W ([K/32][384][32]: a fragment = one contiguous 1 KB, whole lines)
 //     streams from L2 straight into registers, two k-steps ahead -- no LDS
 //     traffic for W;
-//   * A (128 rows x 64 B per k-step) goes global -> registers -> a 2-slot LDS
-//     ring (register staging, three k-steps ahead; rc_sw chunk swizzle,
+//   * A (128 rows x 64 B per k-step) goes global -> registers -> a 4-slot LDS
+//     ring (register staging, four k-steps ahead; rc_sw chunk swizzle,
 //     conflict-free fragment reads);
-//   * one barrier per k-step; every wait is the compiler's exact count of the
-//     wave's own loads and stores (nothing is in flight that it cannot see);
+//   * one barrier per TWO k-steps (in-kernel stamps: with one per k-step the
+//     waves of a SIMD met at every step, the younger ~500 cycles behind); every
+//     wait is the compiler's exact count of the wave's own loads and stores;
 //   * the row epilogue stages y16 through a 96 KB LDS tile and stores whole
 //     rows, with the next tile's first loads already in flight ahead of it.
+// (Measured and not kept: W / A prefetched three or four k-steps ahead -- the
+// vmcnt waits are ~10 % of a k-step, no gain; the next k-step's fragments read
+// between this one's MFMAs -- 79 -> 91 us.)
 // Persistent blocks walk a flat (tile, pass, k-step) sequence; DUAL runs a
 // second GEMM (p2's W, bias, out16) on the same A tile right after the first.
 // Per output element the MFMA k order is rowgemm3's: the same bits.
 // ---------------------------------------------------------------------------
+// f(integral_constant<int, K>) for K = B .. E-1, expanded at compile time
+template <int B, int E>
+struct bd_steps {
+    template <class F>
+    __device__ __forceinline__ static void run(F&& f)
+    {
+        if constexpr (B < E) {
+            f(std::integral_constant<int, B>{});
+            bd_steps<B + 1, E>::run(f);
+        }
+    }
+};
 constexpr int R5_THREADS = 512, R5_BK = 32;
 constexpr int R5_Y = RG_BM * 768;                  // 96 KB
 constexpr int R5_ASLOT = RG_BM * R5_BK * 2;        // 8 KB
-constexpr int R5_LDS = R5_Y + 2 * R5_ASLOT;        // 112 KB
+constexpr int R5_LDS = R5_Y + 4 * R5_ASLOT;        // 128 KB
 
 // (tile, pass, k-step) of a flat step, advanced one step at a time (no
 // 64-bit divisions); past the end it stays on the last step
@@ -555,7 +566,7 @@ struct R5Cursor {
     }
 };
 
-template <int FLAGS, bool DUAL>
+template <int FLAGS, bool DUAL, bool DIRECT = false>
 __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_args p, dpvo_rowgemm_args p2)
 {
     static_assert((FLAGS & ~(RG_RELU | RG_SIGMOID)) == 0, "v5: plain GEMMs only");
@@ -622,6 +633,29 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     auto epilogue = [&](int64_t t, auto qc) __attribute__((always_inline)) {
         constexpr int q = decltype(qc)::value;
         const dpvo_rowgemm_args& pe = q ? p2 : p;
+        if (DIRECT) {
+            // straight from the accumulators: lane (fr, fq) owns row 16 mt + fr,
+            // columns 48 w + 16 nt + 4 fq .. + 3 (8 B); no LDS, no barrier
+            half_t* out = (half_t*)pe.out16;
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++) {
+                const int64_t row = t * RG_BM + 16 * mt + fr;
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++) {
+                    h4_t y;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        half_t v = (half_t)(acc[mt][nt][r] + (float)bias[q][nt][r]);
+                        if (FLAGS & RG_RELU) v = v > (half_t)0 ? v : (half_t)0;
+                        if (FLAGS & RG_SIGMOID) v = (half_t)fast_sigmoid((float)v);
+                        y[r] = v;
+                    }
+                    acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+                    if (row < Mrows) *(h4_t*)(out + row * pe.ldo16 + 48 * w + 16 * nt + 4 * fq) = y;
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
             const int col = 48 * w + 16 * nt + 4 * fq;
@@ -659,71 +693,106 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
         }
     };
 
-    // ---- prologue: stage 0 into slot 0; stages 1, 2 in registers; W stages 0, 1
+    // ---- prologue: stages 0, 1 into slots 0, 1; stages 2, 3 in registers
+    // (stage g: slot g % 4, register set g % 2); W stages 0, 1 (stage f in
+    // wreg[f % 2])
     const unsigned G = gridDim.x;
     R5Cursor cur{0, (int64_t)blockIdx.x, 0, 0};   // step f
     R5Cursor cw = cur, ca = cur;                   // W / A prefetch cursors
-    load_w(cw, wreg[0]);
-    cw.next(total, nks, NP, G);
-    load_w(cw, wreg[1]);
-    cw.next(total, nks, NP, G);                    // at f + 2
-    {
-        const h8_t a0 = load_a(ca);
-        *(h8_t*)(smem + R5_Y + aw_off) = a0;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        load_w(cw, wreg[r]);
+        cw.next(total, nks, NP, G);
     }
-    ca.next(total, nks, NP, G);
-    areg[1] = load_a(ca);
-    ca.next(total, nks, NP, G);
-    areg[0] = load_a(ca);
-    ca.next(total, nks, NP, G);                    // at f + 3
-    // one k-step; PH = f mod 2 (register sets): stage f + 1 waits in
-    // areg[(f + 1) % 2], stage f + 2 in areg[f % 2]
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const h8_t x = load_a(ca);
+        *(h8_t*)(smem + R5_Y + r * R5_ASLOT + aw_off) = x;
+        ca.next(total, nks, NP, G);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        areg[r] = load_a(ca);
+        ca.next(total, nks, NP, G);
+    }
+#ifdef DPVO_STAMPS
+    unsigned long long st_sum[ST_SEGS] = {};
+    RC_STAMP(t_begin)
+#endif
+    // one k-step, PH = f mod 4: stage f is read from slot f % 4 and stage
+    // f + 2 written into slot (f + 2) % 4.  One barrier per TWO k-steps (even
+    // f): it makes stages f, f + 1 visible (written at f - 2, f - 1) and frees
+    // slots (f + 2) % 4, (f + 3) % 4 (stages f - 2, f - 1, read at f - 2,
+    // f - 1), so the waves of a SIMD may drift a k-step apart between them.
     auto step = [&](auto ph) __attribute__((always_inline)) {
         constexpr int PH = decltype(ph)::value;
-        __builtin_amdgcn_s_waitcnt(0xc07f);
-        __builtin_amdgcn_s_barrier();   // slot f & 1 holds stage f; slot (f + 1) & 1 was last read at f - 1
+        constexpr int PR = PH & 1;
+        RC_STAMP(s0)
+        if (PR == 0) {
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_s_barrier();
+        }
+        RC_STAMP(s1)
+#ifdef DPVO_STAMPS
+        asm volatile("" ::"v"(areg[PR]), "v"(wreg[PR][0]), "v"(wreg[PR][1]), "v"(wreg[PR][2]));
+#endif
+        RC_STAMP(s2)
         const char* sa = smem + R5_Y + PH * R5_ASLOT;
         h8_t a[8];
 #pragma unroll
         for (int mt = 0; mt < 8; mt++) a[mt] = *(const h8_t*)(sa + ar_off + 1024 * mt);
-        *(h8_t*)(smem + R5_Y + (PH ^ 1) * R5_ASLOT + aw_off) = areg[PH ^ 1];   // stage f + 1
-        areg[PH ^ 1] = load_a(ca);                                             // stage f + 3
+        *(h8_t*)(smem + R5_Y + ((PH + 2) & 3) * R5_ASLOT + aw_off) = areg[PR];   // stage f + 2
+        areg[PR] = load_a(ca);                                                 // stage f + 4
         ca.next(total, nks, NP, G);
 #pragma unroll
         for (int nt = 0; nt < 3; nt++)
 #pragma unroll
             for (int mt = 0; mt < 8; mt++)
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wreg[PH][nt], a[mt], acc[mt][nt], 0, 0, 0);
-        load_w(cw, wreg[PH]);                                                  // stage f + 2
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wreg[PR][nt], a[mt], acc[mt][nt], 0, 0, 0);
+        load_w(cw, wreg[PR]);                                                  // W stage f + 2
         cw.next(total, nks, NP, G);
+        RC_STAMP(s3)
+        RC_ACC(0, s0, s1) RC_ACC(1, s1, s2) RC_ACC(2, s2, s3)
         if (cur.k == nks - 1) {
             if (DUAL && cur.q)
                 epilogue(cur.t, std::integral_constant<int, DUAL ? 1 : 0>{});
             else
                 epilogue(cur.t, std::integral_constant<int, 0>{});
+            RC_STAMP(s4)
+            RC_ACC(3, s3, s4)
         }
         cur.next(total, nks, NP, G);
     };
-    for (int64_t f = 0; f < total; f += 2) {
-        step(std::integral_constant<int, 0>{});
-        if (f + 1 < total) step(std::integral_constant<int, 1>{});
+    for (int64_t f = 0; f < total; f += 4) {
+        bd_steps<0, 4>::run([&](auto pc) __attribute__((always_inline)) {
+            if (f + decltype(pc)::value < total) step(pc);
+        });
     }
+#ifdef DPVO_STAMPS
+    RC_STAMP(t_end)
+    st_sum[10] += t_end - t_begin;
+    if (lane == 0)
+        for (int k = 0; k < ST_SEGS; k++) dpvo_stamps[((int64_t)blockIdx.x * 8 + w) * ST_SEGS + k] = st_sum[k];
+#endif
 }
 
 // ---------------------------------------------------------------------------
-// v5 chains (round 4): rowchain_kernel's dataflow -- GEMM1 -> y tile -> GEMM2
+// v5 chains (round 4): the chain dataflow -- GEMM1 -> y tile -> GEMM2
 // [-> LayerNorm -> GEMM3 (TRI) | gate GEMM (GATED)] -> row epilogue -- on
 // rowgemm5's machinery: every W (k-blocked) streams from L2 into registers two
 // W-steps ahead over one flat per-block sequence (W1, then W2, then W3 / Wg),
-// A goes through registers into the 2-slot ring three A-steps ahead (GEMM1
-// and the gate pass), the GEMMs over the y tile read it in place and need no
-// barrier at all.  8 waves as 1 (M) x 8 (N), wave tile 128 x 48.  K1 % 64 == 0
-// keeps the register-set parities of both sequences equal to the k-step's.
+// A goes through registers into the 4-slot ring (GEMM1 and the gate pass; one
+// barrier per two A-steps), the GEMMs over the y tile read it in place and
+// need no barrier at all.  8 waves as 1 (M) x 8 (N), wave tile 128 x 48.
+// K1 % 64 == 0 keeps the register-set parities of both sequences equal to the
+// k-step's.  The biases sit in LDS (read at the y-tile writes without waiting
+// behind the prefetch's vmcnt; in registers the LN chains spilled).
 // OVL (residual-only epilogues): tile t's row epilogue runs inside tile
-// t + 1's GEMM1 k-loop on every wave (4 batches of 4 rows, the batch's loads
+// t + 1's GEMM1 k-loop on every wave (8 batches of 2 rows, each batch's loads
 // one k-step ahead of its arithmetic) -- GEMM1 never touches the y tile.
-// Per output element the MFMA k order and the epilogue arithmetic are
-// rowchain_kernel's: the same bits.
+// (Measured at C3 shapes: 151 us with it, 156 without; two batches in flight
+// spill.)  Per output element the MFMA k order and the epilogue arithmetic are
+// rowgemm3's: bit-identical to the unchained launches.
 // ---------------------------------------------------------------------------
 struct R5WCursor {   // (tile, segment, k-step) of the flat W-step sequence
     int64_t f, t;
@@ -849,16 +918,22 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
     auto anext = [&]() __attribute__((always_inline)) { ca.next(total_a, nk1, NPA, G); };
     // one A-step (GEMM1 or the gate pass): stage g in slot g & 1, g + 1 in
     // areg[(g + 1) & 1], g + 2 in areg[g & 1]; PH = g & 1 = the W-step's parity
+    // one A-step g (GEMM1 or the gate pass), PH = g & 1: stage g from slot
+    // g % 4, stage g + 2 (register set PH) into slot (g + 2) % 4, stage g + 4
+    // loaded into set PH.  One barrier per two A-steps (even g): it makes
+    // stages g, g + 1 visible and frees the slots of stages g - 2, g - 1.
+    int ga = 0;
     auto step_a = [&](auto ph) __attribute__((always_inline)) {
         constexpr int PH = decltype(ph)::value;
-        sync();
-        const char* sa = smem + R5_Y + PH * R5_ASLOT;
+        if (PH == 0) sync();
+        const char* sa = smem + R5_Y + (ga & 3) * R5_ASLOT;
         h8_t a[8];
 #pragma unroll
         for (int mt = 0; mt < 8; mt++) a[mt] = *(const h8_t*)(sa + ar_off + 1024 * mt);
-        *(h8_t*)(smem + R5_Y + (PH ^ 1) * R5_ASLOT + aw_off) = areg[PH ^ 1];
-        areg[PH ^ 1] = load_a(ca);
+        *(h8_t*)(smem + R5_Y + ((ga + 2) & 3) * R5_ASLOT + aw_off) = areg[PH];
+        areg[PH] = load_a(ca);
         anext();
+        ga++;
 #pragma unroll
         for (int nt = 0; nt < 3; nt++)
 #pragma unroll
@@ -890,7 +965,7 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
         }
     };
     // TRI: LayerNorm (+ ReLU) of the y tile's rows in place, rounded to fp16
-    // (rowchain_kernel's mid_rows: epi2_finish's LN arithmetic)
+    // (epi2_finish's LN arithmetic)
     auto mid_rows = [&](const dpvo_rowgemm_args& pm) __attribute__((always_inline)) {
         EpiConsts2 km;
         load_consts2<FMID>(pm, lane, km);
@@ -940,20 +1015,23 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
             et * RG_BM + lr, lane, kc, o);
     };
 
-    // ---- prologue: W-steps 0, 1 in registers; A stage 0 in slot 0, 1 and 2 in registers
+    // ---- prologue: W-steps 0, 1 in registers; A stages 0, 1 in slots 0, 1,
+    // 2 and 3 in register sets 0, 1
     load_w(cw, wreg[0]);
     wnext();
     load_w(cw, wreg[1]);
     wnext();
-    {
-        const h8_t a0 = load_a(ca);
-        *(h8_t*)(smem + R5_Y + aw_off) = a0;
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        const h8_t x = load_a(ca);
+        *(h8_t*)(smem + R5_Y + r * R5_ASLOT + aw_off) = x;
+        anext();
     }
-    anext();
-    areg[1] = load_a(ca);
-    anext();
-    areg[0] = load_a(ca);
-    anext();
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+        areg[r] = load_a(ca);
+        anext();
+    }
     int64_t etile = -1;   // OVL: the tile whose row epilogue is still pending
     for (int64_t tile = bid; tile < ntiles; tile += G) {
         const bool more = tile + G < ntiles;
@@ -1044,396 +1122,6 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
             epi_done(tile, 16 * w + q0, kc, st);
         }
     }
-}
-
-// Roles (round 4): waves 0-3 issue every LDS-DMA stage (loaders: GEMM1 stages
-// 8 pieces each -- 2 A + 6 W --, W-only stages 6), so only they wait on the
-// stage vmcnt; all eight waves read fragments and issue MFMAs.
-// OVL (the residual-only chains c1 / c2): the row epilogue of tile t is
-// deferred into the next tile's GEMM1 k-loop -- GEMM1 does not touch the y
-// tile, which still holds tile t's output -- where waves 4-7 run it in
-// row-pair batches after each k-step's MFMAs (16 batches of 2 rows per wave,
-// spread over the k-steps, the next batch's residual loads in flight while one
-// is finished).  Their loads and stores never enter the loaders' vmcnt, and
-// the epilogue's HBM traffic overlaps the k-loops instead of following them.
-// The last tile's epilogue runs after the loop on all eight waves.  The
-// arithmetic per row is epi2_finish's either way: bit-identical results.
-// (Measured at C3: c1 / c2 137 -> 129 us.  With the LayerNorm epilogues the
-// deferred batch's state spills beside the accumulators, and a variant whose
-// GEMM1 runs on the loader waves alone -- 8 x 6 accumulators each, waves 4-7
-// free -- spills ~700 B per lane.)
-template <int F2, bool GATED = false, int FMID = 0>
-__global__ __launch_bounds__(RG_THREADS, 1) void rowchain_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
-                                                                 dpvo_rowgemm_args pg)
-{
-    constexpr bool TRI = FMID != 0;
-    // (the LayerNorm chains' epilogue state does not fit beside the accumulators: spills)
-    constexpr bool OVL = F2 == RG_RES;
-    static_assert(!(TRI && GATED), "a chain is either gated or three GEMMs long");
-    __shared__ __attribute__((aligned(16))) char smem[RC_LDS];
-    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave & 1, wn = wave >> 1;
-    const bool ldw = wave < 4;   // loader waves
-    const int lw = wave & 3;
-    const int K1 = p1.K, ks1 = K1 / RC_BK, ks2 = RG_BN / RC_BK;
-    const int64_t Mrows = p1.M_dev ? min(*p1.M_dev, p1.M) : p1.M;
-    const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
-    if ((int64_t)blockIdx.x >= ntiles) return;
-    const half_t* __restrict__ W1 = (const half_t*)p1.W;
-    const half_t* __restrict__ W2 = (const half_t*)(TRI ? pg.W : p.W);
-    const half_t* __restrict__ zero = (const half_t*)p1.zero_row;
-    // TRI: the third GEMM's W stages come from p.W ([384][384] like W2)
-    const int64_t w3delta = TRI ? (const half_t*)p.W - W2 : 0;
-    const YMapChunk ym;
-    // piece (1 KB = 16 rows x 64 B) lane mapping: row base + L/4, physical chunk
-    // L%4 holding logical chunk (L%4) ^ rc_sw(row); rc_sw(16 q + srow) = rc_sw(srow)
-    const int srow = lane >> 2, pch = lane & 3;
-    // loader lw: A pieces 2 lw, 2 lw + 1 (rows 16 piece + srow) and, in the
-    // k-blocked W ([K/32][384][32]: a stage is one contiguous 384 x 32 block),
-    // W pieces 6 lw .. 6 lw + 5, 512 elements apart
-    const half_t* a1src[2];
-    auto set_tile = [&](int64_t tile) {
-#pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const int r = (2 * lw + j) * 16 + srow;
-            const int64_t m = tile * RG_BM + r;
-            const half_t* row = zero;
-            if (m < Mrows) {
-                const int64_t s = p1.a_idx ? p1.a_idx[m] : m;
-                if (s >= 0 && s < p1.a_rows) row = (const half_t*)p1.A + s * p1.lda;
-            }
-            a1src[j] = row + 8 * (pch ^ rc_sw(r));
-        }
-    };
-    const int wq = (6 * lw * 16 + srow) * RC_BK + 8 * (pch ^ rc_sw(srow));
-    // gate pass: the same stage layout, W pieces from Wg ([384][K1] like W1)
-    const int64_t gdelta = GATED ? (const half_t*)pg.W - W1 : 0;
-    auto issue1 = [&](int ks, int buf, bool gate = false) {   // loaders only
-        char* st = smem + RC_Y + buf * RC_STAGE;
-#pragma unroll
-        for (int j = 0; j < 2; j++) glds16(a1src[j] + ks * RC_BK, st + (2 * lw + j) * 1024);
-        const half_t* w = W1 + wq + (int64_t)ks * (RG_BN * RC_BK) + (GATED && gate ? gdelta : 0);
-#pragma unroll
-        for (int j = 0; j < 6; j++) glds16(w + 512 * j, st + (8 + 6 * lw + j) * 1024);
-    };
-    auto issue2 = [&](int ks, int buf, int64_t wdelta = 0) {   // loaders only
-        char* st = smem + RC_Y + buf * RC_STAGE + RC_A_STAGE;
-        const half_t* w = W2 + wq + (int64_t)ks * (RG_BN * RC_BK) + wdelta;
-#pragma unroll
-        for (int j = 0; j < 6; j++) glds16(w + 512 * j, st + (6 * lw + j) * 1024);
-    };
-    auto sync_lds = [&]() {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-    f4_t acc[4][6];
-    const int fr = lane & 15, fq = lane >> 4;
-    int a_off[4], w_off[6];
-#pragma unroll
-    for (int mt = 0; mt < 4; mt++) {
-        const int row = wm * 64 + mt * 16 + fr;
-        a_off[mt] = row * 64 + 16 * (fq ^ rc_sw(row));
-    }
-#pragma unroll
-    for (int nt = 0; nt < 6; nt++) {
-        const int n = wn * 96 + nt * 16 + fr;
-        w_off[nt] = RC_A_STAGE + n * 64 + 16 * (fq ^ rc_sw(n));
-    }
-    auto zero_acc = [&]() {
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-            for (int nt = 0; nt < 6; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
-    };
-    auto mfma_step = [&](const h8_t (&a)[4], const h8_t (&b)[6]) {
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-            for (int nt = 0; nt < 6; nt++)
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[nt], a[mt], acc[mt][nt], 0, 0, 0);
-    };
-    // one GEMM1 k-step's fragment reads and MFMAs from stage buffer buf
-    auto step1 = [&](int buf) {
-        const char* st = smem + RC_Y + buf * RC_STAGE;
-        h8_t a[4], b[6];
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(st + a_off[mt]);
-#pragma unroll
-        for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
-        mfma_step(a, b);
-    };
-    // acc + bias -> act -> fp16 -> y tile (row mt*16+fr, columns 4 fq.. of block nt)
-    // (called before any stage prefetch is in flight: its bias loads would
-    // otherwise wait behind the prefetch in the in-order vmcnt)
-    auto acc_to_y = [&](const half_t* bias_p, bool relu, bool sigm) {
-#pragma unroll
-        for (int nt = 0; nt < 6; nt++) {
-            const int col = wn * 96 + nt * 16 + 4 * fq;
-            const h4_t bias = *(const h4_t*)(bias_p + col);
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++) {
-                h4_t y;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    half_t v = (half_t)(acc[mt][nt][r] + (float)bias[r]);
-                    if (relu) v = v > (half_t)0 ? v : (half_t)0;
-                    if (sigm) v = (half_t)fast_sigmoid((float)v);
-                    y[r] = v;
-                }
-                *(h4_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, col * 2)) = y;
-            }
-        }
-    };
-    // TRI: LayerNorm (+ ReLU) of the y tile's rows in place, rounded to fp16 --
-    // epi2_finish's LN arithmetic (two rows per wave pass, lane s of half h
-    // owning columns 4 s + 128 j), the result written back instead of stored
-    auto mid_rows = [&](const dpvo_rowgemm_args& pm) {
-        if (!TRI) return;
-        EpiConsts2 km;
-        load_consts2<FMID>(pm, lane, km);
-        const int h = lane >> 5, s = lane & 31;
-#pragma unroll 1
-        for (int i = 0; i < 8; i++) {
-            const int r = wave * 16 + 2 * i + h;
-            ep_f4 v[3];
-#pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const ep_h4 y = *(const ep_h4*)(smem + ym.off(r, (128 * j + 4 * s) * 2));
-                v[j] = ep_f4{(float)y[0], (float)y[1], (float)y[2], (float)y[3]};
-            }
-            float sm = 0.f;
-#pragma unroll
-            for (int j = 0; j < 3; j++) sm += (v[j][0] + v[j][1]) + (v[j][2] + v[j][3]);
-            const float mean = half_sum(sm) * (1.f / RG_BN);
-            float sq = 0.f;
-#pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const ep_f4 d = v[j] - mean;
-                sq += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
-            }
-            const float rstd = rsqrtf(half_sum(sq) * (1.f / RG_BN) + pm.ln_eps);
-#pragma unroll
-            for (int j = 0; j < 3; j++) {
-                v[j] = (v[j] - mean) * rstd * km.g[j] + km.b[j];
-                if (FMID & RG_LN_RELU)
-#pragma unroll
-                    for (int t = 0; t < 4; t++) v[j][t] = fmaxf(v[j][t], 0.f);
-                *(ep_h4*)(smem + ym.off(r, (128 * j + 4 * s) * 2)) =
-                    ep_h4{(half_t)v[j][0], (half_t)v[j][1], (half_t)v[j][2], (half_t)v[j][3]};
-            }
-        }
-    };
-    // ---- the row epilogue in batches of 4 rows (two row pairs): local rows
-    // lr .. lr + 3 of tile `et`
-    auto epi_issue = [&](int64_t et, int lr, EpiOps2<4>& o) {
-        epi2_load<F2, 4>(p, Mrows, et * RG_BM + lr, lane, o);
-    };
-    auto epi_done = [&](int64_t et, int lr, const EpiConsts2& kc, const EpiOps2<4>& o) {
-        const int hh = lane >> 5, ss = lane & 31;
-        epi2_finish<F2, 4>(
-            p, Mrows,
-            [&](int i, int j) { return *(const ep_h4*)(smem + ym.off(lr + 2 * i + hh, (128 * j + 4 * ss) * 2)); },
-            et * RG_BM + lr, lane, kc, o);
-    };
-#ifdef DPVO_STAMPS
-    unsigned long long st_sum[ST_SEGS] = {};
-#endif
-    int64_t etile = -1;   // OVL: the tile whose row epilogue is still pending
-    // GEMM1 (A gathered x W1); OVL: waves 4-7 run the pending epilogue meanwhile
-    auto gemm1 = [&](bool gate) {
-        if (ldw) {
-            for (int ks = 0; ks < ks1; ks++) {
-                RC_STAMP(t0)
-                if (ks + 1 < ks1) {
-                    issue1(ks + 1, (ks + 1) & 1, gate);
-                    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                RC_STAMP(t1)
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-                RC_STAMP(t2)
-                step1(ks & 1);
-                RC_STAMP(t3)
-                __builtin_amdgcn_s_barrier();
-                RC_STAMP(t4)
-                RC_ACC(0, t0, t1) RC_ACC(1, t1, t2) RC_ACC(2, t2, t3) RC_ACC(3, t3, t4)
-            }
-        } else if (OVL && !gate && etile >= 0) {
-            // rows 32 e .. 32 e + 31 (e = wave - 4) in 8 batches of 4: batch b's
-            // residual loads issued after k-step L(b) = b (ks1 - 1) / 8, the batch
-            // finished after k-step L(b) + 1 (one k-step of load latency hidden;
-            // one batch of loads live at a time)
-            const int lr0 = 32 * (wave - 4);
-            EpiOps2<4> st;
-            int bi = 0, bd = 0;   // next batch to issue / to finish
-            for (int ks = 0; ks < ks1; ks++) {
-                RC_STAMP(t1)
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-                RC_STAMP(t2)
-                step1(ks & 1);
-                RC_STAMP(t3)
-                RC_ACC(1, t1, t2) RC_ACC(2, t2, t3)
-                if (bd < bi) {
-                    // LayerNorm constants per batch (L1 hits), not held across the
-                    // k-steps: the register budget is the accumulators' here
-                    EpiConsts2 kc;
-                    load_consts2<F2>(p, lane, kc);
-                    epi_done(etile, lr0 + 4 * bd, kc, st);
-                    bd++;
-                }
-                // (the next batch's loads may not move above this batch's
-                // arithmetic: both would be live at once)
-                __builtin_amdgcn_sched_barrier(0);
-                if (bi < 8 && (bi * (ks1 - 1)) / 8 == ks) {
-                    epi_issue(etile, lr0 + 4 * bi, st);
-                    bi++;
-                }
-                RC_STAMP(t35)
-                __builtin_amdgcn_s_barrier();
-                RC_STAMP(t4)
-                RC_ACC(4, t3, t35) RC_ACC(3, t35, t4)
-            }
-        } else {
-            for (int ks = 0; ks < ks1; ks++) {
-                RC_STAMP(t1)
-                __builtin_amdgcn_s_barrier();
-                asm volatile("" ::: "memory");
-                RC_STAMP(t2)
-                step1(ks & 1);
-                RC_STAMP(t3)
-                __builtin_amdgcn_s_barrier();
-                RC_STAMP(t4)
-                RC_ACC(1, t1, t2) RC_ACC(2, t2, t3) RC_ACC(3, t3, t4)
-            }
-        }
-    };
-    // GEMM over the y tile (stage 0 already issued); wdelta selects W3
-    auto gemm_y = [&](int64_t wdelta) {
-        zero_acc();
-#pragma unroll 1
-        for (int ks = 0; ks < ks2; ks++) {
-            RC_STAMP(t0)
-            if (ldw) {
-                if (ks + 1 < ks2) {
-                    issue2(ks + 1, (ks + 1) & 1, wdelta);
-                    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-                } else {
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-            }
-            RC_STAMP(t1)
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            RC_STAMP(t2)
-            const char* st = smem + RC_Y + (ks & 1) * RC_STAGE;
-            h8_t a[4], b[6];
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++)
-                a[mt] = *(const h8_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, (ks * 4 + fq) * 16));
-#pragma unroll
-            for (int nt = 0; nt < 6; nt++) b[nt] = *(const h8_t*)(st + w_off[nt]);
-            mfma_step(a, b);
-            RC_STAMP(t3)
-            __builtin_amdgcn_s_barrier();
-            RC_STAMP(t4)
-            RC_ACC(5, t0, t1) RC_ACC(6, t1, t2) RC_ACC(7, t2, t3) RC_ACC(8, t3, t4)
-        }
-    };
-    int64_t tile = blockIdx.x;
-    RC_STAMP(t_begin)
-    if (ldw) {
-        set_tile(tile);
-        issue1(0, 0);
-    }
-    for (; tile < ntiles; tile += gridDim.x) {
-        const bool more = tile + gridDim.x < ntiles;
-        RC_STAMP(tt0)
-        zero_acc();
-        gemm1(false);
-        RC_STAMP(tt1)
-        etile = -1;
-        // ---- intermediate -> y tile; W2's first stage into the released stage 0
-        acc_to_y((const half_t*)p1.bias, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
-        if (ldw) issue2(0, 0);
-        sync_lds();
-        RC_STAMP(tt2)
-        gemm_y(0);
-        RC_STAMP(tt3)
-        RC_ACC(11, tt1, tt2)
-        if (TRI) {
-            // the middle Linear's output -> its row epilogue (LayerNorm, ReLU) in
-            // place on the y tile -> the third GEMM's A operand
-            acc_to_y((const half_t*)pg.bias, false, false);
-            if (ldw) issue2(0, 0, w3delta);   // stage 0 of W3 loads under the row pass
-            sync_lds();
-            mid_rows(pg);
-            sync_lds();
-            gemm_y(w3delta);
-        }
-        acc_to_y((const half_t*)p.bias, F2 & RG_RELU, F2 & RG_SIGMOID);
-        if (GATED) {
-            // ---- gate: A x Wg -> sigmoid (rowgemm's SIGMOID rounding) -> y = fp16(gate * y)
-            if (ldw) issue1(0, 0, true);
-            zero_acc();
-            gemm1(true);
-#pragma unroll
-            for (int nt = 0; nt < 6; nt++) {
-                const int col = wn * 96 + nt * 16 + 4 * fq;
-                const h4_t bias = *(const h4_t*)((const half_t*)pg.bias + col);
-#pragma unroll
-                for (int mt = 0; mt < 4; mt++) {
-                    h4_t* yp = (h4_t*)(smem + ym.off(wm * 64 + mt * 16 + fr, col * 2));
-                    h4_t y = *yp;
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        const half_t g = (half_t)fast_sigmoid((float)(half_t)(acc[mt][nt][r] + (float)bias[r]));
-                        y[r] = (half_t)((float)g * (float)y[r]);
-                    }
-                    *yp = y;
-                }
-            }
-        }
-        // ---- the next tile's first GEMM1 stage loads under this epilogue
-        if (more && ldw) {
-            set_tile(tile + gridDim.x);
-            issue1(0, 0);
-        }
-        RC_STAMP(tt4)
-        sync_lds();
-        RC_STAMP(tt5)
-        RC_ACC(12, tt3, tt4) RC_ACC(13, tt4, tt5) RC_ACC(14, tt0, tt5)
-        if (OVL && more) {
-            etile = tile;   // run during the next tile's GEMM1
-            continue;
-        }
-        // the row epilogue now, on every wave: rows 16 wave .. 16 wave + 15
-        RC_STAMP(te0)
-        {
-            EpiConsts2 kc;
-            load_consts2<F2>(p, lane, kc);
-#pragma unroll 1
-            for (int q0 = 0; q0 < 16; q0 += 4) {   // one batch live at a time (register budget)
-                EpiOps2<4> st;
-                epi_issue(tile, 16 * wave + q0, st);
-                epi_done(tile, 16 * wave + q0, kc, st);
-            }
-        }
-        sync_lds();
-        RC_STAMP(te1)
-        RC_ACC(9, te0, te1)
-    }
-#ifdef DPVO_STAMPS
-    RC_STAMP(t_end)
-    st_sum[10] += t_end - t_begin;
-    if (lane == 0)
-        for (int k = 0; k < ST_SEGS; k++) dpvo_stamps[((int64_t)blockIdx.x * 8 + wave) * ST_SEGS + k] = st_sum[k];
-#endif
 }
 
 // v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16
@@ -1592,7 +1280,10 @@ extern "C" int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_
     if (ensure_num_cus()) return -1;
     const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
     const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
-    if (a->flags & DPVO_RG_WKB)
+    static const int exp_d = getenv("DPVO_EXP_D") ? atoi(getenv("DPVO_EXP_D")) : 0;
+    if ((a->flags & DPVO_RG_WKB) && exp_d)
+        hipLaunchKernelGGL((rowgemm5_kernel<0, true, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b);
+    else if (a->flags & DPVO_RG_WKB)
         hipLaunchKernelGGL((rowgemm5_kernel<0, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b);
     else
         hipLaunchKernelGGL((rowgemm3_kernel<0, true>), dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, *b);
