@@ -1563,16 +1563,21 @@ static size_t nb_sort_temp_bytes(int64_t E)
 // carried along (forward substitution for free), then one wave back-
 // substitutes and the poses are retracted.
 // ---------------------------------------------------------------------------
+typedef float bd_f4v __attribute__((ext_vector_type(4)));
+typedef int bd_i4v __attribute__((ext_vector_type(4)));
 constexpr int BD_NMAX = 12;
 constexpr int BD_N6MAX = 6 * BD_NMAX;     // 72
 constexpr int BD_WAVES = 4;
 constexpr int BD_HD_LD = 64;   // row pitch of the dense lower-triangle system the wave solver loads
-constexpr int BD_GRID = 512;    // 4 waves each (measured over 256-2048: 512 is fastest at C3 and C2, scripts/exp_bd_grid.sh)
+// 4 waves each.  Measured over 256-2048 (round 3) and again with this round's
+// reduce and solve: 768 / 1024 workgroups 54-56 us per iteration at C2
+// against 46 at 512 (the reduce reads every workgroup's partial)
+constexpr int BD_GRID = 512;
 static_assert(BD_GRID % 16 == 0, "bd_reduce_kernel: 16 waves split the partials evenly");
 static int bd_grid() { return BD_GRID; }
 
 struct BdLayout {
-    size_t hdr, gid, offs, perm, groups, gbws, gbws_bytes, Em, Cg, ug, Hpart, H, Hd, dX, total;
+    size_t hdr, gid, offs, perm, groups, gbws, gbws_bytes, erec, grec, Em, Cg, ug, Hpart, H, Hd, dX, total;
     int64_t mu_max;
     int n6, nup, ent;
 };
@@ -1594,6 +1599,8 @@ static BdLayout bd_layout(int64_t E, int64_t num_patches, int N)
     L.groups = take(8);
     L.gbws_bytes = dpvo_group_by_workspace_bytes((int64_t)e);
     L.gbws = take(L.gbws_bytes);
+    L.erec = take(e * 32);
+    L.grec = take((size_t)L.mu_max * 16);
     L.Em = take((size_t)L.mu_max * std::max(L.n6, 1) * 4);
     L.Cg = take((size_t)L.mu_max * 4);
     L.ug = take((size_t)L.mu_max * 4);
@@ -1620,6 +1627,11 @@ struct BdParams {
     const int* offs;       // kk group-by CSR
     const int* perm;
     const int64_t* groups;
+    int64_t E;
+    // per-call gathers in CSR order (bd_prep_kernel): edge q = (i, j, target)
+    // and (weight, -, -); group g = (start, count, patch k or -1, -)
+    bd_f4v* erec;
+    bd_i4v* grec;
     int* status;
     float *Em, *Cg, *ug, *Hpart, *H, *Hd, *dX;
 };
@@ -1654,10 +1666,10 @@ struct BdEdge {
     bool iv, jv, self;
 };
 
-__device__ __forceinline__ void bd_edge(const BdParams& p, int64_t e, float px, float py, float dk, float fx, float fy,
-                                        float cx, float cy, BdEdge& o)
+__device__ __forceinline__ void bd_edge(const BdParams& p, const bd_f4v r0, const bd_f4v r1, float px, float py,
+                                        float dk, float fx, float fy, float cx, float cy, BdEdge& o)
 {
-    const int64_t i_abs = p.ii[e], j_abs = p.jj[e];
+    const int64_t i_abs = __float_as_int(r0[0]), j_abs = __float_as_int(r0[1]);
     const float* Pi = p.poses + i_abs * 7;
     const float* Pj = p.poses + j_abs * 7;
     const float ti[3] = {Pi[0], Pi[1], Pi[2]}, tj[3] = {Pj[0], Pj[1], Pj[2]};
@@ -1673,12 +1685,12 @@ __device__ __forceinline__ void bd_edge(const BdParams& p, int64_t e, float px, 
     const float d = (Z >= 0.2f) ? 1.0f / Z : 0.0f;
     const float d2 = d * d;
     const float x1 = fx * (X / Z) + cx, y1 = fy * (Y / Z) + cy;
-    const float rx = p.target[e * 2 + 0] - x1, ry = p.target[e * 2 + 1] - y1;
+    const float rx = r0[2] - x1, ry = r0[3] - y1;
     const bool in_bounds = (sqrtf(rx * rx + ry * ry) < 128.f) && (Z > 0.2f) && (x1 > -64.f) && (y1 > -64.f) &&
                            (x1 < 2.f * cx + 64.f) && (y1 < 2.f * cy + 64.f);
     const float mask = in_bounds ? 1.0f : 0.0f;
-    o.w[0] = mask * p.weight[e * 2 + 0];
-    o.w[1] = mask * p.weight[e * 2 + 1];
+    o.w[0] = mask * r1[0];
+    o.w[1] = mask * r1[1];
     o.r[0] = rx;
     o.r[1] = ry;
     o.Jz[0] = fx * (tij[0] * d - tij[2] * (X * d2));
@@ -1769,6 +1781,27 @@ constexpr int BD_SLOT_IT = 8;                     // wave iterations per flush
 constexpr int BD_SLOTS = BD_SLOT_IT * BD_WAVES;   // 32 listed patches
 constexpr int BD_SLOT_LD = BD_N6MAX + 2;          // E row, Q, Q u
 
+// Once per call: the edge data the patch kernel needs, gathered into CSR
+// order (one coalesced 32-byte record per edge instead of perm -> ii / jj /
+// target / weight), and each group's (start, count, patch), so every BA
+// iteration's per-patch chain of dependent loads is group -> edges -> poses.
+__global__ __launch_bounds__(256) void bd_prep_kernel(BdParams p)
+{
+    const int64_t G = min(*p.groups, p.mu_max);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < p.E; q += stride) {
+        const int64_t e = p.perm[q];
+        p.erec[2 * q] = bd_f4v{__int_as_float((int)p.ii[e]), __int_as_float((int)p.jj[e]), p.target[2 * e],
+                               p.target[2 * e + 1]};
+        p.erec[2 * q + 1] = bd_f4v{p.weight[2 * e], p.weight[2 * e + 1], 0.f, 0.f};
+    }
+    for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < G; g += stride) {
+        const int start = p.offs[g];
+        const int64_t k = p.kk[p.perm[start]];
+        p.grec[g] = bd_i4v{start, p.offs[g + 1] - start, (k < 0 || k >= p.num_patches) ? -1 : (int)k, 0};
+    }
+}
+
 template <bool APPLY, bool HESS>
 __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
 {
@@ -1806,9 +1839,10 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         float* slot = slots + (sit * BD_WAVES + wave) * BD_SLOT_LD;
         if (pose_terms && lane == 0) slot[BD_N6MAX] = slot[BD_N6MAX + 1] = 0.f;   // empty until filled
         if (g < G) do {
-        const int start = p.offs[g], cnt = p.offs[g + 1] - start;
-        const int64_t k = p.kk[p.perm[start]];
-        if (k < 0 || k >= p.num_patches) {
+        const bd_i4v gr = p.grec[g];
+        const int start = gr[0], cnt = gr[1];
+        const int64_t k = gr[2];
+        if (k < 0) {
             if (lane == 0) atomicExch(p.status, -1);  // patch index out of range
             continue;
         }
@@ -1841,9 +1875,9 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         wave_lds_fence();
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const bool on = lane < cnt - c0;
-            const int64_t e = on ? p.perm[start + c0 + lane] : p.perm[start];
+            const int q = on ? start + c0 + lane : start;
             BdEdge o;
-            bd_edge(p, e, px, py, dk, fx, fy, cx, cy, o);
+            bd_edge(p, p.erec[2 * q], p.erec[2 * q + 1], px, py, dk, fx, fy, cx, cy, o);
             if (!on) { o.w[0] = o.w[1] = 0.f; o.iv = o.jv = o.self = false; }
             float cl = 0.f, ul = 0.f;
 #pragma unroll
@@ -2221,35 +2255,54 @@ __global__ __launch_bounds__(64) void bd_solve_wave_kernel(BdParams p)
         a[4 * v + 0] = x[0]; a[4 * v + 1] = x[1]; a[4 * v + 2] = x[2]; a[4 * v + 3] = x[3];
     }
     if (status != 0) return;
-    int fail = 0;
+    // broadcast reads of col[k][c] address LDS as (zero VGPR) + constant offset
+    // (otherwise every read materialises its constant address in a VGPR)
+    int zoff;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zoff));
+    const float(*colz)[64] = reinterpret_cast<const float(*)[64]>(reinterpret_cast<const char*>(col) + zoff);
+    // lane k keeps pivot k (one writelane per column); the first failing
+    // leading minor is read off a ballot after the factor
+    float piv = 1.f;
     // one column step per k, k a compile-time constant (bd_unroll): every a[]
     // index is static, so the system stays in registers at any NN
     bd_unroll<0, n>::run([&](auto kc) {
         constexpr int k = decltype(kc)::value;
         const float d = rdl(a[k], k);
-        fail = (fail == 0 && !(d > 0.f)) ? k + 1 : fail;
+        asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(piv) : "s"(d), "n"(k));
         // lane k: d / sqrt(d) = L[k][k]; lanes below it: L[r][k]; lane n: z_k
         a[k] *= __builtin_amdgcn_rsqf(d);
         if constexpr (k + 1 < n) {
             col[k][lane] = a[k];
             a[k + 1] -= a[k] * rdl(a[k], k + 1);   // the next pivot's column: no LDS latency
-            // columns k + 2 .. n - 1 from the LDS broadcast of column k: aligned
-            // pairs by packed FMAs, an odd leading column alone
+            // columns k + 2 .. n - 1 from the LDS broadcast of column k: the
+            // leading ones alone up to a multiple of 4, then 16-byte broadcast
+            // reads (constant offsets on a zero address) and packed FMAs
 #pragma unroll
-            for (int c = 0; c < n; c += 2) {
-                if (c >= k + 2) {
-                    const bd_f2 lc = *(const bd_f2*)&col[k][c];
+            for (int c = k + 2; c < ((k + 5) & ~3) && c < n; c++) a[c] -= a[k] * colz[k][c];
+#pragma unroll
+            for (int c = (k + 5) & ~3; c < n; c += 4) {
+                if (c + 4 <= n) {
+                    const bd_f4 lc = *(const bd_f4*)&colz[k][c];
+                    const bd_f2 r0 = __builtin_elementwise_fma(-bd_f2{a[k], a[k]}, bd_f2{lc[0], lc[1]},
+                                                               bd_f2{a[c], a[c + 1]});
+                    const bd_f2 r1 = __builtin_elementwise_fma(-bd_f2{a[k], a[k]}, bd_f2{lc[2], lc[3]},
+                                                               bd_f2{a[c + 2], a[c + 3]});
+                    a[c] = r0[0];
+                    a[c + 1] = r0[1];
+                    a[c + 2] = r1[0];
+                    a[c + 3] = r1[1];
+                } else {
+                    const bd_f2 lc = *(const bd_f2*)&colz[k][c];
                     const bd_f2 r = __builtin_elementwise_fma(-bd_f2{a[k], a[k]}, lc, bd_f2{a[c], a[c + 1]});
                     a[c] = r[0];
                     a[c + 1] = r[1];
-                } else if (c + 1 >= k + 2) {
-                    a[c + 1] -= a[k] * col[k][c + 1];
                 }
             }
         }
     });
-    if (fail) {
-        if (lane == 0) atomicExch(p.status, fail);
+    const uint64_t bad = __ballot(lane < n && !(piv > 0.f));
+    if (bad) {
+        if (lane == 0) atomicExch(p.status, __ffsll((unsigned long long)bad));
         return;
     }
     // transpose through LDS: lane r reads column r -- L[i][r] for i > r, z_r
@@ -2326,6 +2379,10 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
         p.perm = (const int*)(ws + L.perm);
         p.groups = (const int64_t*)(ws + L.groups);
     }
+    p.E = E;
+    p.erec = (bd_f4v*)(ws + L.erec);
+    p.grec = (bd_i4v*)(ws + L.grec);
+    hipLaunchKernelGGL(bd_prep_kernel, dim3(grid_for(E, 256, 2048)), dim3(256), 0, s, p);
     p.Em = (float*)(ws + L.Em);
     p.Cg = (float*)(ws + L.Cg);
     p.ug = (float*)(ws + L.ug);

@@ -566,7 +566,7 @@ struct R5Cursor {
     }
 };
 
-template <int FLAGS, bool DUAL, bool DIRECT = false>
+template <int FLAGS, bool DUAL>
 __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_args p, dpvo_rowgemm_args p2)
 {
     static_assert((FLAGS & ~(RG_RELU | RG_SIGMOID)) == 0, "v5: plain GEMMs only");
@@ -633,29 +633,6 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     auto epilogue = [&](int64_t t, auto qc) __attribute__((always_inline)) {
         constexpr int q = decltype(qc)::value;
         const dpvo_rowgemm_args& pe = q ? p2 : p;
-        if (DIRECT) {
-            // straight from the accumulators: lane (fr, fq) owns row 16 mt + fr,
-            // columns 48 w + 16 nt + 4 fq .. + 3 (8 B); no LDS, no barrier
-            half_t* out = (half_t*)pe.out16;
-#pragma unroll
-            for (int mt = 0; mt < 8; mt++) {
-                const int64_t row = t * RG_BM + 16 * mt + fr;
-#pragma unroll
-                for (int nt = 0; nt < 3; nt++) {
-                    h4_t y;
-#pragma unroll
-                    for (int r = 0; r < 4; r++) {
-                        half_t v = (half_t)(acc[mt][nt][r] + (float)bias[q][nt][r]);
-                        if (FLAGS & RG_RELU) v = v > (half_t)0 ? v : (half_t)0;
-                        if (FLAGS & RG_SIGMOID) v = (half_t)fast_sigmoid((float)v);
-                        y[r] = v;
-                    }
-                    acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
-                    if (row < Mrows) *(h4_t*)(out + row * pe.ldo16 + 48 * w + 16 * nt + 4 * fq) = y;
-                }
-            }
-            return;
-        }
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
             const int col = 48 * w + 16 * nt + 4 * fq;
@@ -1280,10 +1257,7 @@ extern "C" int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_
     if (ensure_num_cus()) return -1;
     const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
     const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
-    static const int exp_d = getenv("DPVO_EXP_D") ? atoi(getenv("DPVO_EXP_D")) : 0;
-    if ((a->flags & DPVO_RG_WKB) && exp_d)
-        hipLaunchKernelGGL((rowgemm5_kernel<0, true, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b);
-    else if (a->flags & DPVO_RG_WKB)
+    if (a->flags & DPVO_RG_WKB)
         hipLaunchKernelGGL((rowgemm5_kernel<0, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b);
     else
         hipLaunchKernelGGL((rowgemm3_kernel<0, true>), dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, *b);
