@@ -1567,7 +1567,7 @@ typedef float bd_f4v __attribute__((ext_vector_type(4)));
 typedef int bd_i4v __attribute__((ext_vector_type(4)));
 constexpr int BD_NMAX = 12;
 constexpr int BD_N6MAX = 6 * BD_NMAX;     // 72
-constexpr int BD_WAVES = 4;
+constexpr int BD_WAVES = 4;   // (6, all of C2's ~2,100 kk groups in one pass: 45.8 -> 54.8 us per iteration)
 constexpr int BD_HD_LD = 64;   // row pitch of the dense lower-triangle system the wave solver loads
 // 4 waves each.  Measured over 256-2048 (round 3) and again with this round's
 // reduce and solve: 768 / 1024 workgroups 54-56 us per iteration at C2
@@ -1778,8 +1778,9 @@ __device__ __forceinline__ void bd_jterms_add(const BdEdge& o, float* part, floa
 // entries of the partial and sums the listed patches' products into them in
 // slot order -- a rank-BD_SLOTS update with plain LDS reads, no atomics.
 constexpr int BD_SLOT_IT = 8;                     // wave iterations per flush
-constexpr int BD_SLOTS = BD_SLOT_IT * BD_WAVES;   // 32 listed patches
+constexpr int BD_SLOTS = BD_SLOT_IT * BD_WAVES;   // listed patches per flush
 constexpr int BD_SLOT_LD = BD_N6MAX + 2;          // E row, Q, Q u
+static_assert(BD_SLOTS * BD_SLOT_LD % 4 == 0, "slot list zeroed in 16-byte stores");
 
 // Once per call: the edge data the patch kernel needs, gathered into CSR
 // order (one coalesced 32-byte record per edge instead of perm -> ii / jj /
@@ -1802,6 +1803,21 @@ __global__ __launch_bounds__(256) void bd_prep_kernel(BdParams p)
     }
 }
 
+#ifdef DPVO_STAMPS
+// Diagnostic build only (never the product library): per-wave cycle sums of
+// the patch kernel's phases, s_memtime stamps.  dpvo_bd_stamps[block][wave][seg].
+__device__ unsigned long long dpvo_bd_stamps[BD_GRID * BD_WAVES * 16];
+#define BD_STAMP(v)                                                                            \
+    unsigned long long v;                                                                      \
+    __builtin_amdgcn_sched_barrier(0);                                                         \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");                  \
+    __builtin_amdgcn_sched_barrier(0);
+#define BD_ACC(seg, a, b) bst[seg] += (b) - (a);
+#else
+#define BD_STAMP(v)
+#define BD_ACC(seg, a, b)
+#endif
+
 template <bool APPLY, bool HESS>
 __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
 {
@@ -1809,19 +1825,36 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
     if (*(volatile int*)p.status != 0) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int n6 = p.n6, nup = p.nup, ent = p.ent, N = p.N;
+    const int entp = (ent + 3) & ~3;   // per-wave partial pitch (16-byte aligned)
+#ifdef DPVO_STAMPS
+    unsigned long long bst[16] = {};
+#endif
+    BD_STAMP(t_begin)
     const bool pose_terms = HESS && N > 0;
-    float* part = sm + wave * ent;
-    float* ev = sm + BD_WAVES * ent + wave * BD_N6MAX;
+    float* part = sm + wave * entp;
+    float* ev = sm + BD_WAVES * entp + wave * BD_N6MAX;
     // (row, column) of every upper-triangle entry k = tri_up(r, c): r | c << 8
-    uint16_t* tri_rc = reinterpret_cast<uint16_t*>(sm + BD_WAVES * ent + BD_WAVES * BD_N6MAX);
-    float* slots = sm + BD_WAVES * ent + BD_WAVES * BD_N6MAX + (pose_terms ? (nup + 1) / 2 : 0);
+    uint16_t* tri_rc = reinterpret_cast<uint16_t*>(sm + BD_WAVES * entp + BD_WAVES * BD_N6MAX);
+    float* slots = sm + BD_WAVES * entp + BD_WAVES * BD_N6MAX + (pose_terms ? (nup + 7) / 8 * 4 : 0);   // 16-B aligned
     if (pose_terms) {
-        for (int i = threadIdx.x; i < BD_WAVES * ent; i += blockDim.x) sm[i] = 0.f;
-        for (int r = threadIdx.x; r < n6; r += blockDim.x)
-            for (int c = r; c < n6; c++) tri_rc[tri_up(r, c, n6)] = (uint16_t)(r | c << 8);
-        for (int i = threadIdx.x; i < BD_SLOTS * BD_SLOT_LD; i += blockDim.x) slots[i] = 0.f;
+        // (16-byte stores: BD_WAVES * entp and BD_SLOTS * BD_SLOT_LD are multiples of 4)
+        for (int i = threadIdx.x; i < BD_WAVES * entp / 4; i += blockDim.x) ((bd_f4v*)sm)[i] = bd_f4v{0.f, 0.f, 0.f, 0.f};
+        for (int i = threadIdx.x; i < BD_SLOTS * BD_SLOT_LD / 4; i += blockDim.x)
+            ((bd_f4v*)slots)[i] = bd_f4v{0.f, 0.f, 0.f, 0.f};
+        // (row, column) of packed entry k, one entry per thread and pass: the row
+        // from the closed form of tri_up, corrected by one step either way
+        const float nn = (float)(2 * n6 + 1);
+        for (int k = threadIdx.x; k < nup; k += blockDim.x) {
+            int r = (int)((nn - sqrtf(nn * nn - 8.f * (float)k)) * 0.5f);
+            r = min(max(r, 0), n6 - 1);
+            if (r + 1 < n6 && tri_up(r + 1, r + 1, n6) <= k) r++;
+            if (tri_up(r, r, n6) > k) r--;
+            tri_rc[k] = (uint16_t)(r | (r + k - tri_up(r, r, n6)) << 8);
+        }
     }
     __syncthreads();
+    BD_STAMP(t_init)
+    BD_ACC(0, t_begin, t_init)
     const int64_t G = min(*p.groups, p.mu_max);
     const float lm = p.lmbda[0];
     const float fx = p.intrinsics[0], fy = p.intrinsics[1], cx = p.intrinsics[2], cy = p.intrinsics[3];
@@ -1838,6 +1871,7 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         const int sit = (int)(it % BD_SLOT_IT);
         float* slot = slots + (sit * BD_WAVES + wave) * BD_SLOT_LD;
         if (pose_terms && lane == 0) slot[BD_N6MAX] = slot[BD_N6MAX + 1] = 0.f;   // empty until filled
+        BD_STAMP(ti0)
         if (g < G) do {
         const bd_i4v gr = p.grec[g];
         const int start = gr[0], cnt = gr[1];
@@ -1873,11 +1907,18 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         }
         float Ck = 0.f, uk = 0.f;
         wave_lds_fence();
+        BD_STAMP(ti1)
+        BD_ACC(1, ti0, ti1)
         for (int c0 = 0; c0 < cnt; c0 += 64) {
             const bool on = lane < cnt - c0;
             const int q = on ? start + c0 + lane : start;
             BdEdge o;
             bd_edge(p, p.erec[2 * q], p.erec[2 * q + 1], px, py, dk, fx, fy, cx, cy, o);
+#ifdef DPVO_STAMPS
+            asm volatile("" ::"v"(o.Ji[0][0]), "v"(o.Jj[1][5]), "v"(o.w[0]), "v"(o.r[1]));
+#endif
+            BD_STAMP(tc0)
+            BD_ACC(2, ti1, tc0)
             if (!on) { o.w[0] = o.w[1] = 0.f; o.iv = o.jv = o.self = false; }
             float cl = 0.f, ul = 0.f;
 #pragma unroll
@@ -1898,6 +1939,8 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
             for (int q = 0; q < N && !mixed; q++)
                 mixed = __popcll(__ballot(jt && o.jx == q)) > 1;
             const int passes = mixed ? 64 : 1;
+            BD_STAMP(tc1)
+            BD_ACC(3, tc0, tc1)
             for (int ps = 0; ps < passes; ps++) {
                 const bool act = !mixed || lane == ps;
                 const uint64_t ivm = __ballot(act && o.iv);
@@ -1936,10 +1979,15 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
                     }
                     if (addr >= 0) atomicAdd(&base[addr], val);
                 }
+                BD_STAMP(tc2)
                 if (act) bd_jterms_add(o, part, ev, n6, nup);
                 wave_lds_fence();
+                BD_STAMP(tc3)
+                BD_ACC(4, tc1, tc2)
+                BD_ACC(5, tc2, tc3)
             }
         }
+        BD_STAMP(ti2)
         if (!pose_terms) {
             if (lane == 0) { p.Cg[g] = Ck; p.ug[g] = uk; }
             continue;
@@ -1960,7 +2008,10 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
             slot[BD_N6MAX + 1] = Q * uk;
         }
         wave_lds_fence();
+        BD_STAMP(ti3)
+        BD_ACC(6, ti2, ti3)
         } while (false);
+        BD_STAMP(tf0)
         if (pose_terms && (sit == BD_SLOT_IT - 1 || it == niter - 1)) {
             // flush: H_k -= sum_s (Q_s e_s[r]) e_s[c], g_r -= sum_s (Q u)_s e_s[r],
             // slots in order, into wave 0's partial (one thread per entry)
@@ -1987,17 +2038,28 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
             }
             __syncthreads();
         }
+        BD_STAMP(tf1)
+        BD_ACC(7, tf0, tf1)
+        BD_ACC(8, ti0, tf0)
     }
     if (!pose_terms) return;
     // the workgroup's partial: its waves' partials summed in wave order
     __syncthreads();
+    BD_STAMP(tw0)
     float* dst = p.Hpart + (int64_t)blockIdx.x * ent;
     for (int i = threadIdx.x; i < ent; i += blockDim.x) {
         float s = sm[i];
 #pragma unroll
-        for (int w = 1; w < BD_WAVES; w++) s += sm[w * ent + i];
+        for (int w = 1; w < BD_WAVES; w++) s += sm[w * entp + i];
         dst[i] = s;
     }
+#ifdef DPVO_STAMPS
+    BD_STAMP(t_end)
+    BD_ACC(9, tw0, t_end)
+    BD_ACC(10, t_begin, t_end)
+    if (lane == 0 && APPLY)
+        for (int k = 0; k < 16; k++) dpvo_bd_stamps[((int64_t)blockIdx.x * BD_WAVES + wave) * 16 + k] = bst[k];
+#endif
 }
 
 // H = sum of the patch kernel's workgroup partials, fixed order.  Also stored
@@ -2390,8 +2452,8 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
     p.H = (float*)(ws + L.H);
     p.Hd = (float*)(ws + L.Hd);
     p.dX = (float*)(ws + L.dX);
-    const size_t lds = (size_t)(BD_WAVES * (p.N > 0 ? L.ent : 0) + BD_WAVES * BD_N6MAX) * 4 +
-                       (size_t)(p.N > 0 ? (L.nup + 1) / 2 : 0) * 4 +
+    const size_t lds = (size_t)(BD_WAVES * (p.N > 0 ? (L.ent + 3) / 4 * 4 : 0) + BD_WAVES * BD_N6MAX) * 4 +
+                       (size_t)(p.N > 0 ? (L.nup + 7) / 8 * 4 : 0) * 4 +
                        (size_t)(p.N > 0 ? BD_SLOTS * BD_SLOT_LD : 0) * 4;
     const unsigned gR = (unsigned)((L.ent + 63) / 64);
     for (int it = 0; it < iterations; it++) {
@@ -2429,6 +2491,14 @@ extern "C" size_t dpvo_ba_workspace_bytes(int64_t num_edges, int64_t num_patches
 {
     return dpvo_ba_workspace_bytes_ex(num_edges, num_patches, num_opt_poses, 0);
 }
+
+#ifdef DPVO_STAMPS
+extern "C" int dpvo_diag_bd_stamps(void* host, size_t bytes)
+{
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(dpvo_bd_stamps), std::min(bytes, sizeof(dpvo_bd_stamps)), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int dpvo_ba_forward_csr(float* poses, float* patches, int64_t num_patches, int P, const float* intrinsics,
                                    const float* target, const float* weight, const float* lmbda, const int64_t* ii,
