@@ -371,7 +371,7 @@ def roofline_lines(slam, corr_ms, order_ms, breakdown, counters, path):
     G = E // 22 + E // slam.M   # SoftAgg groups: ~E / 21.6 patches (497 M edges, 23 M patches) + ~E / M frame pairs
     flops = 2.0 * (UPD_MACS_PER_EDGE * E + UPD_MACS_PER_GROUP * G)
     upd_bytes = UPD_BYTES_PER_EDGE * E
-    upd = {"kernel": "update operator (rowchain / rowgemm3 / rowadd_ln / sa_reduce_csr launches)",
+    upd = {"kernel": "update operator (rowchain5 / rowgemm5 / rowadd_ln / sa_reduce_csr launches)",
            "bound": "latency (k-loop + row epilogue; see DESIGN.md)", "unit": "GB/s", "peak": HBM_PEAK_GBS,
            "phase_ms": upd_ms, "algorithmic_bytes": upd_bytes, "flops": flops,
            "tflops": round(flops / (upd_ms * 1e-3) / 1e12, 1), "mfma_peak_tflops": MFMA_PEAK_TFLOPS,

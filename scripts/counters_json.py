@@ -33,7 +33,7 @@ REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 
 CORR = re.compile(r"corr_mfma_kernel|edge_hist_kernel|edge_scatter_kernel")
-UPD = re.compile(r"rowgemm\d?_kernel|rowchain_kernel|rowadd_ln_kernel|sa_reduce_csr|nb_csr_kernel")
+UPD = re.compile(r"rowgemm\d?_kernel|rowchain\d?_kernel|rowadd_ln_kernel|sa_reduce_csr|nb_csr_kernel")
 
 
 def short(name):
