@@ -36,6 +36,10 @@ def main():
     out = {}
     out["c1_res"] = timeit(lambda: U.rowchain(n16, W1, b1, W2, b2, flags1=U.RELU, a_idx=idx, flags=U.RES, res32=n32,
                                               want32=True))
+    out["c1_no16"] = timeit(lambda: U.rowchain(n16, W1, b1, W2, b2, flags1=U.RELU, a_idx=idx, flags=U.RES, res32=n32,
+                                               want32=True, want16=False))
+    out["c1_plain"] = timeit(lambda: U.rowchain(n16, W1, b1, W2, b2, flags1=U.RELU, a_idx=idx, flags=U.LN | U.LN_RELU,
+                                                ln=ln))
     out["gru_ln"] = timeit(lambda: U.rowchain(n16, W1, b1, W2, b2, flags1=U.RELU, flags=U.GATE | U.LN, res32=n32,
                                               gate=(Wg, bg), ln=ln, want32=True))
     Wa, Wb = U.kblock(W1), U.kblock(W2)
