@@ -160,6 +160,11 @@ def test_kblocked_w_is_bit_identical(M, flags):
     assert torch.equal(out[:h], want[:h]) and bool((out[h:] == 7.0).all())
     A = torch.randn(M, D, device="cuda").half()
     (Wa, ba), (Wb, bb) = U.pack_linear(*lin(D, 8)), U.pack_linear(*lin(D, 9))
+    # K = 384 with a device row count: the small-M kernel (the SoftAgg h Linear)
+    want = U.rowgemm(A, Wa, ba, flags=flags)[1]
+    out = torch.full_like(want, 7.0)
+    U.rowgemm(A, U.kblock(Wa), ba, flags=flags, out16=out, M_dev=Md)
+    assert torch.equal(out[:h], want[:h]) and bool((out[h:] == 7.0).all())
     f, g = U.rowgemm_pair(A, U.kblock(Wa), ba, U.kblock(Wb), bb)
     assert torch.equal(f, U.rowgemm(A, Wa, ba)[1]) and torch.equal(g, U.rowgemm(A, Wb, bb)[1])
     with pytest.raises(RuntimeError):
