@@ -1567,7 +1567,11 @@ typedef float bd_f4v __attribute__((ext_vector_type(4)));
 typedef int bd_i4v __attribute__((ext_vector_type(4)));
 constexpr int BD_NMAX = 12;
 constexpr int BD_N6MAX = 6 * BD_NMAX;     // 72
-constexpr int BD_WAVES = 4;   // (6, all of C2's ~2,100 kk groups in one pass: 45.8 -> 54.8 us per iteration)
+// 4 waves per workgroup at ~235 VGPRs (2 per SIMD: the 512 workgroups are all
+// resident).  6 waves -- all of C2's ~2,100 kk groups in one pass -- measured
+// 45.8 -> 54.8 us per iteration as is, 69 with the VGPRs capped for 3 per SIMD
+// (spills).
+constexpr int BD_WAVES = 4;
 constexpr int BD_HD_LD = 64;   // row pitch of the dense lower-triangle system the wave solver loads
 // 4 waves each.  Measured over 256-2048 (round 3) and again with this round's
 // reduce and solve: 768 / 1024 workgroups 54-56 us per iteration at C2
@@ -1650,6 +1654,58 @@ __device__ __forceinline__ float wave64_allsum(float s)
     s = __int_as_float(h[0]) + __int_as_float(h[1]);
     auto w = __builtin_amdgcn_permlane32_swap(__float_as_int(s), __float_as_int(s), false, false);
     return __int_as_float(w[0]) + __int_as_float(w[1]);
+}
+
+// 33 per-lane values summed over the wave, total of value L left in lane L
+// (lanes 33..63: don't care) -- a reduce-scatter butterfly: each exchange
+// step halves the values a lane carries (33 + 16 + 8 + 4 + 2 + 1 exchanges
+// instead of 33 all-lane reductions of 6 each).  A fixed tree: every run
+// gives the same bits.
+__device__ __forceinline__ float wave64_sum33(const float (&v)[33], int lane)
+{
+    float y[32];
+    {
+        // slot 0 pairs with slot 32 (lanes >= 32 keep slot 32), the others with
+        // themselves: y[j] = total over lanes L, L ^ 32 of slot j (+ 32 b5)
+        // (v_permlane32_swap exchanges the first operand's upper 32 lanes with
+        // the second's lower 32: the two results summed are the pair's total)
+        auto h0 = __builtin_amdgcn_permlane32_swap(__float_as_int(v[0]), __float_as_int(v[32]), false, false);
+        y[0] = __int_as_float(h0[0]) + __int_as_float(h0[1]);
+#pragma unroll
+        for (int j = 1; j < 32; j++) {
+            auto h = __builtin_amdgcn_permlane32_swap(__float_as_int(v[j]), __float_as_int(v[j]), false, false);
+            y[j] = __int_as_float(h[0]) + __int_as_float(h[1]);
+        }
+    }
+    float z[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) {   // bit 4: keep slot j (0) or j + 16 (1); permlane16_swap
+        // exchanges the first operand's odd 16-lane rows with the second's even rows
+        auto h = __builtin_amdgcn_permlane16_swap(__float_as_int(y[j]), __float_as_int(y[j + 16]), false, false);
+        z[j] = __int_as_float(h[0]) + __int_as_float(h[1]);
+    }
+    const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2, b0 = lane & 1;
+    float q[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {   // bit 3, partner lane ^ 8 (row rotate by 8)
+        const float send = b3 ? z[j] : z[j + 8], keep = b3 ? z[j + 8] : z[j];
+        q[j] = keep + dpp_rot<0x128>(send);
+    }
+    float r[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {   // bit 2, partner lane ^ 4 (swizzle xor 4)
+        const float send = b2 ? q[j] : q[j + 4], keep = b2 ? q[j + 4] : q[j];
+        r[j] = keep + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(send), 0x101F));
+    }
+    float t2[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {   // bit 1, quad_perm [2, 3, 0, 1]
+        const float send = b1 ? r[j] : r[j + 2], keep = b1 ? r[j + 2] : r[j];
+        t2[j] = keep + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), 0x4E, 0xF, 0xF, false));
+    }
+    // bit 0, quad_perm [1, 0, 3, 2]
+    const float send = b0 ? t2[0] : t2[1], keep = b0 ? t2[1] : t2[0];
+    return keep + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), 0xB1, 0xF, 0xF, false));
 }
 
 __device__ __forceinline__ unsigned wave_or(unsigned v)
@@ -1949,22 +2005,16 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
                     const int i6 = 6 * __shfl(o.ix, __ffsll((unsigned long long)ivm) - 1);
                     float bii[21], vi[6], Ei[6];
                     bd_iterms(o, bii, vi, Ei);
-                    float val = 0.f;
-                    int u = 0;
+                    // lane u < 21: the (i, i) entry u; 21 + t: v_i[t]; 27 + t: E_i[t]
+                    float x33[33];
 #pragma unroll
-                    for (int a = 0; a < 6; a++)
-#pragma unroll
-                        for (int b = a; b < 6; b++, u++) {
-                            const float sum = wave64_allsum(act ? bii[u] : 0.f);
-                            if (lane == u) val = sum;
-                        }
+                    for (int u = 0; u < 21; u++) x33[u] = act ? bii[u] : 0.f;
 #pragma unroll
                     for (int t = 0; t < 6; t++) {
-                        const float sv = wave64_allsum(act ? vi[t] : 0.f);
-                        const float se = wave64_allsum(act ? Ei[t] : 0.f);
-                        if (lane == 21 + t) val = sv;
-                        if (lane == 27 + t) val = se;
+                        x33[21 + t] = act ? vi[t] : 0.f;
+                        x33[27 + t] = act ? Ei[t] : 0.f;
                     }
+                    const float val = wave64_sum33(x33, lane);
                     int addr = -1;
                     float* base = part;
                     if (lane < 21) {
