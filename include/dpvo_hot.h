@@ -414,7 +414,7 @@ int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_args* b, vo
 
 /* Two chained rowgemms, Y = epi2(act1(A W1^T + b1) W2^T + b2), with the 384-wide
  * intermediate kept on chip (the update operator's Linear -> ReLU -> Linear
- * pairs).  g1: A, lda, a_idx, a_rows, W (K1 % 32 == 0), bias, zero_row, M,
+ * pairs).  g1: A, lda, a_idx, a_rows, W (K1 % 64 == 0), bias, zero_row, M,
  * M_dev and flags (DPVO_RG_RELU / DPVO_RG_SIGMOID only); its outputs are not
  * written.  g2: W ([384][384]), bias, flags and every epilogue input / output
  * of dpvo_rowgemm (its A, M and M_dev are taken from g1).
