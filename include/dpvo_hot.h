@@ -408,8 +408,9 @@ int dpvo_rowgemm(const dpvo_rowgemm_args* args, void* stream);
 /* Two plain rowgemms (flags 0) on the same A in one launch: SoftAgg's f and g
  * Linears (blocks.py:33-37 -- agg.f(x), agg.g(x)).  a and b must agree on A,
  * lda, a_idx, a_rows, K, M and M_dev; each has its own W, bias and outputs.
- * Every 128-row tile of A is multiplied by a's W then b's W back to back, so
- * the second pass reads A from L2 rather than HBM. */
+ * Every 128-row tile of A is multiplied by a's W then b's W back to back (the
+ * second pass re-reads the tile; at C3 the counters see it come back through
+ * the memory side, not from L2). */
 int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_args* b, void* stream);
 
 /* Two chained rowgemms, Y = epi2(act1(A W1^T + b1) W2^T + b2), with the 384-wide
