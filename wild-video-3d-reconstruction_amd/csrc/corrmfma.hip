@@ -157,8 +157,6 @@ struct CmLevel {
 // fragments are loaded four tiles ahead (a static register ring).  Products
 // land in a per-wave LDS box [level][patch pixel][RS] (fp32), from which the
 // bilinear epilogue reads each pixel's window and writes 256-byte coalesced rows.
-// STORE = false: timing experiment only (DPVO_CM_DBG=nostore): the epilogue
-// runs but writes nothing, which bounds what consuming corr on chip could save.
 // Tile loads read full 128-B lines: instruction ks gives lane (q16, kc) 16 B
 // of the EVEN (ks = 0, 2) or ODD (ks = 1, 3) pixel of its lane pair, chunk
 // 8 (ks >> 1) + 4 (q16 & 1) + kc of the pixel's 16 chunks -- eight pixels x 128 B
@@ -167,7 +165,6 @@ struct CmLevel {
 // with the loads alone changed).  Two DPP quad permutations and a select per
 // dword then rebuild the MFMA operand (lane (q16, kc): pixel q16, chunk
 // 4 j + kc): an exchange between the lanes of each pair (cm_pair_operands).
-template <bool STORE = true>
 __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParams p)
 {
     using namespace cm;
@@ -395,7 +392,7 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
                     v[lev] = wts[wave][lev][0][q] * r0[0] + wts[wave][lev][1][q] * r0[1] +
                              wts[wave][lev][2][q] * r0[st] + wts[wave][lev][3][q] * r0[st + 1];
                 }
-                if (STORE || v[0] == 1234.5f) *(half2_t*)(orow + 2 * t) = half2_t{(half_t)v[0], (half_t)v[1]};
+                *(half2_t*)(orow + 2 * t) = half2_t{(half_t)v[0], (half_t)v[1]};
             }
         }
     }
@@ -568,7 +565,7 @@ extern "C" int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, co
     int64_t g = std::min<int64_t>((E + cm::WAVES - 1) / cm::WAVES, 256 * 3);   // LDS and VGPRs: 3 per CU
     if (g > 8) g &= ~int64_t(7);
     const unsigned grid = (unsigned)g;
-    hipLaunchKernelGGL(corr_mfma_kernel<true>, dim3(grid), dim3(64 * cm::WAVES), 0, as_stream(stream), p);
+    hipLaunchKernelGGL(corr_mfma_kernel, dim3(grid), dim3(64 * cm::WAVES), 0, as_stream(stream), p);
     DPVO_CHECK_LAUNCH();
     return 0;
 }
