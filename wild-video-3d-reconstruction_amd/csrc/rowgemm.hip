@@ -696,11 +696,12 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     unsigned long long st_sum[ST_SEGS] = {};
     RC_STAMP(t_begin)
 #endif
-    // one k-step, PH = f mod 4: stage f is read from slot f % 4 and stage
-    // f + 2 written into slot (f + 2) % 4.  One barrier per TWO k-steps (even
-    // f): it makes stages f, f + 1 visible (written at f - 2, f - 1) and frees
-    // slots (f + 2) % 4, (f + 3) % 4 (stages f - 2, f - 1, read at f - 2,
-    // f - 1), so the waves of a SIMD may drift a k-step apart between them.
+    // one k-step, PH = f mod 4: stage f is read from slot f % 4 and, after
+    // the MFMAs, stage f + 2 written into slot (f + 2) % 4.  One barrier per
+    // TWO k-steps (even f): it makes stages f, f + 1 visible (written at the
+    // ends of f - 2, f - 1) and frees slots (f + 2) % 4, (f + 3) % 4 (stages
+    // f - 2, f - 1, read at f - 2, f - 1), so the waves of a SIMD may drift a
+    // k-step apart between them.
     auto step = [&](auto ph) __attribute__((always_inline)) {
         constexpr int PH = decltype(ph)::value;
         constexpr int PR = PH & 1;
@@ -711,23 +712,27 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
         }
         RC_STAMP(s1)
 #ifdef DPVO_STAMPS
-        asm volatile("" ::"v"(areg[PR]), "v"(wreg[PR][0]), "v"(wreg[PR][1]), "v"(wreg[PR][2]));
+        asm volatile("" ::"v"(wreg[PR][0]), "v"(wreg[PR][1]), "v"(wreg[PR][2]));
 #endif
         RC_STAMP(s2)
         const char* sa = smem + R5_Y + PH * R5_ASLOT;
         h8_t a[8];
 #pragma unroll
         for (int mt = 0; mt < 8; mt++) a[mt] = *(const h8_t*)(sa + ar_off + 1024 * mt);
-        *(h8_t*)(smem + R5_Y + ((PH + 2) & 3) * R5_ASLOT + aw_off) = areg[PR];   // stage f + 2
-        areg[PR] = load_a(ca);                                                 // stage f + 4
-        ca.next(total, nks, NP, G);
 #pragma unroll
         for (int nt = 0; nt < 3; nt++)
 #pragma unroll
             for (int mt = 0; mt < 8; mt++)
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wreg[PR][nt], a[mt], acc[mt][nt], 0, 0, 0);
+        // W(f + 2) is issued BEFORE A(f + 4): the MFMAs' wait on W(f) at step f
+        // then never covers an HBM A load; only the ring write (after this
+        // step's MFMAs) waits on its A stage
         load_w(cw, wreg[PR]);                                                  // W stage f + 2
         cw.next(total, nks, NP, G);
+        __builtin_amdgcn_sched_barrier(0);
+        *(h8_t*)(smem + R5_Y + ((PH + 2) & 3) * R5_ASLOT + aw_off) = areg[PR];   // stage f + 2
+        areg[PR] = load_a(ca);                                                 // stage f + 4
+        ca.next(total, nks, NP, G);
         RC_STAMP(s3)
         RC_ACC(0, s0, s1) RC_ACC(1, s1, s2) RC_ACC(2, s2, s3)
         if (cur.k == nks - 1) {
@@ -896,8 +901,8 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
     // one A-step (GEMM1 or the gate pass): stage g in slot g & 1, g + 1 in
     // areg[(g + 1) & 1], g + 2 in areg[g & 1]; PH = g & 1 = the W-step's parity
     // one A-step g (GEMM1 or the gate pass), PH = g & 1: stage g from slot
-    // g % 4, stage g + 2 (register set PH) into slot (g + 2) % 4, stage g + 4
-    // loaded into set PH.  One barrier per two A-steps (even g): it makes
+    // g % 4; after the MFMAs stage g + 2 (register set PH) into slot
+    // (g + 2) % 4 and stage g + 4 loaded into set PH.  One barrier per two A-steps (even g): it makes
     // stages g, g + 1 visible and frees the slots of stages g - 2, g - 1.
     int ga = 0;
     auto step_a = [&](auto ph) __attribute__((always_inline)) {
@@ -907,17 +912,19 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
         h8_t a[8];
 #pragma unroll
         for (int mt = 0; mt < 8; mt++) a[mt] = *(const h8_t*)(sa + ar_off + 1024 * mt);
-        *(h8_t*)(smem + R5_Y + ((ga + 2) & 3) * R5_ASLOT + aw_off) = areg[PH];
-        areg[PH] = load_a(ca);
-        anext();
-        ga++;
 #pragma unroll
         for (int nt = 0; nt < 3; nt++)
 #pragma unroll
             for (int mt = 0; mt < 8; mt++)
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wreg[PH][nt], a[mt], acc[mt][nt], 0, 0, 0);
+        // (W before A, the ring write after the MFMAs: as in rowgemm5)
         load_w(cw, wreg[PH]);
         wnext();
+        __builtin_amdgcn_sched_barrier(0);
+        *(h8_t*)(smem + R5_Y + ((ga + 2) & 3) * R5_ASLOT + aw_off) = areg[PH];
+        areg[PH] = load_a(ca);
+        anext();
+        ga++;
     };
     // one k-step of a GEMM over the y tile (read in place; no barrier)
     auto step_y = [&](auto ph, int ks) __attribute__((always_inline)) {
