@@ -652,20 +652,33 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
         __builtin_amdgcn_s_barrier();
-        // whole rows out: wave w stores rows 16 w .. 16 w + 15, two per pass
-        // (lane half h: row 2 i + h, lane s: columns 4 s + 128 j)
-        const int h = lane >> 5, s = lane & 31;
+        // whole rows out: wave w stores rows 16 w .. 16 w + 15, one 768-byte
+        // row per instruction (lanes 0-47, 16 bytes each: 16 stores per lane
+        // instead of 24 of 8 bytes)
         half_t* out = (half_t*)pe.out16;
+        if (((uintptr_t)out & 15) == 0 && (pe.ldo16 & 7) == 0) {
+            if (lane < 48) {
+#pragma unroll 4
+                for (int i = 0; i < 16; i++) {
+                    const int lr = 16 * w + i;
+                    const int64_t row = t * RG_BM + lr;
+                    const h8_t v = *(const h8_t*)(smem + ym.off(lr, 16 * lane));
+                    if (row < Mrows) *(h8_t*)(out + row * pe.ldo16 + 8 * lane) = v;
+                }
+            }
+        } else {   // 8-byte aligned rows: two rows per pass, 8 bytes per lane
+            const int h = lane >> 5, s = lane & 31;
 #pragma unroll 2
-        for (int i = 0; i < 8; i++) {
-            const int lr = 16 * w + 2 * i + h;
-            const int64_t row = t * RG_BM + lr;
-            ep_h4 v[3];
+            for (int i = 0; i < 8; i++) {
+                const int lr = 16 * w + 2 * i + h;
+                const int64_t row = t * RG_BM + lr;
+                ep_h4 v[3];
 #pragma unroll
-            for (int j = 0; j < 3; j++) v[j] = *(const ep_h4*)(smem + ym.off(lr, (128 * j + 4 * s) * 2));
-            if (row < Mrows) {
+                for (int j = 0; j < 3; j++) v[j] = *(const ep_h4*)(smem + ym.off(lr, (128 * j + 4 * s) * 2));
+                if (row < Mrows) {
 #pragma unroll
-                for (int j = 0; j < 3; j++) *(ep_h4*)(out + row * pe.ldo16 + 128 * j + 4 * s) = v[j];
+                    for (int j = 0; j < 3; j++) *(ep_h4*)(out + row * pe.ldo16 + 128 * j + 4 * s) = v[j];
+                }
             }
         }
     };
