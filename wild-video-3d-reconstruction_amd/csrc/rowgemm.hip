@@ -1110,13 +1110,25 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
         }
         // the row epilogue now: rows 16 w .. 16 w + 15 (the next tile's y
         // tile writes follow its GEMM1 k-steps' barriers)
+        // (the accumulators are dead here: the next batch's loads are issued
+        // before this batch's arithmetic, two batches live)
         EpiConsts2 kc;
         load_consts2<F2>(p, lane, kc);
+        if constexpr (OVL) {   // (only the last tile: one batch live, no spill beside the deferred state)
 #pragma unroll 1
-        for (int q0 = 0; q0 < 16; q0 += 4) {
-            EpiOps2<4> st;
-            epi_issue(tile, 16 * w + q0, st);
-            epi_done(tile, 16 * w + q0, kc, st);
+            for (int q0 = 0; q0 < 16; q0 += 4) {
+                EpiOps2<4> st;
+                epi_issue(tile, 16 * w + q0, st);
+                epi_done(tile, 16 * w + q0, kc, st);
+            }
+        } else {
+            EpiOps2<4> st[2];
+            epi_issue(tile, 16 * w, st[0]);
+            bd_steps<0, 4>::run([&](auto bc) __attribute__((always_inline)) {
+                constexpr int b = decltype(bc)::value;
+                if constexpr (b + 1 < 4) epi_issue(tile, 16 * w + 4 * (b + 1), st[(b + 1) & 1]);
+                epi_done(tile, 16 * w + 4 * b, kc, st[b & 1]);
+            });
         }
     }
 }
