@@ -61,7 +61,7 @@ def source_sha(*names):
     return h.hexdigest()[:16]
 
 
-CORR_SOURCES = ("corrmfma.hip", "altcorr.hip")
+CORR_SOURCES = ("corrstage.hip", "corrmfma.hip", "corrmfma.hpp", "altcorr.hip")
 UPD_SOURCES = ("rowgemm.hip", "updateop.hip")
 
 
@@ -169,10 +169,11 @@ def gather_to_rank0(tensors, rank, world):
 
 
 class CorrProbe:
-    """HIP events around every altcorr launch on the stream it runs on: the
-    fused 2-level kernel (dpvo.altcorr.corr_pyramid / corr_pyramid_mfma, called
-    by DPVO.corr) and the matrix-core path's edge ordering (cuda_corr.edge_order,
-    a counting sort of the edges by target frame that DPVO.corr runs first)."""
+    """HIP events around every altcorr call on the stream it runs on: the
+    LDS-staged matrix-core path (dpvo.altcorr.corr_pyramid_staged: its
+    (frame, cell) binning, the staged kernel and the fallback kernel), or the
+    per-edge kernels (corr_pyramid / corr_pyramid_mfma) and the latter's edge
+    ordering (cuda_corr.edge_order) when those are configured."""
 
     def __init__(self):
         self.pairs = {"corr": [], "order": []}
@@ -197,6 +198,7 @@ class CorrProbe:
             return f
         altcorr.corr_pyramid = timed(altcorr.corr_pyramid, "corr")
         altcorr.corr_pyramid_mfma = timed(altcorr.corr_pyramid_mfma, "corr")
+        altcorr.corr_pyramid_staged = timed(altcorr.corr_pyramid_staged, "corr")
         cuda_corr.edge_order = timed(cuda_corr.edge_order, "order")
 
     def clear(self):
@@ -222,9 +224,10 @@ def _gpu_head_start(ms=2.0):
 def phase_breakdown(slam, reps=5):
     """Per-phase device time of one update, measured with events outside the
     timed loop.  The phases follow DPVO.update() (dpvo/dpvo.py) step by step,
-    with the same arguments: reproject; the window keys, both group-bys and
-    altcorr's visiting order (dpvo_window_group_by, jj_order); altcorr (the
-    fused matrix-core kernel in that order); the update operator; the BA
+    with the same arguments: reproject; the window keys and both group-bys
+    (dpvo_window_group_by; + the per-edge altcorr's visiting order when
+    STAGED_CORR is off); altcorr (binning + staged kernel + fallback, or the
+    per-edge kernel in that order); the update operator; the BA
     targets + fastba; the point cloud.  Each rep starts behind a device-side
     delay, so the phases run back to back as in the timed loop."""
     import update_ops
@@ -242,9 +245,11 @@ def phase_breakdown(slam, reps=5):
         e[0].record()
         coords = slam.reproject()
         e[1].record()
-        ctx_idx, jslot, kk_groups, ij_groups, order = update_ops.window_group_by(
+        want_order = not getattr(slam.cfg, "STAGED_CORR", True)
+        ctx_idx, jslot, kk_groups, ij_groups, *rest = update_ops.window_group_by(
             slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M, slam.n - 64, slam.M * slam.pmem, slam.pmem,
-            flag=slam._ba_status, jj_order=True)
+            flag=slam._ba_status, jj_order=want_order)
+        order = rest[0] if want_order else None
         e[2].record()
         with torch.autocast("cuda", enabled=True):
             corr = slam.corr(coords, slots=(ctx_idx, jslot), order=order)
@@ -289,13 +294,14 @@ def gmap_pack_ms(slam, reps=5):
     return round(float(np.median(ts)), 4)
 
 
-def host_cost(slam, reps=6):
+def host_cost(slam, cores, reps=6):
     """Host CPU per eager update(): the Python thread's CPU time (launches,
     ctypes, torch dispatch) against the GPU time of the same update, from
     updates run back to back behind a device-side delay (so the host never
-    waits for the device inside the measured span).  Decides whether several
-    ranks sharing this host would be launch-bound (8 ranks: > 1/8 of the
-    step)."""
+    waits for the device inside the measured span).  Every rank launches from
+    its own thread on its own pinned block of cores (pin_host_cores), so the
+    figure that decides whether a rank is launch-bound is its own launching
+    thread's share of a step, thread_ms / gpu_ms (1.0 = launch-bound)."""
     slam.update()
     torch.cuda.synchronize()
     _gpu_head_start(20.0)
@@ -310,7 +316,8 @@ def host_cost(slam, reps=6):
     thread_ms = (c1 - c0) / reps * 1e3
     gpu_ms = a.elapsed_time(b) / reps
     return {"thread_ms": round(thread_ms, 4), "gpu_ms": round(gpu_ms, 4),
-            "ranks_per_host_before_launch_bound": round(gpu_ms / max(thread_ms, 1e-6), 1)}
+            "launch_thread_share": round(thread_ms / max(gpu_ms, 1e-6), 3),
+            "pinned_cores_per_rank": len(cores) if cores else None}
 
 
 def load_counters(path, edges):
@@ -590,14 +597,14 @@ def main():
     # update() makes no host read (BA's status is checked after the loop,
     # slam.check_ba).  --graph captures it once into a HIP graph during the
     # warmup and replays it (the patch graph does not change between steps);
-    # measured no faster on one GPU (2.78 vs 2.71 ms/step at C3), so eager is
-    # the default and the corr events below time every launch live
+    # within box spread of eager on one GPU (profiles/r4/bench_c3_graph_r4.json),
+    # so eager is the default and the corr events below time every launch live
     with torch.no_grad():
-        host = host_cost(slam)
-    # several ranks share one host: when one eager update() costs the host more
-    # than 1/8 of its GPU time, 8 ranks would be launch-bound -- replay it from
-    # a HIP graph instead (one launch per step)
-    graph = args.graph or (world > 1 and host["thread_ms"] > host["gpu_ms"] / 8)
+        host = host_cost(slam, args.cores)
+    # each rank launches from its own pinned cores: replay update() from a HIP
+    # graph (one launch per step) when a rank's launching thread is busy for
+    # more than half of its step -- host jitter could then starve its GPU
+    graph = args.graph or (world > 1 and host["launch_thread_share"] > 0.5)
     upd = slam.update_graphed if graph else slam.update
     with torch.no_grad():
         for _ in range(max(args.warmup, 2 if graph else 0)):

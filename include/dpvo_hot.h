@@ -41,6 +41,13 @@ enum { DPVO_F16 = 0, DPVO_F32 = 1, DPVO_F64 = 2 };
 
 int dpvo_hot_abi_version(void);
 const char* dpvo_hot_last_error(void);
+/* "sha=<16 hex> flavour=<product|stamps>": the sha256 prefix of the HIP
+ * sources the library was compiled from (the .hip and .hpp files of csrc in byte
+ * order, then this header, concatenated) and whether it is the diagnostic
+ * build with in-kernel stamps (DPVO_STAMPS).  The Python loader refuses a
+ * library whose sha differs from the sources shipped beside it, and a stamps
+ * build unless DPVO_DIAG=1. */
+const char* dpvo_hot_build_info(void);
 
 /* ------------------------------------------------------------------------
  * altcorr -- replaces cuda_corr (reference dpvo/altcorr/correlation.cpp:57-62)
@@ -119,6 +126,26 @@ int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, const void* c
 size_t dpvo_edge_order_workspace_bytes(int num_buckets);
 int dpvo_edge_order(const int64_t* jj, int64_t num_edges, int num_buckets, int* order, void* workspace,
                     size_t workspace_bytes, void* stream);
+
+/* The same [E][882] rows as dpvo_corr_pyramid_mfma, bit for bit, with the
+ * target frames' windows staged in LDS (csrc/corrstage.hip): the edges are
+ * binned on the device by (target frame jj, 8x8-pixel cell of the level-1
+ * map); one workgroup per CU stages a cell's 17x17 level-1 and 11x11 level-2
+ * pixels once and runs all of the cell's edges from LDS.  Edges whose boxes
+ * do not fit their cell's regions (patches spread over more than 4 pixels,
+ * far outside the map, bad indices, non-finite coordinates) run through
+ * dpvo_corr_pyramid_mfma's kernel afterwards.  Same arguments as
+ * dpvo_corr_pyramid_mfma without `order`; workspace: at least
+ * dpvo_corr_staged_workspace_bytes(E, N2, H, W) device bytes for N2 frames of
+ * an H x W level-1 map (0: too many bins; use dpvo_corr_pyramid_mfma).
+ * Six launches: a memset, the binning (count, scan, scatter), the staged
+ * kernel, the fallback kernel. */
+size_t dpvo_corr_staged_workspace_bytes(int64_t num_edges, int64_t num_frames, int64_t height, int64_t width);
+int dpvo_corr_pyramid_staged(const void* table, int64_t num_patches, const void* const* fmaps,
+                             const int64_t* fmap_sizes, const int64_t* fmap_strides, const float* level_scale,
+                             const float* coords, const int64_t* coords_size, const int64_t* coords_stride,
+                             const int64_t* ii, const int64_t* jj, void* corr, int64_t edge_stride, void* workspace,
+                             size_t workspace_bytes, void* stream);
 
 /* cuda_corr.backward (correlation_kernel.cu:236-286): grad is the returned
  * (permuted) view's gradient given as contiguous [B][E][2r+1 (x)][2r+1 (y)][P][P]
@@ -383,7 +410,8 @@ int dpvo_scatter_csr(int op, int dtype, const void* src, int64_t outer, int64_t 
  * be finite); A, W, zero_row 16-byte aligned; zero_row holds >= K zeros.
  * Supported flag sets: 0, RELU, SIGMOID, LN|LN_RELU, RES, RES|LN, GATE,
  * GATE|LN, GATE|HEADS; and WKB, WKB|RELU, WKB|SIGMOID (k-blocked W, K a
- * multiple of 32). */
+ * multiple of 64 as well: the kernel's one barrier per two k-steps must fall
+ * between one tile's y-tile reads and the next tile's writes). */
 enum {
     DPVO_RG_RELU = 1, DPVO_RG_SIGMOID = 2, DPVO_RG_RES = 4, DPVO_RG_GATE = 8, DPVO_RG_LN = 16, DPVO_RG_LN_RELU = 32,
     DPVO_RG_HEADS = 64,

@@ -8,6 +8,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 os.environ["DPVO_HOT_LIB"] = os.path.join(REPO, "diag", "libdpvo_hot.so")
+os.environ["DPVO_DIAG"] = "1"   # the loader refuses the stamps build otherwise
 sys.path.insert(0, os.path.join(REPO, "wild-video-3d-reconstruction_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

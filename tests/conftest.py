@@ -23,6 +23,16 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: requires an MI355X GPU (HIP path through the C-ABI)")
 
 
+def pytest_report_header(config):
+    """which libdpvo_hot.so the run loads (its source sha and flavour)."""
+    try:
+        import _dpvo_hot as H
+        H.lib()
+        return [f"libdpvo_hot: {H.LIB_PATH} {H.build_info} (tree sources sha={H.source_sha()})"]
+    except Exception as e:  # pragma: no cover - reported, the tests then fail on their own
+        return [f"libdpvo_hot: not loadable: {e}"]
+
+
 def pytest_collection_modifyitems(config, items):
     try:
         import torch

@@ -93,3 +93,40 @@ def test_ctypes_signatures_match_the_header():
         if protos.get(name) != got:
             bad[name] = (protos.get(name), got)
     assert not bad, bad
+
+
+def test_library_provenance_matches_the_shipped_sources():
+    """The loaded library was compiled from the csrc/ beside it, as the product
+    (not the stamped diagnostic) build."""
+    import _dpvo_hot as H
+    H.lib()
+    assert H.build_info["flavour"] == "product"
+    assert H.build_info["sha"] == H.source_sha()
+
+
+def test_stale_or_stamped_library_is_refused():
+    import _dpvo_hot as H
+    sha = H.source_sha()
+    stale = "0" * 16 if sha != "0" * 16 else "1" * 16
+    with pytest.raises(ImportError, match="stale"):
+        H.verify_build(f"sha={stale} flavour=product", sha)
+    with pytest.raises(ImportError, match="diagnostic"):
+        H.verify_build(f"sha={sha} flavour=stamps", sha)
+    assert H.verify_build(f"sha={sha} flavour=stamps", sha, diag=True)["flavour"] == "stamps"
+    with pytest.raises(ImportError, match="provenance"):
+        H.verify_build("", sha)
+
+
+def test_stale_library_fails_at_load(tmp_path):
+    """A library whose recorded sha differs from the tree's sources fails when
+    a fresh interpreter loads it (sources edited after the build)."""
+    import shutil
+    import sys
+    csrc = tmp_path / "csrc"
+    shutil.copytree(os.path.join(PKG, "csrc"), csrc)
+    with open(csrc / "common.hpp", "a") as f:
+        f.write("\n// edited after the build\n")
+    code = ("import sys; sys.path.insert(0, %r); import _dpvo_hot as H; H.source_sha = "
+            "(lambda f: (lambda *a, **k: f(%r)))(H.source_sha); H.lib()") % (PKG, str(csrc))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True)
+    assert r.returncode != 0 and "stale" in r.stderr

@@ -225,3 +225,28 @@ def test_ba_window_sizes_of_the_per_patch_path(window):
     assert status == 0
     assert_close_rel(gp, rp)
     assert_close_rel(gq[:, 2], rq[:, 2])
+
+
+@pytest.mark.parametrize("window", [10, 11, 12])
+def test_ba_workspace_guard_untouched(window):
+    """The deterministic path writes nothing past its workspace (the dense rows
+    for the wave solver exist only for <= 10 poses; 11-12 poses used to overrun
+    them into whatever the allocator placed next)."""
+    import _dpvo_hot as H
+    st = synth_dpvo_state(8, n=40, M=16)
+    n = st["n"]
+    p, q = T(st["poses"]), T(st["patches"])[None]
+    ii, jj, kk = T(st["ii"]), T(st["jj"]), T(st["kk"])
+    E = ii.numel()
+    nbytes = H.lib().dpvo_ba_workspace_bytes_ex(E, q.numel() // 27, window, 0)
+    guard = 1 << 16
+    ws = torch.full((nbytes + guard,), 0xAB, dtype=torch.uint8, device="cuda:0")
+    status = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+    intr, tgt, wt = T(st["intrinsics"]), T(st["target"]), T(st["weight"])
+    lm = torch.tensor([1e-4], device="cuda:0")
+    H.check(H.lib().dpvo_ba_forward_csr(
+        H.ptr(p), H.ptr(q), q.numel() // 27, 3, H.ptr(intr), H.ptr(tgt), H.ptr(wt), H.ptr(lm), H.ptr(ii), H.ptr(jj),
+        H.ptr(kk), E, n - window, n, 2, 0, None, None, None, H.ptr(ws), nbytes, H.ptr(status), H.stream_of(p)))
+    torch.cuda.synchronize()
+    assert int(status.item()) == 0
+    assert bool((ws[nbytes:] == 0xAB).all())

@@ -216,6 +216,13 @@ def test_errors():
         U.rowgemm(A, W16, b16, flags=U.RELU | U.LN)   # unsupported combination
     with pytest.raises(RuntimeError):
         U.rowgemm(A.float(), W16, b16)
+    # k-blocked W needs K % 64 == 0 (K = 32: one k-step per tile, no barrier
+    # between a tile's y-tile reads and the next tile's writes)
+    A32 = torch.randn(300, 32, device="cuda").half()
+    w32, b32 = lin(32, 7)
+    W32, c32 = U.pack_linear(w32, b32)
+    with pytest.raises(RuntimeError, match="multiple of 64"):
+        U.rowgemm(A32, U.kblock(W32[:, :32].contiguous()), c32)
 
 
 def test_fused_update_operator_matches_torch_path():

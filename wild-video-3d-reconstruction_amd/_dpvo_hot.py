@@ -7,12 +7,15 @@ call raises, so a silently-degraded run cannot pass for the HIP path.
 from __future__ import annotations
 
 import ctypes
+import glob
+import hashlib
 import os
 
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DPVO_HOT_LIB", os.path.join(HERE, "libdpvo_hot.so"))
+HEADER = os.path.join(os.path.dirname(HERE), "include", "dpvo_hot.h")
 
 F16, F32, F64 = 0, 1, 2
 _DTYPES = {torch.float16: F16, torch.float32: F32, torch.float64: F64}
@@ -27,6 +30,7 @@ _sz = ctypes.c_size_t
 _SIGNATURES = {
     "dpvo_hot_abi_version": (_ip, []),
     "dpvo_hot_last_error": (ctypes.c_char_p, []),
+    "dpvo_hot_build_info": (ctypes.c_char_p, []),
     "dpvo_corr_forward": (_ip, [_ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip, _vp, _vp]),
     "dpvo_corr_forward_pyramid": (_ip, [_ip, _vp, _vp, _vp, _ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip,
                                         _vp, _vp]),
@@ -37,6 +41,9 @@ _SIGNATURES = {
     "dpvo_corr_pack_mfma_bytes": (_sz, [_vp]),
     "dpvo_corr_pack_mfma": (_ip, [_vp, _vp, _vp, _vp, _vp]),
     "dpvo_corr_pyramid_mfma": (_ip, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
+    "dpvo_corr_staged_workspace_bytes": (_sz, [_i64, _i64, _i64, _i64]),
+    "dpvo_corr_pyramid_staged": (_ip, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _sz,
+                                       _vp]),
     "dpvo_edge_order_workspace_bytes": (_sz, [_ip]),
     "dpvo_edge_order": (_ip, [_vp, _i64, _ip, _vp, _vp, _sz, _vp]),
     "dpvo_corr_backward": (_ip, [_ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip, _vp, _vp, _vp]),
@@ -105,11 +112,52 @@ _SIGNATURES = {
 EXPORTED = tuple(_SIGNATURES)
 
 _lib = None
+build_info = None   # the loaded library's dpvo_hot_build_info(), parsed
+
+
+def source_sha(csrc=None, header=HEADER):
+    """sha256 prefix of the HIP sources shipped beside the library, in the
+    Makefile's order (csrc/*.hip and csrc/*.hpp sorted by name, then the C-ABI
+    header); None when the sources are not present."""
+    csrc = csrc or os.path.join(HERE, "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp")),
+                   key=lambda f: "csrc/" + os.path.basename(f))
+    if not files or not os.path.exists(header):
+        return None
+    h = hashlib.sha256()
+    for f in files + [header]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def parse_build_info(info):
+    out = {}
+    for kv in info.split():
+        k, _, v = kv.partition("=")
+        out[k] = v
+    return out
+
+
+def verify_build(info, src_sha, diag=False):
+    """Refuse a library built from other sources than the ones beside it, or
+    the stamped diagnostic build unless diag (DPVO_DIAG=1).  Returns the
+    parsed info."""
+    b = parse_build_info(info)
+    if "sha" not in b or "flavour" not in b:
+        raise ImportError(f"libdpvo_hot.so reports no build provenance ({info!r}): rebuild it (make -B)")
+    if src_sha is not None and b["sha"] != src_sha:
+        raise ImportError(f"libdpvo_hot.so is stale: built from sources sha={b['sha']}, the tree holds "
+                          f"sha={src_sha}; rebuild it (__graft_entry__.build())")
+    if b["flavour"] != "product" and not diag:
+        raise ImportError(f"libdpvo_hot.so is the '{b['flavour']}' diagnostic build; set DPVO_DIAG=1 to load it")
+    return b
 
 
 def lib():
-    """Load libdpvo_hot.so once; raise if it was not built."""
-    global _lib
+    """Load libdpvo_hot.so once; raise if it was not built, is stale against
+    the shipped sources, or is the diagnostic build."""
+    global _lib, build_info
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise ImportError(
@@ -120,6 +168,8 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        build_info = verify_build(handle.dpvo_hot_build_info().decode(), source_sha(),
+                                  diag=os.environ.get("DPVO_DIAG") == "1")
         _lib = handle
     return _lib
 

@@ -23,40 +23,14 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "common.hpp"
+#include "corrmfma.hpp"
 
 namespace dpvo {
 
-namespace cm {
-constexpr int R = 3, D = 8, DO = 7, NP = 9, C = 128, BOXMAX = 12, WAVES = 4;
-constexpr int RS = 148;           // LDS row per patch pixel: the box's <= 144 pixels (+ pad: rows 4 apart, 16 banks apart)
-constexpr int RL = NP * RS;       // per level
-constexpr unsigned OOB = 0x80000000u;   // a buffer offset past every descriptor's range: the load returns 0
-}  // namespace cm
 
 typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
 typedef float f4m_t __attribute__((ext_vector_type(4)));
 
-struct CorrMfmaParams {
-    const half_t* gt;   // [N1][9][128] transposed patch features
-    int N1;
-    const float* coords;
-    int64_t c_s[5];
-    const int64_t* ii;
-    const int64_t* jj;
-    int E;
-    const half_t* fmap[2];
-    int64_t f_s1[2];
-    int N2[2], H2[2], W2[2];
-    int64_t rowb[2];          // row stride in bytes
-    int pixb[2];              // pixel stride in bytes
-    int rowext[2];            // bytes from a row's first pixel to the end of its last
-    int frameext[2];          // bytes from a frame's first pixel to the end of its last
-    float scale[2];
-    half_t* out;
-    int64_t o_e;
-    const int* order;   // optional edge visiting order (edges grouped by target frame), NULL = 0..E-1
-};
 
 
 __device__ __forceinline__ void cm_wave_fence()
@@ -70,19 +44,22 @@ __device__ __forceinline__ void cm_wave_fence()
 // eighth of the (target-frame-grouped) edge sequence, walked by all of its
 // waves in step, so an XCD streams through a few target frames' maps instead
 // of every XCD touching every frame.
+// Slots [begin, E) of the order (begin > 0: the tail of a staged launch's
+// order, dpvo_corr_pyramid_staged's fallback edges).
 struct CmRange { int slot, end, stride; };
-__device__ __forceinline__ CmRange cm_range(int E, int wave)
+__device__ __forceinline__ CmRange cm_range(int begin, int E, int wave)
 {
     const int nblk = gridDim.x, b = blockIdx.x;
+    const int n = E - begin;
     CmRange r;
     if (nblk >= 8 && (nblk & 7) == 0) {
         const int x = b & 7, per = nblk >> 3;
-        const int lo = (int)((int64_t)E * x / 8);
-        r.end = (int)((int64_t)E * (x + 1) / 8);
+        const int lo = begin + (int)((int64_t)n * x / 8);
+        r.end = begin + (int)((int64_t)n * (x + 1) / 8);
         r.slot = lo + (b >> 3) * cm::WAVES + wave;
         r.stride = per * cm::WAVES;
     } else {
-        r.slot = b * cm::WAVES + wave;
+        r.slot = begin + b * cm::WAVES + wave;
         r.end = E;
         r.stride = nblk * cm::WAVES;
     }
@@ -173,7 +150,7 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
     __shared__ int ebase[WAVES][2][16];      // window origin of each patch pixel inside its raw row
     __shared__ int estr[WAVES][2];           // raw row stride of the window (box width, or 8)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const CmRange rg = cm_range(p.E, wave);
+    const CmRange rg = cm_range(p.dev_begin ? *p.dev_begin : 0, p.E, wave);
     int slot = rg.slot;
     if (slot >= rg.end) return;   // the whole wave; nothing below synchronises across waves
     float* rw = raw[wave];
@@ -512,18 +489,19 @@ extern "C" int dpvo_edge_order(const int64_t* jj, int64_t num_edges, int num_buc
     return 0;
 }
 
-extern "C" int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, const void* const* fmaps,
-                                      const int64_t* fmap_sizes, const int64_t* fmap_strides,
-                                      const float* level_scale, const float* coords, const int64_t* coords_size,
-                                      const int64_t* coords_stride, const int64_t* ii, const int64_t* jj, void* corr,
-                                      int64_t edge_stride, const int* order, void* stream)
+namespace dpvo {
+
+int corr_mfma_setup(CorrMfmaParams& p, const void* table, int64_t num_patches, const void* const* fmaps,
+                    const int64_t* fmap_sizes, const int64_t* fmap_strides, const float* level_scale,
+                    const float* coords, const int64_t* coords_size, const int64_t* coords_stride, const int64_t* ii,
+                    const int64_t* jj, void* corr, int64_t edge_stride, const int* order)
 {
     DPVO_CHECK_ARG(coords_size[0] == 1 && coords_size[2] == 2 && coords_size[3] == 3 && coords_size[4] == 3,
                    "coords must be [1][E][2][3][3]");
     DPVO_CHECK_ARG(edge_stride == 0 || edge_stride >= 882, "edge_stride smaller than one edge's 882 features");
     const int64_t E = coords_size[1];
     DPVO_CHECK_ARG(E < 0x7fffffff && num_patches < 0x7fffffff, "too many edges / patches");
-    CorrMfmaParams p{};
+    p = CorrMfmaParams{};
     p.gt = (const half_t*)table;
     p.N1 = (int)num_patches;
     p.coords = coords;
@@ -559,13 +537,32 @@ extern "C" int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, co
     p.o_e = edge_stride ? edge_stride : 882;
     p.order = order;
     DPVO_CHECK_ARG(reinterpret_cast<uintptr_t>(corr) % 4 == 0 && p.o_e % 2 == 0, "corr rows must be 4-byte aligned");
-    if (E == 0) return 0;
+    return 0;
+}
+
+int corr_mfma_launch(const CorrMfmaParams& p, hipStream_t s)
+{
+    if (p.E == 0) return 0;
     // persistent: a few workgroups per CU, each wave walking a grid-stride range of edges
     // (a multiple of 8 once there are 8 workgroups' worth of edges: see cm_range)
-    int64_t g = std::min<int64_t>((E + cm::WAVES - 1) / cm::WAVES, 256 * 3);   // LDS and VGPRs: 3 per CU
+    int64_t g = std::min<int64_t>((p.E + cm::WAVES - 1) / cm::WAVES, 256 * 3);   // LDS and VGPRs: 3 per CU
     if (g > 8) g &= ~int64_t(7);
-    const unsigned grid = (unsigned)g;
-    hipLaunchKernelGGL(corr_mfma_kernel, dim3(grid), dim3(64 * cm::WAVES), 0, as_stream(stream), p);
+    hipLaunchKernelGGL(corr_mfma_kernel, dim3((unsigned)g), dim3(64 * cm::WAVES), 0, s, p);
     DPVO_CHECK_LAUNCH();
     return 0;
+}
+
+}  // namespace dpvo
+
+extern "C" int dpvo_corr_pyramid_mfma(const void* table, int64_t num_patches, const void* const* fmaps,
+                                      const int64_t* fmap_sizes, const int64_t* fmap_strides,
+                                      const float* level_scale, const float* coords, const int64_t* coords_size,
+                                      const int64_t* coords_stride, const int64_t* ii, const int64_t* jj, void* corr,
+                                      int64_t edge_stride, const int* order, void* stream)
+{
+    CorrMfmaParams p;
+    if (corr_mfma_setup(p, table, num_patches, fmaps, fmap_sizes, fmap_strides, level_scale, coords, coords_size,
+                        coords_stride, ii, jj, corr, edge_stride, order))
+        return -1;
+    return corr_mfma_launch(p, as_stream(stream));
 }

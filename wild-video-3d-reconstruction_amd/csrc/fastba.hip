@@ -1573,6 +1573,7 @@ constexpr int BD_N6MAX = 6 * BD_NMAX;     // 72
 // (spills).
 constexpr int BD_WAVES = 4;
 constexpr int BD_HD_LD = 64;   // row pitch of the dense lower-triangle system the wave solver loads
+static_assert(6 * 10 + 1 <= 64 && 6 * 10 < BD_HD_LD, "Hd (64 rows x BD_HD_LD) holds the wave solver's n6 + 1 rows");
 // 4 waves each.  Measured over 256-2048 (round 3) and again with this round's
 // reduce and solve: 768 / 1024 workgroups 54-56 us per iteration at C2
 // against 46 at 512 (the reduce reads every workgroup's partial)
@@ -2148,9 +2149,13 @@ __global__ __launch_bounds__(1024) void bd_reduce_kernel(BdParams p)
             b = n;
         }
         // the wave solver's rows: the damped lower triangle (S += diag(1e-4 S
-        // + 1), ba_cuda.cu:517-518), zeros above it, the g row
-        p.Hd[b * BD_HD_LD + a] = a == b ? t + (1e-4f * t + 1.0f) : t;
-        if (a < b && b < n) p.Hd[a * BD_HD_LD + b] = 0.f;
+        // + 1), ba_cuda.cu:517-518), zeros above it, the g row.  Only for the
+        // windows it solves (n6 + 1 rows of BD_HD_LD): 11-12 poses go to
+        // bd_solve_kernel, which reads H, and would overrun Hd's 64 rows
+        if (n < BD_HD_LD) {
+            p.Hd[b * BD_HD_LD + a] = a == b ? t + (1e-4f * t + 1.0f) : t;
+            if (a < b && b < n) p.Hd[a * BD_HD_LD + b] = 0.f;
+        }
     }
 }
 

@@ -1242,7 +1242,10 @@ static int validate_rowgemm(const dpvo_rowgemm_args* a)
     if (a->flags & DPVO_RG_WKB) {
         DPVO_CHECK_ARG((a->flags & ~(DPVO_RG_WKB | DPVO_RG_RELU | DPVO_RG_SIGMOID)) == 0,
                        "rowgemm: k-blocked W (WKB) takes only RELU / SIGMOID");
-        DPVO_CHECK_ARG(a->K > 0 && a->K % R5_BK == 0, "rowgemm: K must be a positive multiple of 32 with WKB");
+        // K a multiple of 2 k-steps: every tile's last k-step is then odd, so the
+        // even step after it (one barrier per two steps) separates a tile's
+        // y-tile reads from the next tile's y-tile writes (K = 32 would race)
+        DPVO_CHECK_ARG(a->K > 0 && a->K % (2 * R5_BK) == 0, "rowgemm: K must be a positive multiple of 64 with WKB");
         DPVO_CHECK_ARG(a->out16 && a->ldo16 % 4 == 0 && ((uintptr_t)a->out16 & 7) == 0 && !a->out32,
                        "rowgemm: WKB writes out16 only (8-byte aligned rows)");
     } else {

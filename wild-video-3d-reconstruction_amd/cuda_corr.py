@@ -132,6 +132,45 @@ def forward_pyramid_mfma(table, num_patches, pyramid, coords, ii, jj, scales=(1,
     return out
 
 
+def staged_workspace(num_edges, pyramid, out=None):
+    """uint8 device workspace for forward_pyramid_staged (reused when large enough)."""
+    f1 = pyramid[0]
+    nbytes = H.lib().dpvo_corr_staged_workspace_bytes(int(num_edges), int(min(f.shape[1] for f in pyramid)),
+                                                      int(f1.shape[3]), int(f1.shape[4]))
+    if nbytes == 0:
+        raise RuntimeError("forward_pyramid_staged: too many (frame, cell) bins; use forward_pyramid_mfma")
+    if out is None or out.numel() < nbytes:
+        out = torch.empty(nbytes, dtype=torch.uint8, device=f1.device)
+    return out
+
+
+def forward_pyramid_staged(table, num_patches, pyramid, coords, ii, jj, scales=(1, 4), out=None, workspace=None):
+    """forward_pyramid_mfma's rows, bit for bit, with the target-frame windows
+    staged in LDS (csrc/corrstage.hip; see include/dpvo_hot.h).  No visiting
+    order: the edges are binned by (target frame, level-1 cell) on the device.
+    workspace (optional): staged_workspace(E, pyramid), reused across calls."""
+    H.on_gpu(table, coords, ii, jj, *pyramid)
+    if len(pyramid) != 2 or any(f.dtype != torch.float16 for f in pyramid):
+        raise RuntimeError("forward_pyramid_staged: two fp16 pyramid levels")
+    if coords.dtype != torch.float32 or coords.dim() != 5 or tuple(coords.shape[2:]) != (2, 3, 3):
+        raise RuntimeError("forward_pyramid_staged: coords must be float32 [1, E, 2, 3, 3]")
+    E = coords.shape[1]
+    if out is None:
+        out = torch.empty((1, E, 882), dtype=torch.float16, device=coords.device)
+    elif out.shape != (1, E, 882) or out.dtype != torch.float16 or out.stride(2) != 1:
+        raise RuntimeError("forward_pyramid_staged: out must be [1, E, 882] fp16 with unit feature stride")
+    ii, jj = H.idx64(ii), H.idx64(jj)
+    ws = staged_workspace(E, pyramid, workspace)
+    ptrs = (H._vp * 2)(*[f.data_ptr() for f in pyramid])
+    fs = H.i64arr([s for f in pyramid for s in f.shape])
+    fst = H.i64arr([s for f in pyramid for s in f.stride()])
+    sc = (H._fp * 2)(*[float(s) for s in scales])
+    H.check(H.lib().dpvo_corr_pyramid_staged(
+        H.ptr(table), int(num_patches), ptrs, fs, fst, sc, H.ptr(coords), H.sizes(coords), H.strides(coords),
+        H.ptr(ii), H.ptr(jj), H.ptr(out), out.stride(1) if E > 0 else 0, H.ptr(ws), ws.numel(), H.stream_of(coords)))
+    return out
+
+
 def backward(fmap1, fmap2, coords, ii, jj, grad, radius):
     """correlation.cpp:37-45 / correlation_kernel.cu:236-286 -> [fmap1_grad, fmap2_grad]."""
     _check_corr_args(fmap1, fmap2, coords, ii, jj)

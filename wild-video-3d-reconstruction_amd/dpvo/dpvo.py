@@ -202,6 +202,13 @@ class DPVO:
             out = buf[:E, :CORR_DIM].unsqueeze(0)
             if not getattr(self.cfg, "EXACT_CORR", False) and getattr(self.cfg, "CHANNEL_LAST_FMAPS", True):
                 # matrix cores, fp32 accumulation (csrc/corrmfma.hip)
+                if getattr(self.cfg, "STAGED_CORR", True):
+                    # the same rows with each (target frame, 8x8 cell)'s windows
+                    # staged in LDS once for all of its edges (csrc/corrstage.hip)
+                    self._corr_ws = cuda_corr.staged_workspace(E, self.pyramid, getattr(self, "_corr_ws", None))
+                    return altcorr.corr_pyramid_staged(self._gmap_table(mfma=True), self.gmap.shape[1], self.pyramid,
+                                                       coords, ii1, jj1, out=out,
+                                                       workspace=self._corr_ws).view(1, E, -1)
                 # edges grouped by target frame: one frame's map per XCD L2 at a time
                 if order is None:
                     order = cuda_corr.edge_order(jj1, self.pmem)
@@ -427,9 +434,13 @@ class DPVO:
                 # window keys in four launches (an edge outside the window sets
                 # the deferred failure word: the next keyframe() / check_ba() raises)
                 # (+ the edges grouped by target frame: altcorr's visiting order)
-                ctx_idx, jslot, kk_groups, ij_groups, order = update_ops.window_group_by(
+                # (the per-edge matrix-core altcorr's visiting order only when it
+                # runs: the staged kernel bins the edges itself)
+                want_order = not getattr(self.cfg, "STAGED_CORR", True)
+                ctx_idx, jslot, kk_groups, ij_groups, *rest = update_ops.window_group_by(
                     self.pg.ii, self.pg.jj, self.pg.kk, self.M, self.n - 64, self.M * self.pmem, self.pmem,
-                    flag=self._ba_status if defer else self._ba_fail, jj_order=True)
+                    flag=self._ba_status if defer else self._ba_fail, jj_order=want_order)
+                order = rest[0] if want_order else None
                 slots = (ctx_idx, jslot)
             else:
                 kk_groups, ij_groups = self._kk_groups(), self._ij_groups()
@@ -483,6 +494,11 @@ class DPVO:
             if "cholesky" not in str(e):
                 raise
             status = 1
+            # the immediate raise left update() before its point refresh; the
+            # reference catches around BA only and still recomputes the points
+            m = self.pg.m
+            pops.point_cloud_centre(SE3(self.poses), self.patches[:, :m], self.intrinsics, self.ix[:m],
+                                    out=self.pg.points_[:m])
         finally:
             target = self.pg.target
             self.pg.target, self.pg.weight = saved
@@ -492,7 +508,9 @@ class DPVO:
         elif status:
             self._ba_fail.zero_()
             cuda_ba.raise_for_status(status)
-        return self.pg.points_[:self.pg.m], target
+        # a fresh tensor, as the reference returns (pg.points_ is rewritten by
+        # the next update())
+        return self.pg.points_[:self.pg.m].clone(), target
 
     def _window_keys(self):
         """True when every edge of the sliding window has n - 64 <= ii, jj < n
