@@ -468,7 +468,7 @@ def encoder_fixtures():
     print("encoders: reference BasicEncoder4 vectors saved")
 
 
-def update_step_fixtures(pops, ba, lie, dscale=None, save=True):
+def update_step_fixtures(pops, ba, lie, dscale=None, save=True, which="small"):
     """One whole DPVO.update() (dpvo.py:711-749) of the reference from the
     injected steady-state graph of net_inputs.update_step_state(), through the
     reference's own modules:
@@ -488,8 +488,9 @@ def update_step_fixtures(pops, ba, lie, dscale=None, save=True):
     own error at this state.  The C oracle's restatement of ba_cuda.cu is run
     on the r16 targets as a cross-check of the ba.py mapping."""
     net_mod = importlib.import_module("dpvo.net")
-    S = NI.update_step_state()
-    C = NI.STEP
+    C = NI.STEPS[which]
+    S = NI.update_step_state(NI.STEP_SEED, C)
+    iters = C["iters"]
     n, M, pmem = C["n"], C["M"], C["pmem"]
     m = n * M
     t0 = n - C["opt_window"]
@@ -497,7 +498,7 @@ def update_step_fixtures(pops, ba, lie, dscale=None, save=True):
     upd = net_mod.Update(3)
     spec = NI.spec_json(upd.state_dict())
     _load(upd, spec, NI.UPDATE_SEED)
-    dscale = NI.STEP_DSCALE if dscale is None else dscale
+    dscale = C.get("dscale", NI.STEP_DSCALE) if dscale is None else dscale
     with torch.no_grad():   # the delta head scaled (net_inputs.STEP_DSCALE): see there
         upd.d[1].weight.mul_(dscale)
         upd.d[1].bias.mul_(dscale)
@@ -514,7 +515,7 @@ def update_step_fixtures(pops, ba, lie, dscale=None, save=True):
     cx, cy = C["intrinsics"][2], C["intrinsics"][3]
     bounds = [-64, -64, 2 * cx + 64, 2 * cy + 64]
     out = dict(seed=np.int64(NI.STEP_SEED), dscale=np.float64(dscale), update_seed=np.int64(NI.UPDATE_SEED), spec=np.array(spec),
-               t0=np.int64(t0), n=np.int64(n), rows=rows, corr_rows=crow,
+               t0=np.int64(t0), n=np.int64(n), rows=rows, corr_rows=crow, which=np.array(which), iters=np.int64(iters),
                state_checksum=np.stack([NI.checksum(S[k]) for k in sorted(S)]))
     touched = np.unique(S["kk"])
     out["touched"] = touched
@@ -542,7 +543,7 @@ def update_step_fixtures(pops, ba, lie, dscale=None, save=True):
             target = coords[..., 1, 1] + delta.to(dt)
             Gs, pt = lie.SE3(poses.clone()), patches.clone()
             est = torch.zeros_like(pt)
-            for _ in range(2):
+            for _ in range(iters):
                 Gs, pt = ba.BA(Gs, pt, intr, target, weight, 1e-4, ii, jj, kk, bounds, ep=1.0, fixedp=t0,
                                structure_only=False, patches_est=est)
                 dep = pt[0, touched, 2].numpy()
@@ -562,7 +563,7 @@ def update_step_fixtures(pops, ba, lie, dscale=None, save=True):
         if mode == "r16":
             # the C restatement of ba_cuda.cu on the same fp32 targets / weights
             rp, rq, st = oracle.ba_forward(S["poses"], S["patches"], S["intrinsics"], target.numpy(),
-                                           weight.numpy(), 1e-4, S["ii"], S["jj"], S["kk"], t0, n, 2)
+                                           weight.numpy(), 1e-4, S["ii"], S["jj"], S["kk"], t0, n, iters)
             assert st == 0
             dpose = np.abs(rp[t0:n] - r["poses"][t0:n]).max()
             ddep = np.abs(rq[touched, 2, 1, 1] - r["depth"]).max()
@@ -585,11 +586,12 @@ def update_step_fixtures(pops, ba, lie, dscale=None, save=True):
     moved = np.abs(res["f64"]["poses"][t0:n] - S["poses"][t0:n]).max()
     print(f"update_step: E = {E}, window poses moved by up to {moved:.3g}; fixture saved")
     if save:
-        np.savez_compressed(os.path.join(HERE, "update_step_ref.npz"), **out)
+        np.savez_compressed(os.path.join(HERE, C["file"]), **out)
 
 
 if __name__ == "__main__":
-    # python make_golden.py [part ...]: parts lietorch, pops, ba, altcorr, neighbors, update, encoder, step
+    # python make_golden.py [part ...]: parts lietorch, pops, ba, altcorr, neighbors, update, encoder, step,
+    # step_c2 (not in the default set: ~10 min of CPU)
     torch.set_num_threads(8)
     parts = set(sys.argv[1:]) or {"lietorch", "pops", "ba", "altcorr", "neighbors", "update", "encoder", "step"}
     pops, ba, lie = import_reference()
@@ -609,3 +611,5 @@ if __name__ == "__main__":
         encoder_fixtures()
     if "step" in parts:
         update_step_fixtures(pops, ba, lie)
+    if "step_c2" in parts:
+        update_step_fixtures(pops, ba, lie, which="c2")

@@ -138,7 +138,13 @@ STEP_DSCALE = 0.25
 # with M = 12 patches per frame, a 48-frame buffer, n = 40 keyframes (the
 # 36-slot feature rings wrap), 128 x 96 frames (32 x 24 feature maps)
 STEP = dict(n=40, M=12, N=48, pmem=36, ht=96, wd=128, lifetime=13, removal=22, opt_window=10,
-            intrinsics=(20.0, 20.0, 16.0, 12.0))
+            intrinsics=(20.0, 20.0, 16.0, 12.0), iters=2, file="update_step_ref.npz")
+# C2's per-update workload (BASELINE.json configs[1]: default.yaml with M = 96,
+# 8 BA iterations): E = 497 M = 47,712 edges in steady state at n = 40, on
+# 512 x 384 frames (128 x 96 feature maps, the tartan intrinsics / 4)
+STEP_C2 = dict(n=40, M=96, N=48, pmem=36, ht=384, wd=512, lifetime=13, removal=22, opt_window=10,
+               intrinsics=(80.0, 80.0, 64.0, 48.0), iters=8, file="update_step_c2_ref.npz", dscale=1.0)
+STEPS = {"small": STEP, "c2": STEP_C2}
 
 
 def _qmul(a, b):
@@ -165,14 +171,14 @@ def step_edges(n, M, lifetime, removal):
     return ii[keep], jj[keep], kk[keep]
 
 
-def update_step_state(seed=STEP_SEED):
+def update_step_state(seed=STEP_SEED, S=None):
     """Every input of one update(): poses [N][7] (rows >= n zero), patches
     [N*M][3][3][3], intrinsics [N][4] (all fp32), the fp16 rings fmap1
     [pmem][128][h][w], fmap2 [pmem][128][h/4][w/4] (4x4 average of fmap1),
     gmap [pmem][M][128][3][3] (3x3 windows of fmap1 at the patch centres, the
     Patchifier's patchify), imap [pmem][M][384], the edges ii / jj / kk and the
-    fp32 edge state net [E][384]."""
-    S = STEP
+    fp32 edge state net [E][384].  S: STEP (default) or STEP_C2."""
+    S = STEP if S is None else S
     n, M, N, pmem = S["n"], S["M"], S["N"], S["pmem"]
     h, w = S["ht"] // 4, S["wd"] // 4
     g = np.random.default_rng(seed)

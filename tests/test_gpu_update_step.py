@@ -8,7 +8,9 @@ net.Update on seeded weights, ba.py twice with the fastba argument mapping
 (checked against the C restatement of ba_cuda.cu in the generator)
 and projective_ops.point_cloud on net_inputs.update_step_state(): default.yaml,
 M = 12, a 48-frame buffer, n = 40 keyframes (the 36-slot rings wrap), 5,964
-edges.  It records two runs:
+edges, 2 BA iterations; and at C2's per-update size (update_step_c2_ref.npz:
+M = 96, 47,712 edges, 8 BA iterations, 512 x 384 frames).  Each records two
+runs:
   * f64: float64 throughout -- the exact answer for these inputs;
   * r16: the reference's own precisions (fp16 altcorr chain, Update under fp16
     autocast, fp32 BA) -- its distance from f64 is the reference's own error.
@@ -43,21 +45,22 @@ import net_inputs as NI  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def _fixture():
-    return np.load(os.path.join(GOLDEN, "update_step_ref.npz"))
+def _fixture(which="small"):
+    return np.load(os.path.join(GOLDEN, NI.STEPS[which]["file"]))
 
 
 def _tracker(f):
     from dpvo.config import make_cfg
     from dpvo.dpvo import DPVO
     from dpvo.net import VONet
-    C = NI.STEP
-    S = NI.update_step_state(int(f["seed"]))
+    C = NI.STEPS[str(f["which"])] if "which" in f else NI.STEP
+    S = NI.update_step_state(int(f["seed"]), C)
     want = f["state_checksum"]
     got = np.stack([NI.checksum(S[k]) for k in sorted(S)])
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)   # the generator's inputs, regenerated
     n, M, N, pmem = C["n"], C["M"], C["N"], C["pmem"]
     cfg = make_cfg("default", BUFFER_SIZE=N, PATCHES_PER_FRAME=M)
+    cfg.BA_ITERATIONS = C["iters"]
     assert (cfg.REMOVAL_WINDOW, cfg.OPTIMIZATION_WINDOW, cfg.PATCH_LIFETIME) == (22, 10, 13)
     net = VONet()
     params = NI.make_params(str(f["spec"]), int(f["update_seed"]))
@@ -97,8 +100,13 @@ def _rms(a, b):
     return float(np.sqrt((d * d).mean()))
 
 
-def test_update_step_matches_reference_modules():
-    f = _fixture()
+@pytest.mark.parametrize("which", ["small", "c2"])
+def test_update_step_matches_reference_modules(which):
+    """small: M = 12, E = 5,964, 2 BA iterations, delta head x 0.25;
+    c2: C2's per-update workload, M = 96, E = 47,712, 8 BA iterations, the
+    delta head unscaled (BA stays out of the clamp regimes: touched inverse
+    depths in [0.11, 1.13] in every iteration of the reference run)"""
+    f = _fixture(which)
     slam, S = _tracker(f)
     n, t0 = int(f["n"]), int(f["t0"])
     m = slam.pg.m
@@ -149,20 +157,21 @@ def test_update_step_matches_reference_modules():
         assert mx <= 3.0 * amx and mx <= caps[k], (k, mx, amx)
 
 
-def test_update_step_corr_rows_match_exact():
+@pytest.mark.parametrize("which", ["small", "c2"])
+def test_update_step_corr_rows_match_exact(which):
     """the tracker's default (matrix-core) altcorr at this state, rows of the
     stacked [E, 882] corr against the exact (fp64-summed) restatement of the
     reference kernel: within the final fp16 rounding (2^-11 relative) plus
     5e-5 (the fp32 accumulation and the fp32-vs-fp64 coordinates)"""
     import update_ops
-    f = _fixture()
+    f = _fixture(which)
     slam, S = _tracker(f)
     with torch.no_grad():
         coords = slam.reproject()
-        ctx, jslot, _, _, order = update_ops.window_group_by(
+        ctx, jslot, _, _ = update_ops.window_group_by(
             slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M, slam.n - 64, slam.M * slam.pmem, slam.pmem,
-            flag=slam._ba_status, jj_order=True)
-        corr = slam.corr(coords, slots=(ctx, jslot), order=order)
+            flag=slam._ba_status)
+        corr = slam.corr(coords, slots=(ctx, jslot))   # the staged kernel, as update() runs it
     torch.cuda.synchronize()
     rows = f["corr_rows"]
     got = corr[0].float().cpu().numpy()[rows].astype(np.float64)

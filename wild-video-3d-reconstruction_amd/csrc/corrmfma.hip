@@ -366,8 +366,8 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
                 for (int lev = 0; lev < 2; lev++) {
                     const int st = lev ? st1 : st0;
                     const float* r0 = rw + lev * RL + q * RS + ebase[wave][lev][q] + ey[i] * st + ex[i];
-                    v[lev] = wts[wave][lev][0][q] * r0[0] + wts[wave][lev][1][q] * r0[1] +
-                             wts[wave][lev][2][q] * r0[st] + wts[wave][lev][3][q] * r0[st + 1];
+                    v[lev] = cm_bilinear(wts[wave][lev][0][q], wts[wave][lev][1][q], wts[wave][lev][2][q],
+                                         wts[wave][lev][3][q], r0[0], r0[1], r0[st], r0[st + 1]);
                 }
                 *(half2_t*)(orow + 2 * t) = half2_t{(half_t)v[0], (half_t)v[1]};
             }

@@ -37,6 +37,16 @@ struct CorrMfmaParams {
     const int* dev_begin;   // optional: visit order slots [*dev_begin, E) only (read on the device)
 };
 
+// The fp32 bilinear 8x8 -> 7x7 step of one output (correlation_kernel.cu:221-232's
+// four terms) as one explicit chain, so every kernel computing it (per-edge
+// and staged) rounds identically whatever the compiler would contract:
+// w = {(1-dx)(1-dy), dx(1-dy), (1-dx)dy, dx dy}, r = the 2 x 2 products
+__device__ __forceinline__ float cm_bilinear(float w0, float w1, float w2, float w3, float r00, float r01, float r10,
+                                             float r11)
+{
+    return __builtin_fmaf(w3, r11, __builtin_fmaf(w2, r10, __builtin_fmaf(w1, r01, w0 * r00)));
+}
+
 // dpvo_corr_pyramid_mfma's argument checks and parameter block (0, or -1 with the error set)
 int corr_mfma_setup(CorrMfmaParams& p, const void* table, int64_t num_patches, const void* const* fmaps,
                     const int64_t* fmap_sizes, const int64_t* fmap_strides, const float* level_scale,

@@ -360,8 +360,8 @@ __global__ __launch_bounds__(cs::THREADS, 1) void corr_stage_kernel(CorrMfmaPara
             const int pos = t / NP, q = t - pos * NP;
             const int exi = pos / DO, eyi = pos - exi * DO;
             const float* r0 = rw + q * RS + ebase[q] + eyi * bw + exi;
-            v[i] = wts[0 * 16 + q] * r0[0] + wts[1 * 16 + q] * r0[1] + wts[2 * 16 + q] * r0[bw] +
-                   wts[3 * 16 + q] * r0[bw + 1];
+            v[i] = cm_bilinear(wts[0 * 16 + q], wts[1 * 16 + q], wts[2 * 16 + q], wts[3 * 16 + q], r0[0], r0[1],
+                               r0[bw], r0[bw + 1]);
         }
     };
 
