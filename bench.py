@@ -245,7 +245,7 @@ def phase_breakdown(slam, reps=5):
         e[0].record()
         coords = slam.reproject()
         e[1].record()
-        want_order = not getattr(slam.cfg, "STAGED_CORR", True)
+        want_order = not getattr(slam.cfg, "STAGED_CORR", False)
         ctx_idx, jslot, kk_groups, ij_groups, *rest = update_ops.window_group_by(
             slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M, slam.n - 64, slam.M * slam.pmem, slam.pmem,
             flag=slam._ba_status, jj_order=want_order)

@@ -491,6 +491,16 @@ typedef struct dpvo_rowadd_args {
 } dpvo_rowadd_args;
 int dpvo_rowadd_ln(const dpvo_rowadd_args* args, void* stream);
 
+/* dpvo_rowgemm_pair whose A rows are formed as they are staged:
+ * A[m] = fp16(pre->a[m] + pre->b16[pre->b_idx[m]]) (fp32 rows a, lda >= 384;
+ * the fp16 addend rows gathered, b_idx out of [0, b_rows) = no addend), which
+ * is dpvo_rowadd_ln(pre with out16)'s arithmetic: the agg_kk row add
+ * (net.py:87) feeding the agg_ij SoftAgg's f and g Linears (:88) without its
+ * fp16 rows going through HBM.  a, b: WKB (k-blocked) with K = 384, no a_idx
+ * (A is ignored); pre: a, lda, M (= a->M), b16, b_idx, b_rows only. */
+int dpvo_rowgemm_pair_pre(const dpvo_rowgemm_args* a, const dpvo_rowgemm_args* b, const dpvo_rowadd_args* pre,
+                          void* stream);
+
 /* The tracker's per-update edge keys in one launch (DPVO.update / DPVO.corr,
  * dpvo.py:326-327,718 and the SoftAgg group keys of net.py:86-88):
  * key_kk[e] = kk[e] - M base, key_ij[e] = (ii[e] - base) * 64 + (jj[e] - base),

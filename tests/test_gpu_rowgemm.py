@@ -397,3 +397,27 @@ def test_update_operator_corr_chain3_is_two_launches():
     Update.CORR_CHAIN3 = True
     (a, (da, wa, _)), (b, (db, wb, _)) = outs
     assert torch.equal(a, b) and torch.equal(da, db) and torch.equal(wa, wb)
+
+
+@pytest.mark.parametrize("M", [1, 300, 20000])
+def test_rowgemm_pair_pre_equals_rowadd_then_pair(M):
+    """dpvo_rowgemm_pair_pre (A rows fp16(a32 + b16[idx]) formed while staged)
+    is bit-identical to rowadd_ln(a32, b16, idx, want32=False) feeding
+    rowgemm_pair, including out-of-range indices (no addend) and rows past M."""
+    import update_ops as U
+    g = torch.Generator().manual_seed(M)
+    a32 = torch.randn(M, D, generator=g).cuda()
+    G = max(M // 20, 1)
+    b16 = torch.randn(G + 3, D, generator=g).half().cuda()
+    idx = torch.randint(0, G, (M,), generator=g)
+    idx[::17] = -1                      # no addend
+    idx[5::23] = G + 7                  # beyond b_rows: no addend
+    idx = idx.cuda()
+    (wf, bf), (wg, bg) = lin(D, 1), lin(D, 2)
+    Wf, cf = U.pack_linear(wf, bf)
+    Wg, cg = U.pack_linear(wg, bg)
+    Wf, Wg = U.kblock(Wf), U.kblock(Wg)
+    _, n16 = U.rowadd_ln(a32, b16[:G], idx, want32=False)
+    f_ref, g_ref = U.rowgemm_pair(n16, Wf, cf, Wg, cg)
+    f, gg = U.rowgemm_pair_pre(a32, b16, idx, Wf, cf, Wg, cg, b_rows=G)
+    assert torch.equal(f, f_ref) and torch.equal(gg, g_ref)

@@ -168,10 +168,14 @@ def test_update_step_corr_rows_match_exact(which):
     slam, S = _tracker(f)
     with torch.no_grad():
         coords = slam.reproject()
-        ctx, jslot, _, _ = update_ops.window_group_by(
+        ctx, jslot, _, _, order = update_ops.window_group_by(
             slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M, slam.n - 64, slam.M * slam.pmem, slam.pmem,
-            flag=slam._ba_status)
-        corr = slam.corr(coords, slots=(ctx, jslot))   # the staged kernel, as update() runs it
+            flag=slam._ba_status, jj_order=True)
+        corr = slam.corr(coords, slots=(ctx, jslot), order=order)
+        slam.cfg.STAGED_CORR = True
+        staged = slam.corr(coords, slots=(ctx, jslot)).clone()   # the LDS-staged kernel: the same bits
+        slam.cfg.STAGED_CORR = False
+        assert torch.equal(staged, corr)
     torch.cuda.synchronize()
     rows = f["corr_rows"]
     got = corr[0].float().cpu().numpy()[rows].astype(np.float64)

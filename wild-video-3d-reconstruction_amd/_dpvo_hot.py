@@ -85,6 +85,7 @@ _SIGNATURES = {
     "dpvo_scatter_csr": (_ip, [_ip, _ip, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _fp, _vp, _i64, _vp, _vp]),
     "dpvo_rowgemm": (_ip, [_vp, _vp]),
     "dpvo_rowgemm_pair": (_ip, [_vp, _vp, _vp]),
+    "dpvo_rowgemm_pair_pre": (_ip, [_vp, _vp, _vp, _vp]),
     "dpvo_rowchain": (_ip, [_vp, _vp, _vp]),
     "dpvo_rowchain3": (_ip, [_vp, _vp, _vp, _vp]),
     "dpvo_rowchain_gated": (_ip, [_vp, _vp, _vp, _vp]),

@@ -44,7 +44,12 @@ struct CorrMfmaParams {
 __device__ __forceinline__ float cm_bilinear(float w0, float w1, float w2, float w3, float r00, float r01, float r10,
                                              float r11)
 {
-    return __builtin_fmaf(w3, r11, __builtin_fmaf(w2, r10, __builtin_fmaf(w1, r01, w0 * r00)));
+    float v = __builtin_fmaf(w3, r11, __builtin_fmaf(w2, r10, __builtin_fmaf(w1, r01, w0 * r00)));
+    // an fp32 value, rounded to fp16 by the caller's conversion: without this
+    // the compiler may fuse the last fma into the conversion (v_fma_mix*_f16:
+    // one rounding instead of two -- other bits than the per-edge kernel's)
+    asm volatile("" : "+v"(v));
+    return v;
 }
 
 // dpvo_corr_pyramid_mfma's argument checks and parameter block (0, or -1 with the error set)

@@ -566,8 +566,32 @@ struct R5Cursor {
     }
 };
 
-template <int FLAGS, bool DUAL>
-__global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_args p, dpvo_rowgemm_args p2)
+// PRE (dpvo_rowgemm_pair_pre): the A rows are formed while they are staged,
+// A[m] = fp16(pre.a[m] + pre.b16[pre.b_idx[m]]) -- rowadd_ln's fp32 add and
+// rounding (net + agg_kk(net), net.py:87 -> the agg_ij SoftAgg's f / g
+// operand) without its 73 MB fp16 rows round-tripping HBM.
+struct R5PreRaw {
+    f4_t lo, hi;   // 8 fp32 of pre.a
+    h8_t b;        // 8 fp16 of the gathered addend
+    bool add;      // the row has an addend (else v = a, as rowadd_ln: a + 0 would turn -0 into +0)
+};
+template <bool PRE>
+using r5_areg_t = std::conditional_t<PRE, R5PreRaw, h8_t>;
+__device__ __forceinline__ h8_t r5_cvt(const h8_t& x) { return x; }
+__device__ __forceinline__ h8_t r5_cvt(const R5PreRaw& x)
+{
+    h8_t y;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        y[i] = (half_t)(x.add ? x.lo[i] + (float)x.b[i] : x.lo[i]);
+        y[4 + i] = (half_t)(x.add ? x.hi[i] + (float)x.b[4 + i] : x.hi[i]);
+    }
+    return y;
+}
+
+template <int FLAGS, bool DUAL, bool PRE = false>
+__global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_args p, dpvo_rowgemm_args p2,
+                                                                 dpvo_rowadd_args pre)
 {
     static_assert((FLAGS & ~(RG_RELU | RG_SIGMOID)) == 0, "v5: plain GEMMs only");
     __shared__ __attribute__((aligned(16))) char smem[R5_LDS];
@@ -588,21 +612,44 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     const int ar = 16 * w + (lane >> 2), ac = lane & 3;
     int64_t a_tile = -1;
     const half_t* arow = zero;
+    const float* arow32 = nullptr;   // PRE
+    bool aadd = false;               // PRE: this lane's row has an addend
     auto a_row = [&](int64_t t) __attribute__((always_inline)) {
         if (t == a_tile) return;
         a_tile = t;
         const int64_t m = t * RG_BM + ar;
-        const half_t* row = zero;
-        if (m < Mrows) {
-            const int64_t src = p.a_idx ? p.a_idx[m] : m;
-            if (src >= 0 && src < p.a_rows) row = (const half_t*)p.A + src * p.lda;
+        if constexpr (PRE) {
+            // rows past M read row 0 (finite; their outputs are never stored)
+            arow32 = (const float*)pre.a + (m < Mrows ? m : 0) * pre.lda + 8 * ac;
+            const half_t* b = zero;
+            if (m < Mrows && pre.b16) {
+                const int64_t s = pre.b_idx ? pre.b_idx[m] : m;
+                if (s >= 0 && s < pre.b_rows) b = (const half_t*)pre.b16 + s * RG_BN;
+            }
+            aadd = b != zero;
+            arow = b + 8 * ac;
+        } else {
+            const half_t* row = zero;
+            if (m < Mrows) {
+                const int64_t src = p.a_idx ? p.a_idx[m] : m;
+                if (src >= 0 && src < p.a_rows) row = (const half_t*)p.A + src * p.lda;
+            }
+            arow = row + 8 * ac;
         }
-        arow = row + 8 * ac;
     };
-    h8_t areg[2];
-    auto load_a = [&](const R5Cursor& c) __attribute__((always_inline)) -> h8_t {
+    r5_areg_t<PRE> areg[2];
+    auto load_a = [&](const R5Cursor& c) __attribute__((always_inline)) -> r5_areg_t<PRE> {
         a_row(c.t);
-        return *(const h8_t*)(arow + c.k * R5_BK);
+        if constexpr (PRE) {
+            R5PreRaw x;
+            x.lo = *(const f4_t*)(arow32 + c.k * R5_BK);
+            x.hi = *(const f4_t*)(arow32 + c.k * R5_BK + 4);
+            x.b = *(const h8_t*)(arow + c.k * R5_BK);
+            x.add = aadd;
+            return x;
+        } else {
+            return *(const h8_t*)(arow + c.k * R5_BK);
+        }
     };
     // slot image: row r, physical chunk ac ^ rc_sw(r) holds logical chunk ac
     const int aw_off = ar * 64 + 16 * (ac ^ rc_sw(ar));
@@ -696,7 +743,7 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     }
 #pragma unroll
     for (int r = 0; r < 2; r++) {
-        const h8_t x = load_a(ca);
+        const h8_t x = r5_cvt(load_a(ca));
         *(h8_t*)(smem + R5_Y + r * R5_ASLOT + aw_off) = x;
         ca.next(total, nks, NP, G);
     }
@@ -743,8 +790,8 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
         load_w(cw, wreg[PR]);                                                  // W stage f + 2
         cw.next(total, nks, NP, G);
         __builtin_amdgcn_sched_barrier(0);
-        *(h8_t*)(smem + R5_Y + ((PH + 2) & 3) * R5_ASLOT + aw_off) = areg[PR];   // stage f + 2
-        areg[PR] = load_a(ca);                                                 // stage f + 4
+        *(h8_t*)(smem + R5_Y + ((PH + 2) & 3) * R5_ASLOT + aw_off) = r5_cvt(areg[PR]);   // stage f + 2
+        areg[PR] = load_a(ca);                                                         // stage f + 4
         ca.next(total, nks, NP, G);
         RC_STAMP(s3)
         RC_ACC(0, s0, s1) RC_ACC(1, s1, s2) RC_ACC(2, s2, s3)
@@ -1293,9 +1340,34 @@ extern "C" int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_
     const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
     const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
     if (a->flags & DPVO_RG_WKB)
-        hipLaunchKernelGGL((rowgemm5_kernel<0, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b);
+        hipLaunchKernelGGL((rowgemm5_kernel<0, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b,
+                           dpvo_rowadd_args{});
     else
         hipLaunchKernelGGL((rowgemm3_kernel<0, true>), dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, *b);
+    DPVO_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" int dpvo_rowgemm_pair_pre(const dpvo_rowgemm_args* a, const dpvo_rowgemm_args* b,
+                                     const dpvo_rowadd_args* pre, void* stream)
+{
+    DPVO_CHECK_ARG(pre != nullptr && pre->a != nullptr && !pre->a_f16 && pre->lda >= 384 && pre->lda % 4 == 0 &&
+                       ((uintptr_t)pre->a & 15) == 0,
+                   "rowgemm_pair_pre: pre.a must be fp32 rows of >= 384 (16-byte aligned)");
+    DPVO_CHECK_ARG(!pre->b16 || ((uintptr_t)pre->b16 & 15) == 0, "rowgemm_pair_pre: pre.b16 must be 16-byte aligned");
+    DPVO_CHECK_ARG(!pre->ln_g && !pre->c16 && !pre->out32 && !pre->out16,
+                   "rowgemm_pair_pre: pre is the row add only (no LayerNorm, second addend or outputs)");
+    if (validate_rowgemm(a) || validate_rowgemm(b)) return -1;
+    DPVO_CHECK_ARG(a->flags == DPVO_RG_WKB && b->flags == DPVO_RG_WKB, "rowgemm_pair_pre: k-blocked W on both");
+    DPVO_CHECK_ARG(a->K == 384 && b->K == 384 && a->M == b->M && a->M == pre->M && a->M_dev == b->M_dev &&
+                       !a->a_idx && !b->a_idx,
+                   "rowgemm_pair_pre: K = 384, one M, no row gather (the rows are pre's)");
+    if (a->M <= 0) return 0;
+    if (ensure_num_cus()) return -1;
+    const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
+    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+    hipLaunchKernelGGL((rowgemm5_kernel<0, true, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b,
+                       *pre);
     DPVO_CHECK_LAUNCH();
     return 0;
 }
@@ -1312,7 +1384,7 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
 #define R5_CASE(F)                                                                                                  \
     case (F) | DPVO_RG_WKB:                                                                                         \
         hipLaunchKernelGGL((rowgemm5_kernel<(F), false>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, \
-                           *a);                                                                                     \
+                           *a, dpvo_rowadd_args{});                                                                 \
         break;
         R5_CASE(0)
         R5_CASE(DPVO_RG_RELU)

@@ -202,10 +202,9 @@ class DPVO:
             out = buf[:E, :CORR_DIM].unsqueeze(0)
             if not getattr(self.cfg, "EXACT_CORR", False) and getattr(self.cfg, "CHANNEL_LAST_FMAPS", True):
                 # matrix cores, fp32 accumulation (csrc/corrmfma.hip)
-                if getattr(self.cfg, "STAGED_CORR", True):
+                if getattr(self.cfg, "STAGED_CORR", False) and self._staged_ok(E):
                     # the same rows with each (target frame, 8x8 cell)'s windows
                     # staged in LDS once for all of its edges (csrc/corrstage.hip)
-                    self._corr_ws = cuda_corr.staged_workspace(E, self.pyramid, getattr(self, "_corr_ws", None))
                     return altcorr.corr_pyramid_staged(self._gmap_table(mfma=True), self.gmap.shape[1], self.pyramid,
                                                        coords, ii1, jj1, out=out,
                                                        workspace=self._corr_ws).view(1, E, -1)
@@ -217,6 +216,16 @@ class DPVO:
             table = self._gmap_table()
         return altcorr.corr_pyramid(self.gmap, self.pyramid, coords, ii1, jj1, 3, (1, 4), out=out,
                                     table=table).view(1, E, -1)
+
+    def _staged_ok(self, E):
+        """the staged kernel's workspace for E edges (cached); False when its
+        (frame, cell) bins would not fit it (rings far larger than the
+        tracker's 36 frames): DPVO.corr then runs the per-edge kernel"""
+        try:
+            self._corr_ws = cuda_corr.staged_workspace(E, self.pyramid, getattr(self, "_corr_ws", None))
+            return True
+        except RuntimeError:
+            return False
 
     def _gmap_table(self, mfma=False):
         """The gmap ring packed for altcorr (the exact kernel's scalar-operand
@@ -436,7 +445,7 @@ class DPVO:
                 # (+ the edges grouped by target frame: altcorr's visiting order)
                 # (the per-edge matrix-core altcorr's visiting order only when it
                 # runs: the staged kernel bins the edges itself)
-                want_order = not getattr(self.cfg, "STAGED_CORR", True)
+                want_order = not getattr(self.cfg, "STAGED_CORR", False)
                 ctx_idx, jslot, kk_groups, ij_groups, *rest = update_ops.window_group_by(
                     self.pg.ii, self.pg.jj, self.pg.kk, self.M, self.n - 64, self.M * self.pmem, self.pmem,
                     flag=self._ba_status if defer else self._ba_fail, jj_order=want_order)

@@ -39,6 +39,7 @@ class Update(nn.Module):
 
     FUSED = True  # inference under fp16 autocast runs the fused HIP path (class-level switch for A/B tests)
     CORR_CHAIN3 = True  # the corr MLP + first LayerNorm as one three-GEMM launch (False: two launches)
+    FUSE_AGG_ADD = True  # the agg_kk row add inside agg_ij's f / g launch (False: a rowadd_ln pass; same bits)
 
     # ------------------------------------------------------------ fused path
     def _packed(self):
@@ -129,14 +130,21 @@ class Update(nn.Module):
                 gid, offs, perm, G = ij_groups
             else:
                 gid, offs, perm, G = U.group_by(ii * 12345 + jj, key_bits=ij_bits)
-            f16, g16 = U.rowgemm_pair(n16, *pf, *pg_)
+            if kk_add is not None and self.FUSE_AGG_ADD:
+                # the agg_kk row add formed as the f / g GEMMs stage their A rows
+                # (the fp16 rows of net + agg_kk(net) never reach HBM)
+                f16, g16 = U.rowgemm_pair_pre(n32, *kk_add, *pf, *pg_)
+            else:
+                f16, g16 = U.rowgemm_pair(n16, *pf, *pg_)
             # frame-pair groups are few and long (~190 edges at C3): split over waves
             y = U.softagg_csr(f16, g16, offs, perm, G, E, long_groups=ij)
             _, hy, _ = U.rowgemm(y, *ph, M_dev=G)
             if kk_add is None:
                 # net + agg_kk(net): only its fp16 rows (agg_ij's GEMM operand) are
-                # stored; the fp32 sum is recomputed by the next add, in order
-                _, n16 = U.rowadd_ln(n32, hy, gid, want32=False)
+                # stored -- or none (FUSE_AGG_ADD); the fp32 sum is recomputed by
+                # the next add, in order
+                if not self.FUSE_AGG_ADD:
+                    _, n16 = U.rowadd_ln(n32, hy, gid, want32=False)
                 kk_add = (hy, gid)
             else:
                 n32, n16 = U.rowadd_ln(n32, *kk_add, c16=hy, c_idx=gid, ln=ln)

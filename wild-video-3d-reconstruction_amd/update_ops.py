@@ -451,6 +451,40 @@ def rowgemm_pair(A, Wa, ba, Wb, bb, M_dev=None):
     return outs[0], outs[1]
 
 
+def rowgemm_pair_pre(a32, b16, b_idx, Wa, ba, Wb, bb, b_rows=None):
+    """rowgemm_pair(rowadd_ln(a32, b16, b_idx, want32=False)[1], Wa, ba, Wb, bb)
+    in one launch (dpvo_rowgemm_pair_pre): the A rows fp16(a32 + b16[b_idx])
+    are formed as the GEMM stages them -- the same bits, without the fp16 rows
+    in HBM.  Wa / Wb k-blocked [12, 384, 32] (K = 384)."""
+    H.on_gpu(a32, b16, b_idx, Wa, ba, Wb, bb)
+    if a32.dtype != torch.float32 or a32.dim() != 2 or a32.shape[1] != WIDTH or a32.stride(1) != 1:
+        raise RuntimeError("rowgemm_pair_pre: a32 must be fp32 [M, 384] row-contiguous")
+    if b16.dtype != torch.float16 or b16.dim() != 2 or b16.shape[1] != WIDTH or not b16.is_contiguous():
+        raise RuntimeError("rowgemm_pair_pre: b16 must be fp16 [G, 384] contiguous")
+    if b_idx.dtype != torch.int64 or b_idx.numel() < a32.shape[0]:
+        raise RuntimeError("rowgemm_pair_pre: b_idx must be int64 with one entry per row")
+    if any(t.dtype != torch.float16 for t in (Wa, ba, Wb, bb)) or Wa.dim() != 3 or Wb.shape != Wa.shape:
+        raise RuntimeError("rowgemm_pair_pre: k-blocked fp16 weights and fp16 biases")
+    Kp = _kb_K(Wa)
+    M, dev = a32.shape[0], a32.device
+    outs, args = [], []
+    for W, b in ((Wa, ba), (Wb, bb)):
+        o = torch.empty(M, WIDTH, dtype=torch.float16, device=dev)
+        a = RowGemmArgs()
+        z = _p(zero_row(dev, Kp))
+        a.A, a.lda, a.a_idx, a.a_rows = z, Kp, None, M   # (A unused: the rows are pre's)
+        a.W, a.K, a.N, a.bias, a.zero_row = _p(W), Kp, WIDTH, _p(b), z
+        a.M, a.flags = M, WKB
+        a.out16, a.ldo16 = _p(o), o.stride(0)
+        outs.append(o)
+        args.append(a)
+    pre = RowAddArgs()
+    pre.a, pre.a_f16, pre.lda, pre.M = _p(a32), 0, a32.stride(0), M
+    pre.b16, pre.b_idx, pre.b_rows = _p(b16), _p(b_idx), b16.shape[0] if b_rows is None else b_rows
+    H.check(H.lib().dpvo_rowgemm_pair_pre(_ct.byref(args[0]), _ct.byref(args[1]), _ct.byref(pre), H.stream_of(a32)))
+    return outs[0], outs[1]
+
+
 def rowadd_ln(a, b16=None, b_idx=None, ln=None, want32=True, want16=True, c16=None, c_idx=None):
     """v = a (+ b16[b_idx]) (+ c16[c_idx]) [-> LayerNorm] over 384-wide rows ->
     (out32, out16).  The second addend is the next row add, in order: one call
