@@ -1,0 +1,54 @@
+"""Where the c1 / c2 chain's time goes (rowchain5_kernel<RES>, csrc/rowgemm.hip,
+DPVO_STAMPS build in diag/libdpvo_hot.so): per tile, cycles in the GEMM1
+k-loop (with the previous tile's residual epilogue overlapped), the GEMM1 ->
+y tile write, GEMM2, the y-tile write, at C3 shapes (E = 95,424 gathered rows)."""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["DPVO_HOT_LIB"] = os.path.join(REPO, "diag", "libdpvo_hot.so")
+os.environ["DPVO_DIAG"] = "1"   # the loader refuses the stamps build otherwise
+sys.path.insert(0, os.path.join(REPO, "wild-video-3d-reconstruction_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import _dpvo_hot as H  # noqa: E402
+import update_ops as U  # noqa: E402
+
+
+def main(E=95424):
+    g = torch.Generator(device="cuda").manual_seed(0)
+    n16 = (0.5 * torch.randn(E, 384, generator=g, device="cuda")).half()
+    n32 = torch.randn(E, 384, generator=g, device="cuda")
+    nb = torch.randint(-1, E, (E,), generator=g, device="cuda")
+    W = [U.kblock((torch.randn(384, 384, generator=g, device="cuda") / 20).half()) for _ in range(2)]
+    b = torch.zeros(384, device="cuda").half()
+    for _ in range(3):
+        U.rowchain(n16, W[0], b, W[1], b, flags1=U.RELU, a_idx=nb, flags=U.RES, res32=n32, want32=True)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(10):
+        U.rowchain(n16, W[0], b, W[1], b, flags1=U.RELU, a_idx=nb, flags=U.RES, res32=n32, want32=True)
+    ev[1].record()
+    torch.cuda.synchronize()
+    print(f"chain: {ev[0].elapsed_time(ev[1]) / 10 * 1e3:.1f} us per launch (stamps inflate it)")
+    buf = np.zeros(1024 * 8 * 16, np.uint64)
+    lib = H.lib()
+    lib.dpvo_diag_stamps.restype = ctypes.c_int
+    lib.dpvo_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    assert lib.dpvo_diag_stamps(buf.ctypes.data, buf.nbytes) == 0
+    nblk = min((E + 127) // 128, torch.cuda.get_device_properties(0).multi_processor_count)
+    st = buf.reshape(1024, 8, 16)[:nblk].astype(np.float64)
+    tiles = st[:, 0, 11]
+    print(f"{nblk} blocks, tiles / block {tiles.mean():.2f} (max {tiles.max():.0f})")
+    names = {0: "GEMM1 k-loop (+ OVL epilogue)", 1: "GEMM1 acc -> y tile + sync", 2: "GEMM2 + sync",
+             3: "GEMM2 + y-tile write + sync", 4: "row epilogue (non-OVL)", 10: "total"}
+    for k, n in names.items():
+        per = st[:, :, k].sum(0) / tiles.sum() if k != 10 else st[:, :, k].mean(0)
+        print(f"  {n:32s} {per.mean():10.0f} cycles {'per tile' if k != 10 else 'per wave'}  (waves {np.round(per)})")
+
+
+if __name__ == "__main__":
+    main()

@@ -1077,7 +1077,18 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
         anext();
     }
     int64_t etile = -1;   // OVL: the tile whose row epilogue is still pending
+#ifdef DPVO_STAMPS
+    // chain segments: 0 GEMM1 k-loop (+ OVL epilogue), 1 GEMM1 -> y tile + sync,
+    // 2 GEMM2 (+ TRI: mid rows + GEMM3) + syncs, 3 y-tile write (+ gate pass) + sync,
+    // 4 row epilogue (non-OVL / last tile), 10 total, 11 tiles
+    unsigned long long st_sum[ST_SEGS] = {};
+    RC_STAMP(c_begin)
+#endif
     for (int64_t tile = bid; tile < ntiles; tile += G) {
+#ifdef DPVO_STAMPS
+        RC_STAMP(c0)
+        st_sum[11] += 1;
+#endif
         const bool more = tile + G < ntiles;
         // ---- GEMM1 (+ OVL: the previous tile's row epilogue, rows 16 w .. 16 w + 15
         // in 8 batches of 2: batch b's loads after k-step L(b) = b (nk1 - 3) / 7,
@@ -1110,8 +1121,14 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
             }
         }
         etile = -1;
+#ifdef DPVO_STAMPS
+        RC_STAMP(c1)
+#endif
         acc_to_y(0, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
         sync();
+#ifdef DPVO_STAMPS
+        RC_STAMP(c2)
+#endif
         gemm_y();
         sync();   // every wave is done reading the y tile
         if (TRI) {
@@ -1123,6 +1140,10 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
             sync();
             acc_to_y(2, F2 & RG_RELU, F2 & RG_SIGMOID);
         } else {
+#ifdef DPVO_STAMPS
+            RC_STAMP(c3t)
+            RC_ACC(2, c2, c3t)
+#endif
             acc_to_y(1, F2 & RG_RELU, F2 & RG_SIGMOID);
         }
         if (GATED) {
@@ -1151,6 +1172,10 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
             }
         }
         sync();
+#ifdef DPVO_STAMPS
+        RC_STAMP(c4)
+        RC_ACC(0, c0, c1) RC_ACC(1, c1, c2) RC_ACC(3, c2, c4)
+#endif
         if (OVL && more && nk1 >= 12) {   // (12 k-steps fit the 8 batches' schedule)
             etile = tile;   // runs inside the next tile's GEMM1
             continue;
@@ -1177,7 +1202,17 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
                 epi_done(tile, 16 * w + 4 * b, kc, st[b & 1]);
             });
         }
+#ifdef DPVO_STAMPS
+        RC_STAMP(c5)
+        RC_ACC(4, c4, c5)
+#endif
     }
+#ifdef DPVO_STAMPS
+    RC_STAMP(c_end)
+    st_sum[10] += c_end - c_begin;
+    if (lane == 0)
+        for (int k = 0; k < ST_SEGS; k++) dpvo_stamps[((int64_t)blockIdx.x * 8 + w) * ST_SEGS + k] = st_sum[k];
+#endif
 }
 
 // v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16
