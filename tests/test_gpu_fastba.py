@@ -186,6 +186,25 @@ def test_ba_bitwise_repeatable(iters):
     assert_close_rel(runs[0][1][:, 2], qa[:, 2])
 
 
+@pytest.mark.parametrize("M,iters", [(96, 2), (96, 8), (200, 2)])
+def test_ba_partial_last_round_matches_oracle(M, iters):
+    """Patch counts just past a multiple of the 2,048 resident waves (2,112
+    and 4,400 patches: a last round of 64 / 304 patches, most slots of the
+    final flush empty) match the oracle, bit-repeatably."""
+    st = synth_dpvo_state(5, n=60, M=M)
+    G = len(np.unique(st["kk"]))
+    assert 0 < G % 2048 <= 512, G
+    n = st["n"]
+    gp, gq = _ba_run(st, n - 10, n, iters)
+    rp, rq, status = oracle.ba_forward(st["poses"], st["patches"], st["intrinsics"], st["target"], st["weight"],
+                                       1e-4, st["ii"], st["jj"], st["kk"], n - 10, n, iters)
+    assert status == 0
+    assert_close_rel(gp, rp)
+    assert_close_rel(gq[:, 2], rq[:, 2])
+    again = _ba_run(st, n - 10, n, iters)
+    assert np.array_equal(again[0], gp) and np.array_equal(again[1], gq)
+
+
 def test_ba_mixed_frames_and_repeated_targets():
     """Outside DPVO's edge rules: edges of one patch from different frames i,
     and the same (patch, target) pair twice -- the lane-by-lane fallback of

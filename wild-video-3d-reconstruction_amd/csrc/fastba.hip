@@ -1829,14 +1829,22 @@ __device__ __forceinline__ void bd_jterms_add(const BdEdge& o, float* part, floa
 }
 
 // The Schur term  H -= sum_k Q_k e_k e_k^T,  g -= sum_k Q_k u_k e_k  over a
-// workgroup's patches: every wave parks its patch's E row and Q_k, Q_k u_k in
-// a slot of the workgroup's list (slot = wave + BD_WAVES * its local
-// iteration: a fixed order), and at a flush every thread owns upper-triangle
-// entries of the partial and sums the listed patches' products into them in
-// slot order -- a rank-BD_SLOTS update with plain LDS reads, no atomics.
+// workgroup's patches: every wave parks its patch's E row, Q_k E row and
+// Q_k u_k in a slot of the workgroup's list (slot = wave + BD_WAVES * its
+// local iteration: a fixed order), and at a flush every thread owns
+// upper-triangle entries of the partial and sums the listed patches' products
+// into them in slot order -- a rank-BD_SLOTS update with plain LDS reads, no
+// atomics.  Every entry is a sum of a[s] * b[s] over the slots (Hessian entry
+// (r, c): (Q e)[r] * e[c]; gradient entry r: (Q u) * e[r]), so a thread takes
+// its entries BD_FLUSH_J at a time, two LDS reads per entry and slot with the
+// reads of the BD_FLUSH_J independent sums in flight together (one entry at a
+// time, the sum's dependence left the reads' latency exposed: ~14k cycles per
+// flush at C2, 6k now).
 constexpr int BD_SLOT_IT = 8;                     // wave iterations per flush
 constexpr int BD_SLOTS = BD_SLOT_IT * BD_WAVES;   // listed patches per flush
-constexpr int BD_SLOT_LD = BD_N6MAX + 2;          // E row, Q, Q u
+constexpr int BD_SLOT_LD = 2 * BD_N6MAX + 2;      // E row, Q E row, Q u, pad
+constexpr int BD_SLOT_QE = BD_N6MAX, BD_SLOT_QU = 2 * BD_N6MAX;
+constexpr int BD_FLUSH_J = 4;
 static_assert(BD_SLOTS * BD_SLOT_LD % 4 == 0, "slot list zeroed in 16-byte stores");
 
 // Once per call: the edge data the patch kernel needs, gathered into CSR
@@ -1927,7 +1935,11 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         const int64_t g = it * stride + (int64_t)blockIdx.x * BD_WAVES + wave;
         const int sit = (int)(it % BD_SLOT_IT);
         float* slot = slots + (sit * BD_WAVES + wave) * BD_SLOT_LD;
-        if (pose_terms && lane == 0) slot[BD_N6MAX] = slot[BD_N6MAX + 1] = 0.f;   // empty until filled
+        if (pose_terms) {   // empty until filled (Q e = 0, Q u = 0)
+            if (lane < n6) slot[BD_SLOT_QE + lane] = 0.f;
+            if (lane + 64 < n6) slot[BD_SLOT_QE + 64 + lane] = 0.f;
+            if (lane == 0) slot[BD_SLOT_QU] = 0.f;
+        }
         BD_STAMP(ti0)
         if (g < G) do {
         const bd_i4v gr = p.grec[g];
@@ -2052,12 +2064,15 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         if (lane == 0) { p.Cg[g] = Ck; p.ug[g] = uk; }
         // the Schur term goes through the workgroup's slot list (flushed below)
         const float Q = 1.0f / (Ck + lm);
-        if (lane < n6) slot[lane] = e0;
-        if (lane + 64 < n6) slot[lane + 64] = e1;
-        if (lane == 0) {
-            slot[BD_N6MAX] = Q;
-            slot[BD_N6MAX + 1] = Q * uk;
+        if (lane < n6) {
+            slot[lane] = e0;
+            slot[BD_SLOT_QE + lane] = Q * e0;
         }
+        if (lane + 64 < n6) {
+            slot[lane + 64] = e1;
+            slot[BD_SLOT_QE + 64 + lane] = Q * e1;
+        }
+        if (lane == 0) slot[BD_SLOT_QU] = Q * uk;
         wave_lds_fence();
         BD_STAMP(ti3)
         BD_ACC(6, ti2, ti3)
@@ -2065,27 +2080,29 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
         BD_STAMP(tf0)
         if (pose_terms && (sit == BD_SLOT_IT - 1 || it == niter - 1)) {
             // flush: H_k -= sum_s (Q_s e_s[r]) e_s[c], g_r -= sum_s (Q u)_s e_s[r],
-            // slots in order, into wave 0's partial (one thread per entry)
+            // slots in order, into wave 0's partial
             __syncthreads();
             const int ns = (sit + 1) * BD_WAVES;
-            {
-                for (int kx = threadIdx.x; kx < ent; kx += blockDim.x) {
-                    float acc = sm[kx];
-                    if (kx < nup) {
-                        const int rc = tri_rc[kx], r = rc & 255, c = rc >> 8;
-                        for (int q = 0; q < ns; q++) {
-                            const float* sl = slots + q * BD_SLOT_LD;
-                            acc -= (sl[BD_N6MAX] * sl[r]) * sl[c];
-                        }
-                    } else {
-                        const int r = kx - nup;
-                        for (int q = 0; q < ns; q++) {
-                            const float* sl = slots + q * BD_SLOT_LD;
-                            acc -= sl[BD_N6MAX + 1] * sl[r];
-                        }
-                    }
-                    sm[kx] = acc;
+            for (int k0 = threadIdx.x; k0 < ent; k0 += BD_FLUSH_J * (int)blockDim.x) {
+                float acc[BD_FLUSH_J];
+                int oa[BD_FLUSH_J], ob[BD_FLUSH_J];
+#pragma unroll
+                for (int j = 0; j < BD_FLUSH_J; j++) {
+                    const int kx = k0 + j * (int)blockDim.x;
+                    const int rc = kx < nup ? tri_rc[kx] : 0;
+                    oa[j] = kx < nup ? BD_SLOT_QE + (rc & 255) : BD_SLOT_QU;
+                    ob[j] = kx < nup ? rc >> 8 : kx - nup;
+                    if (kx >= ent) oa[j] = ob[j] = 0;   // (a pass past the end: read, never stored)
+                    acc[j] = kx < ent ? sm[kx] : 0.f;
                 }
+                for (int q = 0; q < ns; q++) {
+                    const float* sl = slots + q * BD_SLOT_LD;
+#pragma unroll
+                    for (int j = 0; j < BD_FLUSH_J; j++) acc[j] -= sl[oa[j]] * sl[ob[j]];
+                }
+#pragma unroll
+                for (int j = 0; j < BD_FLUSH_J; j++)
+                    if (k0 + j * (int)blockDim.x < ent) sm[k0 + j * (int)blockDim.x] = acc[j];
             }
             __syncthreads();
         }
