@@ -853,7 +853,11 @@ struct R5WCursor {   // (tile, segment, k-step) of the flat W-step sequence
     }
 };
 
-template <int F2, bool GATED = false, int FMID = 0>
+// F1: GEMM1's activation as a compile-time constant (RG_RELU: every chain of
+// the update operator), or -1 to read it from p1.flags.  With the runtime
+// flags the y-tile conversion evaluates the sigmoid (exp + rcp per element)
+// beside the ReLU and selects: ~10k cycles per tile, an eighth of a c1 tile.
+template <int F2, bool GATED = false, int FMID = 0, int F1 = -1>
 __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
                                                                   dpvo_rowgemm_args pg)
 {
@@ -1124,7 +1128,10 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
 #ifdef DPVO_STAMPS
         RC_STAMP(c1)
 #endif
-        acc_to_y(0, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
+        if constexpr (F1 >= 0)
+            acc_to_y(0, (F1 & RG_RELU) != 0, (F1 & RG_SIGMOID) != 0);
+        else
+            acc_to_y(0, p1.flags & RG_RELU, p1.flags & RG_SIGMOID);
         sync();
 #ifdef DPVO_STAMPS
         RC_STAMP(c2)
@@ -1483,6 +1490,7 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
     dpvo_rowgemm_args a2 = *g2;
     a2.M = g1->M;
     a2.M_dev = g1->M_dev;
+    const bool relu1 = g1->flags == DPVO_RG_RELU;   // (the compile-time activation)
     if (gate) {
         // the gated y goes through the RES epilogue (res16 none): x + fp16(gate * y)
         a2.gate16 = nullptr;
@@ -1490,8 +1498,12 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
         switch (f) {
 #define RCG_CASE(F)                                                                                                   \
     case (F):                                                                                                         \
-        hipLaunchKernelGGL((rowchain5_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES, true>), dim3(grid), dim3(R5_THREADS), \
-                           0, as_stream(stream), *g1, a2, *gate);                                                     \
+        if (relu1)                                                                                                    \
+            hipLaunchKernelGGL((rowchain5_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES, true, 0, RG_RELU>), dim3(grid), \
+                               dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, *gate);                               \
+        else                                                                                                          \
+            hipLaunchKernelGGL((rowchain5_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES, true>), dim3(grid),             \
+                               dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, *gate);                               \
         break;
             RCG_CASE(DPVO_RG_GATE | DPVO_RG_LN)
             RCG_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
@@ -1506,7 +1518,12 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
     switch (f) {
 #define RCH_CASE(F)                                                                                                   \
     case (F):                                                                                                         \
-        hipLaunchKernelGGL(rowchain5_kernel<(F)>, dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, a2); \
+        if (relu1)                                                                                                    \
+            hipLaunchKernelGGL((rowchain5_kernel<(F), false, 0, RG_RELU>), dim3(grid), dim3(R5_THREADS), 0,           \
+                               as_stream(stream), *g1, a2, a2);                                                       \
+        else                                                                                                          \
+            hipLaunchKernelGGL(rowchain5_kernel<(F)>, dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a2,   \
+                               a2);                                                                                   \
         break;
         RCH_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
         RCH_CASE(DPVO_RG_RES)
@@ -1562,8 +1579,12 @@ extern "C" int dpvo_rowchain3(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_ar
     dpvo_rowgemm_args a3 = *g3;
     a3.M = g1->M;
     a3.M_dev = g1->M_dev;
-    hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | DPVO_RG_LN, false, DPVO_RG_LN | DPVO_RG_LN_RELU>), dim3(grid),
-                       dim3(R5_THREADS), 0, as_stream(stream), *g1, a3, *g2);
+    if (g1->flags == DPVO_RG_RELU)
+        hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | DPVO_RG_LN, false, DPVO_RG_LN | DPVO_RG_LN_RELU, RG_RELU>),
+                           dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a3, *g2);
+    else
+        hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | DPVO_RG_LN, false, DPVO_RG_LN | DPVO_RG_LN_RELU>),
+                           dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a3, *g2);
     DPVO_CHECK_LAUNCH();
     return 0;
 }
