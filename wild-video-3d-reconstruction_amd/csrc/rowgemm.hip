@@ -124,6 +124,13 @@ struct EpiOps2 {
     ep_h4 add[R / 2][3];    // res16[idx] or gate16
 };
 
+// A row of zeros the epilogue reads in place of an absent res16 row: the add
+// registers are then always load destinations (a zero-fill branch beside the
+// load made the compiler drain every outstanding load -- the chain's W / A
+// prefetch included -- before each OVL batch, to order the zero writes after
+// the registers' previous loads).
+__device__ half_t g_epi_zero_row[RG_BN];   // (device globals start zeroed)
+
 template <int FLAGS, int R>
 __device__ __forceinline__ void epi2_load(const dpvo_rowgemm_args& p, int64_t M, int64_t row0, int lane, EpiOps2<R>& o)
 {
@@ -134,18 +141,18 @@ __device__ __forceinline__ void epi2_load(const dpvo_rowgemm_args& p, int64_t M,
         const int64_t rr = row0 + 2 * i + h;
         const int64_t row = rr < M ? rr : M - 1;   // clamped for loads; stores skip rows >= M
         const float* r32 = (const float*)p.res32 + row * p.ldr;
-        const half_t* r16 = nullptr;
+        const half_t* r16 = g_epi_zero_row;
         if (FLAGS & RG_GATE) {
             r16 = (const half_t*)p.gate16 + row * RG_BN;
         } else if (p.res16) {
             const int64_t src = p.res16_idx ? p.res16_idx[row] : row;
-            r16 = src >= 0 ? (const half_t*)p.res16 + src * RG_BN : nullptr;
+            if (src >= 0) r16 = (const half_t*)p.res16 + src * RG_BN;
         }
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             const int c = 128 * j + 4 * s;
             o.base[i][j] = *(const ep_f4*)(r32 + c);
-            o.add[i][j] = r16 ? *(const ep_h4*)(r16 + c) : ep_h4{(half_t)0, (half_t)0, (half_t)0, (half_t)0};
+            o.add[i][j] = *(const ep_h4*)(r16 + c);
         }
     }
 }
