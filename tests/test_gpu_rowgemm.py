@@ -316,6 +316,31 @@ def test_rowchain_is_two_rowgemms(case, big):
             assert torch.equal(r, g)
 
 
+@pytest.mark.parametrize("flags1,M", [("relu", 2048 * 128 + 77), ("sigmoid", 3000), ("none", 3000)])
+def test_rowchain_gather_many_tiles_and_runtime_activation(flags1, M):
+    """c1 / c2's gathered chain with more than 8 tiles per 256 workgroups
+    (2,049 tiles: the launch then sizes the grid so that each block's row
+    sources fit its LDS table), and the first GEMM's activation when it is not
+    the compile-time ReLU (read from the flags at run time): both still
+    bit-identical to two rowgemm launches."""
+    import update_ops as U
+    torch.manual_seed(5)
+    dev = "cuda"
+    f1 = {"relu": U.RELU, "sigmoid": U.SIGMOID, "none": 0}[flags1]
+    A = (torch.randn(4096, 384, device=dev) * 0.5).half()
+    W1, b1 = U.pack_linear(torch.randn(384, 384, device=dev) / 20.0, torch.randn(384, device=dev) * 0.1)
+    W2, b2 = U.pack_linear(torch.randn(384, 384, device=dev) / 20.0, torch.randn(384, device=dev) * 0.1)
+    res32 = torch.randn(M, 384, device=dev)
+    a_idx = torch.randint(-1, A.shape[0], (M,), device=dev)
+    _, h, _ = U.rowgemm(A, W1, b1, flags=f1, a_idx=a_idx)
+    ref = U.rowgemm(h, W2, b2, flags=U.RES, res32=res32, want32=True)
+    got = U.rowchain(A, W1, b1, W2, b2, flags1=f1, a_idx=a_idx, flags=U.RES, res32=res32, want32=True)
+    for r, g in zip(ref, got):
+        assert (r is None) == (g is None)
+        if r is not None:
+            assert torch.equal(r, g)
+
+
 @pytest.mark.parametrize("M", [1, 1000, 50000])
 @pytest.mark.parametrize("last", [False, True])
 def test_rowchain_gated_is_gate_gemm_plus_chain(M, last):

@@ -843,6 +843,8 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
 // spill.)  Per output element the MFMA k order and the epilogue arithmetic are
 // rowgemm3's: bit-identical to the unchained launches.
 // ---------------------------------------------------------------------------
+constexpr int R5_IDX_TILES = 8;   // rowchain5: tiles per block whose row sources sit in LDS
+
 struct R5WCursor {   // (tile, segment, k-step) of the flat W-step sequence
     int64_t f, t;
     int s, k;
@@ -875,7 +877,8 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
     constexpr int NPA = GATED ? 2 : 1;   // A passes per tile
     constexpr int nk2 = RG_BN / R5_BK;
     constexpr int BIAS_OFF = R5_LDS;   // the three biases, 768 B each, after the A ring
-    __shared__ __attribute__((aligned(16))) char smem[R5_LDS + 3 * RG_BN * 2];
+    constexpr int IDX_OFF = BIAS_OFF + 3 * RG_BN * 2;   // the gathered rows' sources, R5_IDX_TILES tiles
+    __shared__ __attribute__((aligned(16))) char smem[R5_LDS + 3 * RG_BN * 2 + (!GATED && !TRI ? R5_IDX_TILES * RG_BM * 8 : 0)];
     typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -891,17 +894,39 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
     const int64_t total_w = my_tiles * (nk1 + nk2 + (NSEG == 3 ? n2 : 0));
     const YMapChunk ym;
     const half_t* __restrict__ zero = (const half_t*)p1.zero_row;
+    // ---- the gathered rows' sources (p1.a_idx) of this block's tiles, in LDS
+    // before the first A load: a_row reads them there, so crossing into the
+    // next tile inside the k-loop waits on LDS, not (vmcnt 0) on every load
+    // the wave has in flight -- the W / A prefetch and the OVL epilogue's
+    // (the host sizes the grid so that a block has <= R5_IDX_TILES tiles)
+    // (the two-GEMM chains only -- c1 / c2 gather; the gated and three-GEMM
+    // chains keep the direct read, their registers are full)
+    constexpr bool IDX_LDS = !GATED && !TRI;
+    int64_t* idx_lds = (int64_t*)(smem + IDX_OFF);
+    if (IDX_LDS && p1.a_idx) {
+        for (int i = threadIdx.x; i < (int)my_tiles * RG_BM; i += blockDim.x) {
+            const int64_t m = ((int64_t)blockIdx.x + (int64_t)(i / RG_BM) * G) * RG_BM + i % RG_BM;
+            idx_lds[i] = m < Mrows ? p1.a_idx[m] : -1;
+        }
+        __syncthreads();
+    }
     // ---- A staging (rowgemm5's): lane holds row 16 w + (lane >> 2), chunk lane & 3
     const int ar = 16 * w + (lane >> 2), ac = lane & 3;
     int64_t a_tile = -1;
+    int a_lt = -1;   // the block-local index of a_tile (the cursor moves a tile at a time)
     const half_t* arow = zero;
     auto a_row = [&](int64_t t) __attribute__((always_inline)) {
         if (t == a_tile) return;
         a_tile = t;
+        if constexpr (!GATED && !TRI) a_lt++;
         const int64_t m = t * RG_BM + ar;
         const half_t* row = zero;
         if (m < Mrows) {
-            const int64_t src = p1.a_idx ? p1.a_idx[m] : m;
+            int64_t src;
+            if constexpr (IDX_LDS)
+                src = p1.a_idx ? idx_lds[a_lt * RG_BM + ar] : m;
+            else
+                src = p1.a_idx ? p1.a_idx[m] : m;
             if (src >= 0 && src < p1.a_rows) row = (const half_t*)p1.A + src * p1.lda;
         }
         arow = row + 8 * ac;
@@ -1493,7 +1518,8 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
     if (g1->M <= 0) return 0;
     if (ensure_num_cus()) return -1;
     const int64_t ntiles = (g1->M + RG_BM - 1) / RG_BM;
-    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+    // (at least ntiles / R5_IDX_TILES blocks: a block's row sources fit its LDS table)
+    const unsigned grid = (unsigned)std::max<int64_t>(std::min<int64_t>(ntiles, g_num_cus), (ntiles + R5_IDX_TILES - 1) / R5_IDX_TILES);
     dpvo_rowgemm_args a2 = *g2;
     a2.M = g1->M;
     a2.M_dev = g1->M_dev;
@@ -1582,7 +1608,8 @@ extern "C" int dpvo_rowchain3(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_ar
     if (g1->M <= 0) return 0;
     if (ensure_num_cus()) return -1;
     const int64_t ntiles = (g1->M + RG_BM - 1) / RG_BM;
-    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+    // (at least ntiles / R5_IDX_TILES blocks: a block's row sources fit its LDS table)
+    const unsigned grid = (unsigned)std::max<int64_t>(std::min<int64_t>(ntiles, g_num_cus), (ntiles + R5_IDX_TILES - 1) / R5_IDX_TILES);
     dpvo_rowgemm_args a3 = *g3;
     a3.M = g1->M;
     a3.M_dev = g1->M_dev;
