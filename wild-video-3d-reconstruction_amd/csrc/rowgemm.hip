@@ -579,9 +579,19 @@ struct R5Cursor {
 // operand) without its 73 MB fp16 rows round-tripping HBM.
 struct R5PreRaw {
     f4_t lo, hi;   // 8 fp32 of pre.a
-    h8_t b;        // 8 fp16 of the gathered addend
-    bool add;      // the row has an addend (else v = a, as rowadd_ln: a + 0 would turn -0 into +0)
+    h8_t b;        // 8 fp16 of the gathered addend, or -0 (a row without one)
 };
+// The addend of a row without one: -0, so that v + b == v for every v (rowadd_ln
+// then adds nothing; a +0 would turn -0 into +0)
+struct R5NegZeroRow {
+    unsigned short v[RG_BN];
+    constexpr R5NegZeroRow() : v{}
+    {
+        for (int i = 0; i < RG_BN; i++) v[i] = 0x8000;
+    }
+};
+__device__ constexpr R5NegZeroRow g_pre_negzero{};
+constexpr int R5_PRE_IDX_TILES = 8;   // PRE: tiles per block whose addend sources sit in LDS
 template <bool PRE>
 using r5_areg_t = std::conditional_t<PRE, R5PreRaw, h8_t>;
 __device__ __forceinline__ h8_t r5_cvt(const h8_t& x) { return x; }
@@ -590,8 +600,8 @@ __device__ __forceinline__ h8_t r5_cvt(const R5PreRaw& x)
     h8_t y;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        y[i] = (half_t)(x.add ? x.lo[i] + (float)x.b[i] : x.lo[i]);
-        y[4 + i] = (half_t)(x.add ? x.hi[i] + (float)x.b[4 + i] : x.hi[i]);
+        y[i] = (half_t)(x.lo[i] + (float)x.b[i]);
+        y[4 + i] = (half_t)(x.hi[i] + (float)x.b[4 + i]);
     }
     return y;
 }
@@ -601,7 +611,7 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
                                                                  dpvo_rowadd_args pre)
 {
     static_assert((FLAGS & ~(RG_RELU | RG_SIGMOID)) == 0, "v5: plain GEMMs only");
-    __shared__ __attribute__((aligned(16))) char smem[R5_LDS];
+    __shared__ __attribute__((aligned(16))) char smem[R5_LDS + (PRE ? R5_PRE_IDX_TILES * RG_BM * 8 : 0)];
     typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -615,25 +625,37 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     const YMapChunk ym;
     const int fr = lane & 15, fq = lane >> 4;
     const half_t* __restrict__ zero = (const half_t*)p.zero_row;
+    // PRE: the addend rows' sources of this block's tiles, in LDS before the
+    // first A load (a_row then waits on LDS, not -- vmcnt 0 -- on every load in
+    // flight, when the A stream crosses into the next tile); the host sizes
+    // the grid so that a block has <= R5_PRE_IDX_TILES tiles
+    int64_t* idx_lds = (int64_t*)(smem + R5_LDS);
+    if constexpr (PRE) {
+        for (int i = threadIdx.x; i < (int)my_tiles * RG_BM; i += blockDim.x) {
+            const int64_t m = ((int64_t)blockIdx.x + (int64_t)(i / RG_BM) * gridDim.x) * RG_BM + i % RG_BM;
+            int64_t src = -1;
+            if (m < Mrows && pre.b16) src = pre.b_idx ? pre.b_idx[m] : m;
+            idx_lds[i] = src;
+        }
+        __syncthreads();
+    }
     // ---- A staging: lane holds row 16 w + (lane >> 2), logical chunk lane & 3
     const int ar = 16 * w + (lane >> 2), ac = lane & 3;
     int64_t a_tile = -1;
+    int a_lt = -1;                   // PRE: the block-local index of a_tile
     const half_t* arow = zero;
     const float* arow32 = nullptr;   // PRE
-    bool aadd = false;               // PRE: this lane's row has an addend
     auto a_row = [&](int64_t t) __attribute__((always_inline)) {
         if (t == a_tile) return;
         a_tile = t;
         const int64_t m = t * RG_BM + ar;
         if constexpr (PRE) {
+            a_lt++;
             // rows past M read row 0 (finite; their outputs are never stored)
             arow32 = (const float*)pre.a + (m < Mrows ? m : 0) * pre.lda + 8 * ac;
-            const half_t* b = zero;
-            if (m < Mrows && pre.b16) {
-                const int64_t s = pre.b_idx ? pre.b_idx[m] : m;
-                if (s >= 0 && s < pre.b_rows) b = (const half_t*)pre.b16 + s * RG_BN;
-            }
-            aadd = b != zero;
+            const int64_t s = idx_lds[a_lt * RG_BM + ar];
+            const half_t* b = (const half_t*)g_pre_negzero.v;
+            if (s >= 0 && s < pre.b_rows) b = (const half_t*)pre.b16 + s * RG_BN;
             arow = b + 8 * ac;
         } else {
             const half_t* row = zero;
@@ -652,7 +674,6 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
             x.lo = *(const f4_t*)(arow32 + c.k * R5_BK);
             x.hi = *(const f4_t*)(arow32 + c.k * R5_BK + 4);
             x.b = *(const h8_t*)(arow + c.k * R5_BK);
-            x.add = aadd;
             return x;
         } else {
             return *(const h8_t*)(arow + c.k * R5_BK);
@@ -1439,7 +1460,9 @@ extern "C" int dpvo_rowgemm_pair_pre(const dpvo_rowgemm_args* a, const dpvo_rowg
     if (a->M <= 0) return 0;
     if (ensure_num_cus()) return -1;
     const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
-    const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+    // (at least ntiles / R5_PRE_IDX_TILES blocks: a block's addend sources fit its LDS table)
+    const unsigned grid =
+        (unsigned)std::max<int64_t>(std::min<int64_t>(ntiles, g_num_cus), (ntiles + R5_PRE_IDX_TILES - 1) / R5_PRE_IDX_TILES);
     hipLaunchKernelGGL((rowgemm5_kernel<0, true, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b,
                        *pre);
     DPVO_CHECK_LAUNCH();
