@@ -625,38 +625,43 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     const YMapChunk ym;
     const int fr = lane & 15, fq = lane >> 4;
     const half_t* __restrict__ zero = (const half_t*)p.zero_row;
-    // PRE: the addend rows' sources of this block's tiles, in LDS before the
-    // first A load (a_row then waits on LDS, not -- vmcnt 0 -- on every load in
-    // flight, when the A stream crosses into the next tile); the host sizes
-    // the grid so that a block has <= R5_PRE_IDX_TILES tiles
+    // PRE: the addend rows' sources -- the first tile's read directly in the
+    // prologue, the block's later tiles' from an LDS table filled after the
+    // prologue's loads are issued (published by the first k-step's barrier),
+    // so that crossing into the next tile inside the k-loop waits on LDS, not
+    // (vmcnt 0) on every load in flight; the host sizes the grid so that a
+    // block has <= R5_PRE_IDX_TILES tiles
     int64_t* idx_lds = (int64_t*)(smem + R5_LDS);
-    if constexpr (PRE) {
-        for (int i = threadIdx.x; i < (int)my_tiles * RG_BM; i += blockDim.x) {
-            const int64_t m = ((int64_t)blockIdx.x + (int64_t)(i / RG_BM) * gridDim.x) * RG_BM + i % RG_BM;
-            int64_t src = -1;
-            if (m < Mrows && pre.b16) src = pre.b_idx ? pre.b_idx[m] : m;
-            idx_lds[i] = src;
-        }
-        __syncthreads();
-    }
+    auto pre_src = [&](int64_t m) __attribute__((always_inline)) -> int64_t {
+        return (m < Mrows && pre.b16) ? (pre.b_idx ? pre.b_idx[m] : m) : -1;
+    };
     // ---- A staging: lane holds row 16 w + (lane >> 2), logical chunk lane & 3
     const int ar = 16 * w + (lane >> 2), ac = lane & 3;
+
     int64_t a_tile = -1;
     int a_lt = -1;                   // PRE: the block-local index of a_tile
     const half_t* arow = zero;
     const float* arow32 = nullptr;   // PRE
+    auto pre_set = [&](int64_t t, int64_t s) __attribute__((always_inline)) {
+        const int64_t m = t * RG_BM + ar;
+        // rows past M read row 0 (finite; their outputs are never stored)
+        arow32 = (const float*)pre.a + (m < Mrows ? m : 0) * pre.lda + 8 * ac;
+        const half_t* b = (const half_t*)g_pre_negzero.v;
+        if (s >= 0 && s < pre.b_rows) b = (const half_t*)pre.b16 + s * RG_BN;
+        arow = b + 8 * ac;
+    };
+    if constexpr (PRE) {   // the first tile, from global (the table is filled after the prologue)
+        a_tile = blockIdx.x;
+        a_lt = 0;
+        pre_set(a_tile, pre_src(a_tile * RG_BM + ar));
+    }
     auto a_row = [&](int64_t t) __attribute__((always_inline)) {
         if (t == a_tile) return;
         a_tile = t;
         const int64_t m = t * RG_BM + ar;
         if constexpr (PRE) {
             a_lt++;
-            // rows past M read row 0 (finite; their outputs are never stored)
-            arow32 = (const float*)pre.a + (m < Mrows ? m : 0) * pre.lda + 8 * ac;
-            const int64_t s = idx_lds[a_lt * RG_BM + ar];
-            const half_t* b = (const half_t*)g_pre_negzero.v;
-            if (s >= 0 && s < pre.b_rows) b = (const half_t*)pre.b16 + s * RG_BN;
-            arow = b + 8 * ac;
+            pre_set(t, idx_lds[a_lt * RG_BM + ar]);
         } else {
             const half_t* row = zero;
             if (m < Mrows) {
@@ -779,6 +784,10 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     for (int r = 0; r < 2; r++) {
         areg[r] = load_a(ca);
         ca.next(total, nks, NP, G);
+    }
+    if constexpr (PRE) {   // (stages 0-3 are the first tile's: NP nks >= 4, K % 64 == 0)
+        for (int i = RG_BM + threadIdx.x; i < (int)my_tiles * RG_BM; i += blockDim.x)
+            idx_lds[i] = pre_src(((int64_t)blockIdx.x + (int64_t)(i / RG_BM) * G) * RG_BM + i % RG_BM);
     }
 #ifdef DPVO_STAMPS
     unsigned long long st_sum[ST_SEGS] = {};
@@ -915,42 +924,57 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
     const int64_t total_w = my_tiles * (nk1 + nk2 + (NSEG == 3 ? n2 : 0));
     const YMapChunk ym;
     const half_t* __restrict__ zero = (const half_t*)p1.zero_row;
-    // ---- the gathered rows' sources (p1.a_idx) of this block's tiles, in LDS
-    // before the first A load: a_row reads them there, so crossing into the
-    // next tile inside the k-loop waits on LDS, not (vmcnt 0) on every load
-    // the wave has in flight -- the W / A prefetch and the OVL epilogue's
-    // (the host sizes the grid so that a block has <= R5_IDX_TILES tiles)
-    // (the two-GEMM chains only -- c1 / c2 gather; the gated and three-GEMM
-    // chains keep the direct read, their registers are full)
+    // ---- the gathered rows' sources (p1.a_idx): the first tile's read
+    // directly in the prologue, the block's later tiles' from an LDS table
+    // filled after the prologue's loads are issued (published by GEMM1's first
+    // barrier), so crossing into the next tile inside the k-loop waits on LDS,
+    // not (vmcnt 0) on every load the wave has in flight -- the W / A prefetch
+    // and the OVL epilogue's.  (K1 = 64: the prologue's four A stages already
+    // cross, so the whole table is filled first.)  The host sizes the grid so
+    // that a block has <= R5_IDX_TILES tiles.  The two-GEMM chains only (c1 /
+    // c2 gather); the gated and three-GEMM chains keep the direct read, their
+    // registers are full.
     constexpr bool IDX_LDS = !GATED && !TRI;
     int64_t* idx_lds = (int64_t*)(smem + IDX_OFF);
-    if (IDX_LDS && p1.a_idx) {
-        for (int i = threadIdx.x; i < (int)my_tiles * RG_BM; i += blockDim.x) {
+    const bool idx_tab = IDX_LDS && p1.a_idx, idx_early = idx_tab && nk1 < 4;
+    auto idx_fill = [&](int i0) __attribute__((always_inline)) {
+        for (int i = i0 + threadIdx.x; i < (int)my_tiles * RG_BM; i += blockDim.x) {
             const int64_t m = ((int64_t)blockIdx.x + (int64_t)(i / RG_BM) * G) * RG_BM + i % RG_BM;
             idx_lds[i] = m < Mrows ? p1.a_idx[m] : -1;
         }
+    };
+    if (idx_early) {
+        idx_fill(0);
         __syncthreads();
     }
     // ---- A staging (rowgemm5's): lane holds row 16 w + (lane >> 2), chunk lane & 3
     const int ar = 16 * w + (lane >> 2), ac = lane & 3;
+
     int64_t a_tile = -1;
     int a_lt = -1;   // the block-local index of a_tile (the cursor moves a tile at a time)
     const half_t* arow = zero;
+    auto a_set = [&](int64_t m, int64_t src) __attribute__((always_inline)) {
+        const half_t* row = zero;
+        if (m < Mrows && src >= 0 && src < p1.a_rows) row = (const half_t*)p1.A + src * p1.lda;
+        arow = row + 8 * ac;
+    };
+    if (idx_tab && !idx_early) {   // the first tile, from global (the table is filled after the prologue)
+        a_tile = blockIdx.x;
+        a_lt = 0;
+        const int64_t m0 = a_tile * RG_BM + ar;
+        a_set(m0, m0 < Mrows ? p1.a_idx[m0] : -1);
+    }
     auto a_row = [&](int64_t t) __attribute__((always_inline)) {
         if (t == a_tile) return;
         a_tile = t;
         if constexpr (!GATED && !TRI) a_lt++;
         const int64_t m = t * RG_BM + ar;
-        const half_t* row = zero;
-        if (m < Mrows) {
-            int64_t src;
-            if constexpr (IDX_LDS)
-                src = p1.a_idx ? idx_lds[a_lt * RG_BM + ar] : m;
-            else
-                src = p1.a_idx ? p1.a_idx[m] : m;
-            if (src >= 0 && src < p1.a_rows) row = (const half_t*)p1.A + src * p1.lda;
-        }
-        arow = row + 8 * ac;
+        int64_t src;
+        if constexpr (IDX_LDS)
+            src = !p1.a_idx ? m : idx_lds[a_lt * RG_BM + ar];
+        else
+            src = p1.a_idx ? (m < Mrows ? p1.a_idx[m] : -1) : m;
+        a_set(m, src);
     };
     h8_t areg[2];
     auto load_a = [&](const R5Cursor& c) __attribute__((always_inline)) -> h8_t {
@@ -1133,6 +1157,7 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
         areg[r] = load_a(ca);
         anext();
     }
+    if (idx_tab && !idx_early) idx_fill(RG_BM);   // (tiles 1.. : read after GEMM1's first barrier)
     int64_t etile = -1;   // OVL: the tile whose row epilogue is still pending
 #ifdef DPVO_STAMPS
     // chain segments: 0 GEMM1 k-loop (+ OVL epilogue), 1 GEMM1 -> y tile + sync,
