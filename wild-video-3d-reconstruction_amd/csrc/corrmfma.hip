@@ -97,12 +97,20 @@ struct CmEdgeIn {
     float cx, cy;   // patch pixel (lane & 15)'s coordinates (x, y) when < 9 -- level scaling applied later
 };
 
+// The edge's slot, index and frame indices are wave-uniform: read through the
+// scalar cache (constant address space: s_load), so the next edge's dependent
+// index chain waits on lgkmcnt only.  As vector loads, the wait for the order
+// entry before the ii / jj loads was a vmcnt(0) -- every edge drained the
+// previous edge's epilogue stores before its own work could start.
+typedef const __attribute__((address_space(4))) int cm_cint;
+typedef const __attribute__((address_space(4))) int64_t cm_cint64;
 __device__ __forceinline__ CmEdgeIn cm_load_edge(const CorrMfmaParams& p, int slot, int q16)
 {
     CmEdgeIn in;
-    in.e = p.order ? p.order[slot] : slot;
-    in.ix = (int)p.ii[in.e];
-    in.jx = (int)p.jj[in.e];
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    in.e = p.order ? ((cm_cint*)p.order)[slot] : slot;
+    in.ix = (int)((cm_cint64*)p.ii)[in.e];
+    in.jx = (int)((cm_cint64*)p.jj)[in.e];
     const int q = q16 < cm::NP ? q16 : 0;
     const float* cb = p.coords + (int64_t)in.e * p.c_s[1] + (q / 3) * p.c_s[3] + (q % 3) * p.c_s[4];
     in.cx = cb[0];
