@@ -664,9 +664,13 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
             pre_set(t, idx_lds[a_lt * RG_BM + ar]);
         } else {
             const half_t* row = zero;
-            if (m < Mrows) {
-                const int64_t src = p.a_idx ? p.a_idx[m] : m;
-                if (src >= 0 && src < p.a_rows) row = (const half_t*)p.A + src * p.lda;
+            if (p.a_idx) {   // (the index load's wait inside the branch, not at the join)
+                if (m < Mrows) {
+                    const int64_t src = p.a_idx[m];
+                    if (src >= 0 && src < p.a_rows) row = (const half_t*)p.A + src * p.lda;
+                }
+            } else if (m < Mrows && m < p.a_rows) {
+                row = (const half_t*)p.A + m * p.lda;
             }
             arow = row + 8 * ac;
         }
@@ -969,12 +973,13 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
         a_tile = t;
         if constexpr (!GATED && !TRI) a_lt++;
         const int64_t m = t * RG_BM + ar;
-        int64_t src;
-        if constexpr (IDX_LDS)
-            src = !p1.a_idx ? m : idx_lds[a_lt * RG_BM + ar];
-        else
-            src = p1.a_idx ? (m < Mrows ? p1.a_idx[m] : -1) : m;
-        a_set(m, src);
+        if constexpr (IDX_LDS) {
+            a_set(m, !p1.a_idx ? m : idx_lds[a_lt * RG_BM + ar]);
+        } else if (p1.a_idx) {   // (the load's wait stays inside this branch: a wait at
+            a_set(m, m < Mrows ? p1.a_idx[m] : -1);   // the join would drain the queue on every path)
+        } else {
+            a_set(m, m);
+        }
     };
     h8_t areg[2];
     auto load_a = [&](const R5Cursor& c) __attribute__((always_inline)) -> h8_t {
