@@ -2133,27 +2133,41 @@ __global__ __launch_bounds__(64 * BD_WAVES) void bd_patch_kernel(BdParams p)
 // H = sum of the patch kernel's workgroup partials, fixed order.  Also stored
 // as dense rows for the wave solver: Hd[b][a] = H(a, b) (a <= b, the lower
 // triangle, row pitch BD_HD_LD) and row n6 = g.
+// 32 entries per workgroup (twice the workgroups of a 64-entry split: the
+// reduce is bound by how fast few CUs pull the 512 partials, 3.9 MB at C2/C3):
+// half h = lane / 32 of each wave reads partial rows 2 (wave + 16 j) + h, every
+// row segment a full 128-byte line; the halves' sums are added by a lane swap,
+// the waves' in wave order -- a fixed order, so the same bits every call.
+constexpr int BR_E = 32;
 __global__ __launch_bounds__(1024) void bd_reduce_kernel(BdParams p)
 {
-    __shared__ float red[16][64];
+    __shared__ float red[16][BR_E];
     if (*(volatile int*)p.status != 0) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int i = blockIdx.x * 64 + lane;
-    // all of this wave's partials in flight at once (one HBM round trip, not
-    // eight), then summed in partial order: the same bits as a running sum
-    constexpr int PER = BD_GRID / 16;
+    const int h = lane >> 5, e = lane & 31;
+    const int i = blockIdx.x * BR_E + e;
+    // all of this lane's partials in flight at once (one HBM round trip),
+    // then summed in row order
+    constexpr int PER = BD_GRID / 32;
+    static_assert(BD_GRID % 32 == 0, "16 waves x 2 halves split the partials evenly");
     float v[PER];
 #pragma unroll
-    for (int j = 0; j < PER; j++) v[j] = i < p.ent ? p.Hpart[(int64_t)(wave + 16 * j) * p.ent + i] : 0.f;
+    for (int j = 0; j < PER; j++)
+        v[j] = i < p.ent ? p.Hpart[(int64_t)(2 * (wave + 16 * j) + h) * p.ent + i] : 0.f;
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < PER; j++) s += v[j];
-    red[wave][lane] = s;
+    {
+        auto w2 = __builtin_amdgcn_permlane32_swap(__float_as_int(s), __float_as_int(s), false, false);
+        const float o = __int_as_float(h ? w2[0] : w2[1]);   // the other half's sum
+        s = h ? o + s : s + o;                              // (half 0's + half 1's in both)
+    }
+    if (h == 0) red[wave][e] = s;
     __syncthreads();
-    if (wave == 0 && i < p.ent) {
+    if (wave == 0 && h == 0 && i < p.ent) {
         float t = 0.f;
 #pragma unroll
-        for (int w = 0; w < 16; w++) t += red[w][lane];
+        for (int w = 0; w < 16; w++) t += red[w][e];
         p.H[i] = t;
         const int n = p.n6;
         int a = 0, b;
@@ -2527,7 +2541,7 @@ static int ba_forward_det(BdParams p, char* ws, const BdLayout& L, int64_t E, co
     const size_t lds = (size_t)(BD_WAVES * (p.N > 0 ? (L.ent + 3) / 4 * 4 : 0) + BD_WAVES * BD_N6MAX) * 4 +
                        (size_t)(p.N > 0 ? (L.nup + 7) / 8 * 4 : 0) * 4 +
                        (size_t)(p.N > 0 ? BD_SLOTS * BD_SLOT_LD : 0) * 4;
-    const unsigned gR = (unsigned)((L.ent + 63) / 64);
+    const unsigned gR = (unsigned)((L.ent + BR_E - 1) / BR_E);
     for (int it = 0; it < iterations; it++) {
         if (it == 0)
             hipLaunchKernelGGL((bd_patch_kernel<false, true>), dim3(bd_grid()), dim3(64 * BD_WAVES), lds, s, p);
