@@ -179,8 +179,7 @@ __global__ __launch_bounds__(MM2_THREADS) void motion_mag_part_kernel(const floa
         const float *ka = intr + a * 4, *kb = intr + b * 4;
         const float* pa = patches + kk[e] * 3 * PP;
         float s = 0.f;
-#pragma unroll
-        for (int64_t q = 0; q < PP; q++) {
+        for (int64_t q = 0; q < PP; q++) {   // (PP = P * P at run time: not unrolled)
             float x0, y0, x1, y1, x2, y2;
             project_px(g0, ka, ka, pa, PP, q, x0, y0);
             project_px(g1, ka, kb, pa, PP, q, x1, y1);
