@@ -590,7 +590,10 @@ struct R5NegZeroRow {
         for (int i = 0; i < RG_BN; i++) v[i] = 0x8000;
     }
 };
-__device__ constexpr R5NegZeroRow g_pre_negzero{};
+// (a non-const __device__ object: global address space, so that a pointer to
+// it or to an addend row stays a global pointer -- a constant one made the
+// loads through it flat loads)
+__device__ R5NegZeroRow g_pre_negzero = R5NegZeroRow{};
 constexpr int R5_PRE_IDX_TILES = 8;   // PRE: tiles per block whose addend sources sit in LDS
 template <bool PRE>
 using r5_areg_t = std::conditional_t<PRE, R5PreRaw, h8_t>;
@@ -1312,6 +1315,12 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
 typedef float rl_f4 __attribute__((ext_vector_type(4)));
 typedef half_t rl_h4 __attribute__((ext_vector_type(4)));
 
+// Every load of a row is issued before the first use: the two row-source
+// indices together, then the a, b and c rows together (absent addends read a
+// row of -0, so v + b == v exactly, as the skipped add; the fp16 / fp32 choice
+// of a is a template parameter).  Branching per load had the compiler wait on
+// each in turn: ~7 dependent HBM round trips per row, 67 us at C3.
+template <bool A16>
 __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
 {
     const int sub = threadIdx.x & 31;
@@ -1328,23 +1337,19 @@ __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
             }
         }
     }
+    const half_t* negzero = (const half_t*)g_pre_negzero.v;
     for (int64_t row = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 5; row < p.M;
          row += ((int64_t)gridDim.x * blockDim.x) >> 5) {
         float v[12];
-        const half_t* b = nullptr;
-        const half_t* c2 = nullptr;
-        if (p.b16) {
-            const int64_t s = p.b_idx ? p.b_idx[row] : row;
-            if (s >= 0 && s < p.b_rows) b = (const half_t*)p.b16 + s * RG_BN;
-        }
-        if (p.c16) {
-            const int64_t s = p.c_idx ? p.c_idx[row] : row;
-            if (s >= 0 && s < p.c_rows) c2 = (const half_t*)p.c16 + s * RG_BN;
-        }
+        const int64_t sb = p.b_idx ? p.b_idx[row] : row;
+        const int64_t sc = p.c_idx ? p.c_idx[row] : row;
+        const half_t* b = p.b16 && sb >= 0 && sb < p.b_rows ? (const half_t*)p.b16 + sb * RG_BN : negzero;
+        const half_t* c2 = p.c16 && sc >= 0 && sc < p.c_rows ? (const half_t*)p.c16 + sc * RG_BN : negzero;
+        rl_h4 hb[3], hc[3];
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             const int c = 128 * j + 4 * sub;
-            if (p.a_f16) {
+            if constexpr (A16) {
                 const rl_h4 h = *(const rl_h4*)((const half_t*)p.a + row * p.lda + c);
 #pragma unroll
                 for (int t = 0; t < 4; t++) v[4 * j + t] = (float)h[t];
@@ -1353,23 +1358,18 @@ __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
 #pragma unroll
                 for (int t = 0; t < 4; t++) v[4 * j + t] = a[t];
             }
+            hb[j] = *(const rl_h4*)(b + c);
+            hc[j] = *(const rl_h4*)(c2 + c);
         }
-        if (b) {
+        // ((a + b) + c: the two row adds of consecutive rowadd_ln calls, in order)
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const rl_h4 h = *(const rl_h4*)(b + 128 * j + 4 * sub);
+        for (int j = 0; j < 3; j++)
 #pragma unroll
-                for (int t = 0; t < 4; t++) v[4 * j + t] += (float)h[t];
-            }
-        }
-        if (c2) {   // ((a + b) + c: the two row adds of consecutive rowadd_ln calls, in order)
+            for (int t = 0; t < 4; t++) v[4 * j + t] += (float)hb[j][t];
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                const rl_h4 h = *(const rl_h4*)(c2 + 128 * j + 4 * sub);
+        for (int j = 0; j < 3; j++)
 #pragma unroll
-                for (int t = 0; t < 4; t++) v[4 * j + t] += (float)h[t];
-            }
-        }
+            for (int t = 0; t < 4; t++) v[4 * j + t] += (float)hc[j][t];
         if (p.ln_g) {
             // half-wave sums with DPP rotations and a gfx950 lane swap: VALU
             // only (a + b == b + a, so both lanes of a swapped pair agree)
@@ -1709,7 +1709,10 @@ extern "C" int dpvo_rowadd_ln(const dpvo_rowadd_args* a, void* stream)
     DPVO_CHECK_ARG(!a->ln_g == !a->ln_b, "rowadd_ln: LayerNorm needs both weight and bias");
     if (a->M <= 0) return 0;
     const unsigned grid = grid_for(a->M * 32, 256, 16384);
-    hipLaunchKernelGGL(rowadd_ln_kernel, dim3(grid), dim3(256), 0, as_stream(stream), *a);
+    if (a->a_f16)
+        hipLaunchKernelGGL(rowadd_ln_kernel<true>, dim3(grid), dim3(256), 0, as_stream(stream), *a);
+    else
+        hipLaunchKernelGGL(rowadd_ln_kernel<false>, dim3(grid), dim3(256), 0, as_stream(stream), *a);
     DPVO_CHECK_LAUNCH();
     return 0;
 }
