@@ -614,7 +614,10 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
                                                                  dpvo_rowadd_args pre)
 {
     static_assert((FLAGS & ~(RG_RELU | RG_SIGMOID)) == 0, "v5: plain GEMMs only");
-    __shared__ __attribute__((aligned(16))) char smem[R5_LDS + (PRE ? R5_PRE_IDX_TILES * RG_BM * 8 : 0)];
+    // (PRE: the addend-source table, then both passes' biases -- in LDS, not
+    // registers: the staged fp32 + fp16 A register sets leave none to spare)
+    constexpr int PRE_BIAS = R5_LDS + R5_PRE_IDX_TILES * RG_BM * 8;
+    __shared__ __attribute__((aligned(16))) char smem[R5_LDS + (PRE ? R5_PRE_IDX_TILES * RG_BM * 8 + 2 * RG_BN * 2 : 0)];
     typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -703,13 +706,21 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) r[nt] = *(const h8_t*)(src + nt * 16 * R5_BK);
     };
-    // ---- biases of this wave's columns, both passes
-    h4_t bias[NP][3];
+    // ---- biases of this wave's columns, both passes (PRE: staged in LDS here,
+    // read by the epilogues, which follow the k-loop's barriers)
+    h4_t bias[PRE ? 1 : NP][3];
+    if constexpr (PRE) {
+        if (threadIdx.x < NP * 96) {
+            const int b = threadIdx.x / 96, c = 4 * (threadIdx.x % 96);
+            *(h4_t*)(smem + PRE_BIAS + b * RG_BN * 2 + 2 * c) = *(const h4_t*)((const half_t*)(b ? p2.bias : p.bias) + c);
+        }
+    } else {
 #pragma unroll
-    for (int q = 0; q < NP; q++)
+        for (int q = 0; q < NP; q++)
 #pragma unroll
-        for (int nt = 0; nt < 3; nt++)
-            bias[q][nt] = *(const h4_t*)((const half_t*)(q ? p2.bias : p.bias) + 48 * w + 16 * nt + 4 * fq);
+            for (int nt = 0; nt < 3; nt++)
+                bias[q][nt] = *(const h4_t*)((const half_t*)(q ? p2.bias : p.bias) + 48 * w + 16 * nt + 4 * fq);
+    }
     f4_t acc[8][3];
 #pragma unroll
     for (int mt = 0; mt < 8; mt++)
@@ -723,12 +734,17 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
             const int col = 48 * w + 16 * nt + 4 * fq;
+            h4_t bq;
+            if constexpr (PRE)
+                bq = *(const h4_t*)(smem + PRE_BIAS + q * RG_BN * 2 + 2 * col);
+            else
+                bq = bias[q][nt];
 #pragma unroll
             for (int mt = 0; mt < 8; mt++) {
                 h4_t y;
 #pragma unroll
                 for (int r = 0; r < 4; r++) {
-                    half_t v = (half_t)(acc[mt][nt][r] + (float)bias[q][nt][r]);
+                    half_t v = (half_t)(acc[mt][nt][r] + (float)bq[r]);
                     if (FLAGS & RG_RELU) v = v > (half_t)0 ? v : (half_t)0;
                     if (FLAGS & RG_SIGMOID) v = (half_t)fast_sigmoid((float)v);
                     y[r] = v;
