@@ -61,7 +61,7 @@ def source_sha(*names):
     return h.hexdigest()[:16]
 
 
-CORR_SOURCES = ("corrstage.hip", "corrmfma.hip", "corrmfma.hpp", "altcorr.hip")
+CORR_SOURCES = ("corrmfma.hip", "corrmfma.hpp", "altcorr.hip")
 UPD_SOURCES = ("rowgemm.hip", "updateop.hip")
 
 
@@ -170,10 +170,8 @@ def gather_to_rank0(tensors, rank, world):
 
 class CorrProbe:
     """HIP events around every altcorr call on the stream it runs on: the
-    LDS-staged matrix-core path (dpvo.altcorr.corr_pyramid_staged: its
-    (frame, cell) binning, the staged kernel and the fallback kernel), or the
     per-edge kernels (corr_pyramid / corr_pyramid_mfma) and the latter's edge
-    ordering (cuda_corr.edge_order) when those are configured."""
+    ordering (cuda_corr.edge_order) when the caller did not supply one."""
 
     def __init__(self):
         self.pairs = {"corr": [], "order": []}
@@ -198,7 +196,6 @@ class CorrProbe:
             return f
         altcorr.corr_pyramid = timed(altcorr.corr_pyramid, "corr")
         altcorr.corr_pyramid_mfma = timed(altcorr.corr_pyramid_mfma, "corr")
-        altcorr.corr_pyramid_staged = timed(altcorr.corr_pyramid_staged, "corr")
         cuda_corr.edge_order = timed(cuda_corr.edge_order, "order")
 
     def clear(self):
@@ -225,9 +222,8 @@ def phase_breakdown(slam, reps=5):
     """Per-phase device time of one update, measured with events outside the
     timed loop.  The phases follow DPVO.update() (dpvo/dpvo.py) step by step,
     with the same arguments: reproject; the window keys and both group-bys
-    (dpvo_window_group_by; + the per-edge altcorr's visiting order when
-    STAGED_CORR is off); altcorr (binning + staged kernel + fallback, or the
-    per-edge kernel in that order); the update operator; the BA
+    (dpvo_window_group_by, with altcorr's visiting order); altcorr (the
+    per-edge matrix-core kernel in that order); the update operator; the BA
     targets + fastba; the point cloud.  Each rep starts behind a device-side
     delay, so the phases run back to back as in the timed loop."""
     import update_ops
@@ -245,11 +241,9 @@ def phase_breakdown(slam, reps=5):
         e[0].record()
         coords = slam.reproject()
         e[1].record()
-        want_order = not getattr(slam.cfg, "STAGED_CORR", False)
-        ctx_idx, jslot, kk_groups, ij_groups, *rest = update_ops.window_group_by(
+        ctx_idx, jslot, kk_groups, ij_groups, order = update_ops.window_group_by(
             slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M, slam.n - 64, slam.M * slam.pmem, slam.pmem,
-            flag=slam._ba_status, jj_order=want_order)
-        order = rest[0] if want_order else None
+            flag=slam._ba_status, jj_order=True)
         e[2].record()
         with torch.autocast("cuda", enabled=True):
             corr = slam.corr(coords, slots=(ctx_idx, jslot), order=order)

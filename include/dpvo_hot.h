@@ -127,26 +127,6 @@ size_t dpvo_edge_order_workspace_bytes(int num_buckets);
 int dpvo_edge_order(const int64_t* jj, int64_t num_edges, int num_buckets, int* order, void* workspace,
                     size_t workspace_bytes, void* stream);
 
-/* The same [E][882] rows as dpvo_corr_pyramid_mfma, bit for bit, with the
- * target frames' windows staged in LDS (csrc/corrstage.hip): the edges are
- * binned on the device by (target frame jj, 8x8-pixel cell of the level-1
- * map); one workgroup per CU stages a cell's 17x17 level-1 and 11x11 level-2
- * pixels once and runs all of the cell's edges from LDS.  Edges whose boxes
- * do not fit their cell's regions (patches spread over more than 4 pixels,
- * far outside the map, bad indices, non-finite coordinates) run through
- * dpvo_corr_pyramid_mfma's kernel afterwards.  Same arguments as
- * dpvo_corr_pyramid_mfma without `order`; workspace: at least
- * dpvo_corr_staged_workspace_bytes(E, N2, H, W) device bytes for N2 frames of
- * an H x W level-1 map (0: too many bins; use dpvo_corr_pyramid_mfma).
- * Six launches: a memset, the binning (count, scan, scatter), the staged
- * kernel, the fallback kernel. */
-size_t dpvo_corr_staged_workspace_bytes(int64_t num_edges, int64_t num_frames, int64_t height, int64_t width);
-int dpvo_corr_pyramid_staged(const void* table, int64_t num_patches, const void* const* fmaps,
-                             const int64_t* fmap_sizes, const int64_t* fmap_strides, const float* level_scale,
-                             const float* coords, const int64_t* coords_size, const int64_t* coords_stride,
-                             const int64_t* ii, const int64_t* jj, void* corr, int64_t edge_stride, void* workspace,
-                             size_t workspace_bytes, void* stream);
-
 /* cuda_corr.backward (correlation_kernel.cu:236-286): grad is the returned
  * (permuted) view's gradient given as contiguous [B][E][2r+1 (x)][2r+1 (y)][P][P]
  * float; gmap_grad / fmap_grad (contiguous, dtype, zero-filled by caller)

@@ -45,3 +45,16 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture
+def poisoned():
+    """Every buffer the shims allocate uninitialised (outputs, workspaces) is
+    filled with 0xff -- NaN in every float type, -1 in the integer types --
+    for the test's duration (_dpvo_hot.set_poison): a kernel that reads memory
+    it never wrote shows up as NaNs or as bits that differ between patterns."""
+    import _dpvo_hot as H
+    old = H.poison()
+    H.set_poison(0xFF)
+    yield 0xFF
+    H.set_poison(old)

@@ -591,7 +591,7 @@ def update_step_fixtures(pops, ba, lie, dscale=None, save=True, which="small"):
 
 if __name__ == "__main__":
     # python make_golden.py [part ...]: parts lietorch, pops, ba, altcorr, neighbors, update, encoder, step,
-    # step_c2 (not in the default set: ~10 min of CPU)
+    # step_c2, step_c3 (not in the default set: ~10 / ~20 min of CPU)
     torch.set_num_threads(8)
     parts = set(sys.argv[1:]) or {"lietorch", "pops", "ba", "altcorr", "neighbors", "update", "encoder", "step"}
     pops, ba, lie = import_reference()
@@ -613,3 +613,5 @@ if __name__ == "__main__":
         update_step_fixtures(pops, ba, lie)
     if "step_c2" in parts:
         update_step_fixtures(pops, ba, lie, which="c2")
+    if "step_c3" in parts:
+        update_step_fixtures(pops, ba, lie, which="c3")

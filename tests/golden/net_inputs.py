@@ -144,7 +144,15 @@ STEP = dict(n=40, M=12, N=48, pmem=36, ht=96, wd=128, lifetime=13, removal=22, o
 # 512 x 384 frames (128 x 96 feature maps, the tartan intrinsics / 4)
 STEP_C2 = dict(n=40, M=96, N=48, pmem=36, ht=384, wd=512, lifetime=13, removal=22, opt_window=10,
                intrinsics=(80.0, 80.0, 64.0, 48.0), iters=8, file="update_step_c2_ref.npz", dscale=1.0)
-STEPS = {"small": STEP, "c2": STEP_C2}
+# C3's per-update workload (BASELINE.json configs[2], the metric's config:
+# dpvo_2k.yaml, M = 192, 2 BA iterations -- dpvo.py:734): E = 497 M = 95,424
+# edges in steady state at n = 40, on 512 x 384 frames.  (dpvo_2k.yaml has
+# default.yaml's windows; only KEYFRAME_THRESH differs, which update() does
+# not read.)
+STEP_C3 = dict(n=40, M=192, N=48, pmem=36, ht=384, wd=512, lifetime=13, removal=22, opt_window=10,
+               intrinsics=(80.0, 80.0, 64.0, 48.0), iters=2, file="update_step_c3_ref.npz", dscale=1.0,
+               preset="dpvo_2k")
+STEPS = {"small": STEP, "c2": STEP_C2, "c3": STEP_C3}
 
 
 def _qmul(a, b):

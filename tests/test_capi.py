@@ -113,6 +113,12 @@ def test_stale_or_stamped_library_is_refused():
     with pytest.raises(ImportError, match="diagnostic"):
         H.verify_build(f"sha={sha} flavour=stamps", sha)
     assert H.verify_build(f"sha={sha} flavour=stamps", sha, diag=True)["flavour"] == "stamps"
+    # an experiment build (scripts/build_exp.sh) from other sources: only with DPVO_DIAG=1
+    with pytest.raises(ImportError, match="stale"):
+        H.verify_build(f"sha={stale} flavour=cbase", sha)
+    assert H.verify_build(f"sha={stale} flavour=cbase", sha, diag=True)["flavour"] == "cbase"
+    with pytest.raises(ImportError, match="stale"):   # never the product
+        H.verify_build(f"sha={stale} flavour=product", sha, diag=True)
     with pytest.raises(ImportError, match="provenance"):
         H.verify_build("", sha)
 

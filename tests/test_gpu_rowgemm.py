@@ -4,8 +4,9 @@ Linear -> fp16 output, glue ops in fp32, LayerNorm in fp32.  Accumulation
 order differs from hipBLASLt, so fp16 outputs may differ by an ulp."""
 import pytest
 import torch
+from tests_helpers import same
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("poisoned")]
 
 D = 384
 
@@ -130,12 +131,12 @@ def test_rowgemm_pair_equals_two_launches(M):
     Wa, ba16 = U.pack_linear(wa, ba)
     Wb, bb16 = U.pack_linear(wb, bb)
     f, g = U.rowgemm_pair(A, Wa, ba16, Wb, bb16)
-    assert torch.equal(f, U.rowgemm(A, Wa, ba16)[1])
-    assert torch.equal(g, U.rowgemm(A, Wb, bb16)[1])
+    assert same(f, U.rowgemm(A, Wa, ba16)[1])
+    assert same(g, U.rowgemm(A, Wb, bb16)[1])
     # device row count (the SoftAgg h GEMM's G): rows past it untouched
     Md = torch.tensor([M // 2], dtype=torch.int64, device="cuda")
     f2, g2 = U.rowgemm_pair(A, Wa, ba16, Wb, bb16, M_dev=Md)
-    assert torch.equal(f2[:M // 2], f[:M // 2]) and torch.equal(g2[:M // 2], g[:M // 2])
+    assert same(f2[:M // 2], f[:M // 2]) and same(g2[:M // 2], g[:M // 2])
 
 
 @pytest.mark.parametrize("M", [1, 127, 3000, 40000])
@@ -152,21 +153,21 @@ def test_kblocked_w_is_bit_identical(M, flags):
     idx = torch.randint(-1, M, (M + 37,), device="cuda")
     want = U.rowgemm(buf, W16, b16, flags=flags, a_idx=idx)[1]
     got = U.rowgemm(buf, U.kblock(W16), b16, flags=flags, a_idx=idx)[1]
-    assert torch.equal(got, want)
+    assert same(got, want)
     Md = torch.tensor([(M + 1) // 2], dtype=torch.int64, device="cuda")
     out = torch.full_like(want, 7.0)
     U.rowgemm(buf, U.kblock(W16), b16, flags=flags, a_idx=idx, out16=out, M_dev=Md)
     h = (M + 1) // 2
-    assert torch.equal(out[:h], want[:h]) and bool((out[h:] == 7.0).all())
+    assert same(out[:h], want[:h]) and bool((out[h:] == 7.0).all())
     A = torch.randn(M, D, device="cuda").half()
     (Wa, ba), (Wb, bb) = U.pack_linear(*lin(D, 8)), U.pack_linear(*lin(D, 9))
     # K = 384 with a device row count: the small-M kernel (the SoftAgg h Linear)
     want = U.rowgemm(A, Wa, ba, flags=flags)[1]
     out = torch.full_like(want, 7.0)
     U.rowgemm(A, U.kblock(Wa), ba, flags=flags, out16=out, M_dev=Md)
-    assert torch.equal(out[:h], want[:h]) and bool((out[h:] == 7.0).all())
+    assert same(out[:h], want[:h]) and bool((out[h:] == 7.0).all())
     f, g = U.rowgemm_pair(A, U.kblock(Wa), ba, U.kblock(Wb), bb)
-    assert torch.equal(f, U.rowgemm(A, Wa, ba)[1]) and torch.equal(g, U.rowgemm(A, Wb, bb)[1])
+    assert same(f, U.rowgemm(A, Wa, ba)[1]) and same(g, U.rowgemm(A, Wb, bb)[1])
     with pytest.raises(RuntimeError):
         U.rowgemm(A, U.kblock(Wa), ba, flags=U.RES, res32=torch.zeros(M, D, device="cuda"))
 
@@ -201,8 +202,8 @@ def test_rowadd_ln():
     s32, s16 = U.rowadd_ln(a, hk, jx, want16=False)[0], U.rowadd_ln(a, hk, jx, want32=False)[1]
     r32, r16 = U.rowadd_ln(s32, h2, ix2, ln=(g, be, 1e-3))
     c32, c16 = U.rowadd_ln(a, hk, jx, ln=(g, be, 1e-3), c16=h2, c_idx=ix2)
-    assert torch.equal(c32, r32) and torch.equal(c16, r16)
-    assert torch.equal(s16, U.rowadd_ln(a, hk, jx)[1])
+    assert same(c32, r32) and same(c16, r16)
+    assert same(s16, U.rowadd_ln(a, hk, jx)[1])
 
 
 def test_errors():
@@ -275,8 +276,8 @@ def test_fused_update_operator_context_index_is_the_gathered_context():
     with torch.no_grad(), torch.autocast("cuda", enabled=True):
         a = upd(net, ring[:, idx], corr, None, ii, jj, kk)
         b = upd(net, ring, corr, None, ii, jj, kk, inp_idx=idx)
-    assert torch.equal(a[0], b[0])
-    assert torch.equal(a[1][0], b[1][0]) and torch.equal(a[1][1], b[1][1])
+    assert same(a[0], b[0])
+    assert same(a[1][0], b[1][0]) and same(a[1][1], b[1][1])
 
 
 @pytest.mark.parametrize("big", [False, True])
@@ -313,7 +314,7 @@ def test_rowchain_is_two_rowgemms(case, big):
     for r, g in zip(ref, got):
         assert (r is None) == (g is None)
         if r is not None:
-            assert torch.equal(r, g)
+            assert same(r, g)
 
 
 @pytest.mark.parametrize("flags1,M", [("relu", 2048 * 128 + 77), ("sigmoid", 3000), ("none", 3000)])
@@ -338,7 +339,7 @@ def test_rowchain_gather_many_tiles_and_runtime_activation(flags1, M):
     for r, g in zip(ref, got):
         assert (r is None) == (g is None)
         if r is not None:
-            assert torch.equal(r, g)
+            assert same(r, g)
 
 
 @pytest.mark.parametrize("M", [1, 1000, 50000])
@@ -366,7 +367,7 @@ def test_rowchain_gated_is_gate_gemm_plus_chain(M, last):
     for r, g in zip(ref, got):
         assert (r is None) == (g is None)
         if r is not None:
-            assert torch.equal(r, g)
+            assert same(r, g)
     with pytest.raises(RuntimeError):
         U.rowchain(A, W1, b1, W2, b2, flags1=U.RELU, gate16=g16, gate=(Wg, bg), **kw)
 
@@ -399,7 +400,7 @@ def test_rowchain3_is_chain_plus_rowgemm(M, gathered):
     for r, g in zip(ref, got):
         assert (r is None) == (g is None)
         if r is not None:
-            assert torch.equal(r, g)
+            assert same(r, g)
 
 
 def test_update_operator_corr_chain3_is_two_launches():
@@ -421,14 +422,16 @@ def test_update_operator_corr_chain3_is_two_launches():
             outs.append(upd(net, inp, corr, None, ii, jj, kk))
     Update.CORR_CHAIN3 = True
     (a, (da, wa, _)), (b, (db, wb, _)) = outs
-    assert torch.equal(a, b) and torch.equal(da, db) and torch.equal(wa, wb)
+    assert same(a, b) and same(da, db) and same(wa, wb)
 
 
-@pytest.mark.parametrize("M", [1, 300, 20000])
+@pytest.mark.parametrize("M", [1, 300, 20000, 70000, 95424])
 def test_rowgemm_pair_pre_equals_rowadd_then_pair(M):
     """dpvo_rowgemm_pair_pre (A rows fp16(a32 + b16[idx]) formed while staged)
     is bit-identical to rowadd_ln(a32, b16, idx, want32=False) feeding
-    rowgemm_pair, including out-of-range indices (no addend) and rows past M."""
+    rowgemm_pair, including out-of-range indices (no addend) and rows past M.
+    M = 70000 / 95424 (C3's edge count) give a block several tiles, so the
+    addend sources come from the LDS table."""
     import update_ops as U
     g = torch.Generator().manual_seed(M)
     a32 = torch.randn(M, D, generator=g).cuda()
@@ -445,4 +448,4 @@ def test_rowgemm_pair_pre_equals_rowadd_then_pair(M):
     _, n16 = U.rowadd_ln(a32, b16[:G], idx, want32=False)
     f_ref, g_ref = U.rowgemm_pair(n16, Wf, cf, Wg, cg)
     f, gg = U.rowgemm_pair_pre(a32, b16, idx, Wf, cf, Wg, cg, b_rows=G)
-    assert torch.equal(f, f_ref) and torch.equal(gg, g_ref)
+    assert same(f, f_ref) and same(gg, g_ref)

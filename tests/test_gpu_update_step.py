@@ -8,9 +8,10 @@ net.Update on seeded weights, ba.py twice with the fastba argument mapping
 (checked against the C restatement of ba_cuda.cu in the generator)
 and projective_ops.point_cloud on net_inputs.update_step_state(): default.yaml,
 M = 12, a 48-frame buffer, n = 40 keyframes (the 36-slot rings wrap), 5,964
-edges, 2 BA iterations; and at C2's per-update size (update_step_c2_ref.npz:
-M = 96, 47,712 edges, 8 BA iterations, 512 x 384 frames).  Each records two
-runs:
+edges, 2 BA iterations; at C2's per-update size (update_step_c2_ref.npz:
+M = 96, 47,712 edges, 8 BA iterations, 512 x 384 frames); and at C3's, the
+workload bench.py times (update_step_c3_ref.npz: dpvo_2k.yaml, M = 192,
+95,424 edges, 2 BA iterations).  Each records two runs:
   * f64: float64 throughout -- the exact answer for these inputs;
   * r16: the reference's own precisions (fp16 altcorr chain, Update under fp16
     autocast, fp32 BA) -- its distance from f64 is the reference's own error.
@@ -59,7 +60,7 @@ def _tracker(f):
     got = np.stack([NI.checksum(S[k]) for k in sorted(S)])
     np.testing.assert_allclose(got, want, rtol=1e-12, atol=0)   # the generator's inputs, regenerated
     n, M, N, pmem = C["n"], C["M"], C["N"], C["pmem"]
-    cfg = make_cfg("default", BUFFER_SIZE=N, PATCHES_PER_FRAME=M)
+    cfg = make_cfg(C.get("preset", "default"), BUFFER_SIZE=N, PATCHES_PER_FRAME=M)
     cfg.BA_ITERATIONS = C["iters"]
     assert (cfg.REMOVAL_WINDOW, cfg.OPTIMIZATION_WINDOW, cfg.PATCH_LIFETIME) == (22, 10, 13)
     net = VONet()
@@ -100,12 +101,14 @@ def _rms(a, b):
     return float(np.sqrt((d * d).mean()))
 
 
-@pytest.mark.parametrize("which", ["small", "c2"])
+@pytest.mark.parametrize("which", ["small", "c2", "c3"])
 def test_update_step_matches_reference_modules(which):
     """small: M = 12, E = 5,964, 2 BA iterations, delta head x 0.25;
     c2: C2's per-update workload, M = 96, E = 47,712, 8 BA iterations, the
     delta head unscaled (BA stays out of the clamp regimes: touched inverse
-    depths in [0.11, 1.13] in every iteration of the reference run)"""
+    depths in [0.11, 1.13] in every iteration of the reference run);
+    c3: the metric's per-update workload (dpvo_2k.yaml), M = 192, E = 95,424,
+    2 BA iterations -- what bench.py times, pinned end to end"""
     f = _fixture(which)
     slam, S = _tracker(f)
     n, t0 = int(f["n"]), int(f["t0"])
@@ -157,7 +160,7 @@ def test_update_step_matches_reference_modules(which):
         assert mx <= 3.0 * amx and mx <= caps[k], (k, mx, amx)
 
 
-@pytest.mark.parametrize("which", ["small", "c2"])
+@pytest.mark.parametrize("which", ["small", "c2", "c3"])
 def test_update_step_corr_rows_match_exact(which):
     """the tracker's default (matrix-core) altcorr at this state, rows of the
     stacked [E, 882] corr against the exact (fp64-summed) restatement of the
@@ -171,11 +174,7 @@ def test_update_step_corr_rows_match_exact(which):
         ctx, jslot, _, _, order = update_ops.window_group_by(
             slam.pg.ii, slam.pg.jj, slam.pg.kk, slam.M, slam.n - 64, slam.M * slam.pmem, slam.pmem,
             flag=slam._ba_status, jj_order=True)
-        corr = slam.corr(coords, slots=(ctx, jslot), order=order)
-        slam.cfg.STAGED_CORR = True
-        staged = slam.corr(coords, slots=(ctx, jslot)).clone()   # the LDS-staged kernel: the same bits
-        slam.cfg.STAGED_CORR = False
-        assert torch.equal(staged, corr)
+        corr = slam.corr(coords, slots=(ctx, jslot), order=order).clone()   # (a view of the cached buffer)
     torch.cuda.synchronize()
     rows = f["corr_rows"]
     got = corr[0].float().cpu().numpy()[rows].astype(np.float64)

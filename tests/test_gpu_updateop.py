@@ -7,8 +7,9 @@ import pytest
 import torch
 
 from oracle import oracle
+from tests_helpers import same
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("poisoned")]
 
 
 def _case(E, G, D, dtype, seed, empty=()):
@@ -53,7 +54,7 @@ def test_softagg_strided_halves_and_determinism():
     lab = torch.randint(0, G, (E,), device="cuda")
     a = update_ops.softagg(fs[:, :D], fs[:, D:], lab, G)
     b = update_ops.softagg(fs[:, :D], fs[:, D:], lab, G)
-    assert torch.equal(a, b)
+    assert same(a, b)
     want = oracle.softagg(fs[:, :D].double().cpu().numpy(), fs[:, D:].double().cpu().numpy(), lab.cpu().numpy(), G)
     np.testing.assert_allclose(a.double().cpu().numpy(), want, rtol=2e-3, atol=2e-3)
 
@@ -81,7 +82,7 @@ def test_gather_rows(in_dt, out_dt):
     idx = torch.randint(-1, 500, (2000,), generator=g)
     out = update_ops.gather_rows(x.cuda(), idx.cuda(), dtype=out_dt).cpu()
     want = torch.from_numpy(oracle.gather_rows(x.numpy(), idx.numpy())).to(out_dt)
-    assert torch.equal(out, want)
+    assert same(out, want)
 
 
 def test_errors():
@@ -101,7 +102,7 @@ def test_group_by_matches_torch_unique(n, hi):
     gid, offs, perm, G = update_ops.group_by(key)
     uniq, inv = torch.unique(key, return_inverse=True)
     assert int(G.item()) == uniq.numel()
-    assert torch.equal(gid, inv)
+    assert same(gid, inv)
     g = int(G.item())
     offs, perm = offs[: g + 1].long().cpu(), perm.long().cpu()
     assert offs[0] == 0 and offs[-1] == n
@@ -124,10 +125,10 @@ def test_group_by_counting_sort_equals_radix(n, bits, distinct):
     a = update_ops.group_by(key, key_bits=bits)
     b = update_ops.group_by(key, key_bits=bits, radix=True)
     G = int(a[3].item())
-    assert torch.equal(a[3], b[3]) and torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])
-    assert torch.equal(a[1][:G + 1], b[1][:G + 1])   # entries past G are unspecified
+    assert same(a[3], b[3]) and same(a[0], b[0]) and same(a[2], b[2])
+    assert same(a[1][:G + 1], b[1][:G + 1])   # entries past G are unspecified
     uniq, inv = torch.unique(key, return_inverse=True)
-    assert int(a[3].item()) == uniq.numel() and torch.equal(a[0], inv)
+    assert int(a[3].item()) == uniq.numel() and same(a[0], inv)
 
 
 def test_group_by_counting_sort_runs_of_equal_keys():
@@ -141,7 +142,7 @@ def test_group_by_counting_sort_runs_of_equal_keys():
     a = update_ops.group_by(key, key_bits=16)
     b = update_ops.group_by(key, key_bits=16, radix=True)
     G = int(a[3].item())
-    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2]) and torch.equal(a[1][:G + 1], b[1][:G + 1])
+    assert same(a[0], b[0]) and same(a[2], b[2]) and same(a[1][:G + 1], b[1][:G + 1])
 
 
 def test_group_by_empty():
@@ -163,7 +164,7 @@ def test_softagg_csr_matches_oracle_and_dense_path():
     want = oracle.softagg(fs[:, :D].double().cpu().numpy(), fs[:, D:].double().cpu().numpy(), gid.cpu().numpy(), g)
     np.testing.assert_allclose(y.double().cpu().numpy(), want, rtol=2e-3, atol=2e-3)
     dense = update_ops.softagg(fs[:, :D], fs[:, D:], gid, g)
-    assert torch.equal(y, dense)   # same ascending order, same arithmetic
+    assert same(y, dense)   # same ascending order, same arithmetic
 
 
 def test_rowgemm_device_row_count():
@@ -174,7 +175,7 @@ def test_rowgemm_device_row_count():
     out = torch.full((1000, 384), 7.0, device="cuda").half()
     U.rowgemm(A, W16, b16, out16=out, M_dev=torch.tensor([300], device="cuda"))
     _, ref, _ = U.rowgemm(A, W16, b16)
-    assert torch.equal(out[:300], ref[:300])
+    assert same(out[:300], ref[:300])
     assert (out[300:] == 7.0).all()
 
 
@@ -189,7 +190,7 @@ def test_edge_targets_equal_torch_composition():
     delta, weight = heads[None, :, :2], heads[None, :, 2:]
     centre = coords[..., 1, 1]
     t, w = update_ops.edge_targets(centre, delta, weight)
-    assert torch.equal(t, centre + delta.float()) and torch.equal(w, weight.float())
+    assert same(t, centre + delta.float()) and same(w, weight.float())
 
 
 @pytest.mark.parametrize("ngroups", [50, 3000])
@@ -205,8 +206,8 @@ def test_softagg_csr_long_groups(ngroups):
     g = int(G.item())
     y = update_ops.softagg_csr(fs[:, :D], fs[:, D:], offs, perm, G, E, long_groups=True)[:g]
     y2 = update_ops.softagg_csr(fs[:, :D], fs[:, D:], offs, perm, G, E, long_groups=True)[:g]
-    assert torch.equal(y, y2)
+    assert same(y, y2)
     want = oracle.softagg(fs[:, :D].double().cpu().numpy(), fs[:, D:].double().cpu().numpy(), gid.cpu().numpy(), g)
     np.testing.assert_allclose(y.double().cpu().numpy(), want, rtol=2e-3, atol=2e-3)
     if ngroups == 3000:   # ~7 edges per group: the unsplit arithmetic
-        assert torch.equal(y, update_ops.softagg_csr(fs[:, :D], fs[:, D:], offs, perm, G, E)[:g])
+        assert same(y, update_ops.softagg_csr(fs[:, :D], fs[:, D:], offs, perm, G, E)[:g])

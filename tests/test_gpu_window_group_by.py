@@ -3,8 +3,9 @@
 the same slots, flag and both CSRs, bit for bit."""
 import pytest
 import torch
+from tests_helpers import same
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("poisoned")]
 
 
 def separate(ii, jj, kk, M, base, ring, frames, flag=None):
@@ -16,12 +17,12 @@ def separate(ii, jj, kk, M, base, ring, frames, flag=None):
 
 
 def assert_same(got, want):
-    assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1])
+    assert same(got[0], want[0]) and same(got[1], want[1])
     for g, w in ((got[2], want[2]), (got[3], want[3])):
         G = int(w[3].item())
-        assert torch.equal(g[3], w[3])
-        assert torch.equal(g[0], w[0]) and torch.equal(g[2], w[2])
-        assert torch.equal(g[1][:G + 1], w[1][:G + 1])   # offs past the group count is scratch
+        assert same(g[3], w[3])
+        assert same(g[0], w[0]) and same(g[2], w[2])
+        assert same(g[1][:G + 1], w[1][:G + 1])   # offs past the group count is scratch
 
 
 @pytest.mark.parametrize("preset,buffer,n", [("fast", 96, 70), ("dpvo_2k", 2048, 2040)])
@@ -58,7 +59,7 @@ def test_random_window_edges(E, M, seed):
     got = update_ops.window_group_by(*args, jj_order=True)
     assert_same(got[:4], separate(*args))
     order = got[4].long()
-    assert torch.equal(torch.sort(order).values, torch.arange(E, device="cuda"))
+    assert same(torch.sort(order).values, torch.arange(E, device="cuda"))
     assert bool((jj[order][1:] >= jj[order][:-1]).all())
 
 

@@ -124,10 +124,11 @@ def test_encoder_mirror_float64_matches_reference(frame):
     np.testing.assert_allclose(imap[:, ys, xs].T, f[f"f{frame}_imap"], rtol=1e-5, atol=1e-6)
 
 
-@pytest.mark.parametrize("which", ["small", "c2"])
+@pytest.mark.parametrize("which", ["small", "c2", "c3"])
 def test_update_step_inputs_regenerate(which):
-    """update_step_ref.npz's (M = 12) and update_step_c2_ref.npz's (C2's
-    per-update size, M = 96, 8 BA iterations) inputs come back bit for bit
+    """update_step_ref.npz's (M = 12), update_step_c2_ref.npz's (C2's
+    per-update size, M = 96, 8 BA iterations) and update_step_c3_ref.npz's
+    (C3's, M = 192, 2 BA iterations) inputs come back bit for bit
     from their seed (the GPU test regenerates them instead of loading the
     state), and each fixture's edge set is the steady state the tracker sees
     (497 M edges)"""

@@ -87,3 +87,44 @@ def global_state(seed, n=160, M=6):
     jj = np.repeat(je, M)
     kk = (ie[:, None] * M + np.arange(M)[None]).reshape(-1).astype(np.int64)
     return with_edges(g, n, M, poses, patches, intrinsics, ii, jj, kk)
+
+
+def first_diff(a, b):
+    """None when a and b hold the same bits (NaNs compared by pattern), else a
+    message naming the first differing element: flat index, its coordinates
+    and both values."""
+    import torch
+    if a.shape != b.shape or a.dtype != b.dtype:
+        return f"shape / dtype {tuple(a.shape)} {a.dtype} vs {tuple(b.shape)} {b.dtype}"
+    x, y = a.detach().contiguous().reshape(-1), b.detach().contiguous().reshape(-1)
+    if x.dtype.is_floating_point:
+        ib = {2: torch.int16, 4: torch.int32, 8: torch.int64}[x.element_size()]
+        x, y = x.view(ib), y.view(ib)
+    ne = (x != y).nonzero()
+    if ne.numel() == 0:
+        return None
+    i = int(ne[0, 0])
+    coord = np.unravel_index(i, tuple(a.shape)) if a.dim() else ()
+    av, bv = a.reshape(-1)[i].item(), b.reshape(-1)[i].item()
+    return (f"{ne.shape[0]} of {x.numel()} elements differ; first at flat {i}, index "
+            f"{tuple(int(c) for c in coord)}: {av!r} vs {bv!r}")
+
+
+def assert_same_bits(a, b, what="tensor"):
+    msg = first_diff(a, b)
+    assert msg is None, f"{what}: {msg}"
+
+
+def same(a, b, what="tensor"):
+    """torch.equal for the bit-identity tests: True, or an AssertionError that
+    names the first differing element (first_diff).  Tensors of different
+    dtypes fall back to torch.equal's value comparison."""
+    import torch
+    if a.dtype != b.dtype:
+        if not torch.equal(a, b):
+            raise AssertionError(f"{what}: values differ ({a.dtype} vs {b.dtype})")
+        return True
+    msg = first_diff(a, b)
+    if msg is not None:
+        raise AssertionError(f"{what}: {msg}")
+    return True

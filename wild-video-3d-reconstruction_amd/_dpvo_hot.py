@@ -41,9 +41,6 @@ _SIGNATURES = {
     "dpvo_corr_pack_mfma_bytes": (_sz, [_vp]),
     "dpvo_corr_pack_mfma": (_ip, [_vp, _vp, _vp, _vp, _vp]),
     "dpvo_corr_pyramid_mfma": (_ip, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _vp]),
-    "dpvo_corr_staged_workspace_bytes": (_sz, [_i64, _i64, _i64, _i64]),
-    "dpvo_corr_pyramid_staged": (_ip, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _sz,
-                                       _vp]),
     "dpvo_edge_order_workspace_bytes": (_sz, [_ip]),
     "dpvo_edge_order": (_ip, [_vp, _i64, _ip, _vp, _vp, _sz, _vp]),
     "dpvo_corr_backward": (_ip, [_ip, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _ip, _vp, _vp, _vp]),
@@ -142,12 +139,14 @@ def parse_build_info(info):
 
 def verify_build(info, src_sha, diag=False):
     """Refuse a library built from other sources than the ones beside it, or
-    the stamped diagnostic build unless diag (DPVO_DIAG=1).  Returns the
-    parsed info."""
+    a diagnostic / experiment build (in-kernel stamps, scripts/build_exp.sh)
+    unless diag (DPVO_DIAG=1).  With diag a non-product build may come from
+    other sources (an experiment's A/B variant); the product never.  Returns
+    the parsed info."""
     b = parse_build_info(info)
     if "sha" not in b or "flavour" not in b:
         raise ImportError(f"libdpvo_hot.so reports no build provenance ({info!r}): rebuild it (make -B)")
-    if src_sha is not None and b["sha"] != src_sha:
+    if src_sha is not None and b["sha"] != src_sha and not (diag and b["flavour"] != "product"):
         raise ImportError(f"libdpvo_hot.so is stale: built from sources sha={b['sha']}, the tree holds "
                           f"sha={src_sha}; rebuild it (__graft_entry__.build())")
     if b["flavour"] != "product" and not diag:
@@ -213,6 +212,42 @@ def sizes(t):
 
 def strides(t):
     return i64arr(t.stride())
+
+
+# Debug switch: fill every device buffer the shims allocate uninitialised
+# (kernel outputs and workspaces) with one byte pattern before the kernel
+# sees it -- 0xff is NaN in fp16 / fp32 / fp64 and -1 in the integer types.
+# A kernel that reads memory it never wrote then gives different bits under
+# two patterns (tests/test_gpu_update_async.py).  DPVO_POISON=0xff at import,
+# or set_poison(byte) / set_poison(None).
+_POISON = None
+
+
+def set_poison(byte):
+    """byte pattern (0..255) for every buffer empty() hands out, None = off"""
+    global _POISON
+    _POISON = None if byte is None else int(byte) & 0xFF
+
+
+def poison():
+    return _POISON
+
+
+if os.environ.get("DPVO_POISON"):
+    set_poison(int(os.environ["DPVO_POISON"], 0))
+
+
+def empty(*size, dtype=torch.float32, device=None):
+    """torch.empty, poisoned under set_poison() (device tensors only)"""
+    t = torch.empty(*size, dtype=dtype, device=device)
+    if _POISON is not None and t.is_cuda and t.numel():
+        t.view(torch.uint8).fill_(_POISON)
+    return t
+
+
+def new_empty(like, *size):
+    """like.new_empty(*size) through empty()"""
+    return empty(*size, dtype=like.dtype, device=like.device)
 
 
 def idx64(t):

@@ -6,7 +6,9 @@
 #ifndef DPVO_SRC_SHA
 #error "DPVO_SRC_SHA must be defined by the build (see Makefile)"
 #endif
-#ifdef DPVO_STAMPS
+#if defined(DPVO_EXP_FLAVOUR)
+#define DPVO_FLAVOUR DPVO_EXP_FLAVOUR   // experiment builds (scripts/build_exp.sh): refused unless DPVO_DIAG=1
+#elif defined(DPVO_STAMPS)
 #define DPVO_FLAVOUR "stamps"
 #else
 #define DPVO_FLAVOUR "product"

@@ -44,22 +44,19 @@ __device__ __forceinline__ void cm_wave_fence()
 // eighth of the (target-frame-grouped) edge sequence, walked by all of its
 // waves in step, so an XCD streams through a few target frames' maps instead
 // of every XCD touching every frame.
-// Slots [begin, E) of the order (begin > 0: the tail of a staged launch's
-// order, dpvo_corr_pyramid_staged's fallback edges).
 struct CmRange { int slot, end, stride; };
-__device__ __forceinline__ CmRange cm_range(int begin, int E, int wave)
+__device__ __forceinline__ CmRange cm_range(int E, int wave)
 {
     const int nblk = gridDim.x, b = blockIdx.x;
-    const int n = E - begin;
     CmRange r;
     if (nblk >= 8 && (nblk & 7) == 0) {
         const int x = b & 7, per = nblk >> 3;
-        const int lo = begin + (int)((int64_t)n * x / 8);
-        r.end = begin + (int)((int64_t)n * (x + 1) / 8);
+        const int lo = (int)((int64_t)E * x / 8);
+        r.end = (int)((int64_t)E * (x + 1) / 8);
         r.slot = lo + (b >> 3) * cm::WAVES + wave;
         r.stride = per * cm::WAVES;
     } else {
-        r.slot = begin + b * cm::WAVES + wave;
+        r.slot = b * cm::WAVES + wave;
         r.end = E;
         r.stride = nblk * cm::WAVES;
     }
@@ -72,6 +69,13 @@ __device__ __forceinline__ CmRange cm_range(int begin, int E, int wave)
 //   m[2h]     = even lane: l[2h] (own)        odd lane: l[2h+1] of lane - 1
 //   m[2h + 1] = even lane: l[2h] of lane + 1  odd lane: l[2h+1] (own)
 // (DPP quad_perm(0,0,2,2) / (1,1,3,3) fetch the pair partner's register).
+// The DPP moves carry no "old" operand (every lane of a quad_perm is
+// written): a DPP move and a select per dword.  (update_dpp with an explicit
+// old value of 0 cost a v_mov of that 0 as well: with the OOB change in the
+// tile loads below, the loop went from ~98 to ~74 VALU instructions per tile,
+// 0.364 -> 0.354 ms at C3, bit-identical.  Folding the DPP into the select
+// (v_cndmask_b32_dpp, 58 per tile) measured no faster: the loop is not bound
+// by VALU issue alone; profiles/r6/NOTES.md.)
 __device__ __forceinline__ void cm_pair_operands(const h8_t* l, h8_t* m, bool odd)
 {
     typedef unsigned u4_t __attribute__((ext_vector_type(4)));
@@ -81,8 +85,8 @@ __device__ __forceinline__ void cm_pair_operands(const h8_t* l, h8_t* m, bool od
         u4_t m0, m1;
 #pragma unroll
         for (int d = 0; d < 4; d++) {
-            const unsigned from_o = (unsigned)__builtin_amdgcn_update_dpp(0, (int)o[d], 0xA0, 0xF, 0xF, false);
-            const unsigned from_e = (unsigned)__builtin_amdgcn_update_dpp(0, (int)e[d], 0xF5, 0xF, 0xF, false);
+            const unsigned from_o = (unsigned)__builtin_amdgcn_mov_dpp((int)o[d], 0xA0, 0xF, 0xF, false);
+            const unsigned from_e = (unsigned)__builtin_amdgcn_mov_dpp((int)e[d], 0xF5, 0xF, 0xF, false);
             m0[d] = odd ? from_o : e[d];
             m1[d] = odd ? o[d] : from_e;
         }
@@ -158,7 +162,7 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
     __shared__ int ebase[WAVES][2][16];      // window origin of each patch pixel inside its raw row
     __shared__ int estr[WAVES][2];           // raw row stride of the window (box width, or 8)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const CmRange rg = cm_range(p.dev_begin ? *p.dev_begin : 0, p.E, wave);
+    const CmRange rg = cm_range(p.E, wave);
     int slot = rg.slot;
     if (slot >= rg.end) return;   // the whole wave; nothing below synchronises across waves
     float* rw = raw[wave];
@@ -305,16 +309,17 @@ __global__ __launch_bounds__(64 * cm::WAVES) void corr_mfma_kernel(CorrMfmaParam
             fc.tl++;
             const __amdgpu_buffer_rsrc_t rs =
                 __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(fc.frame), (short)0, fc.num, 0x00020000);
-            // full-line loads (see cm_pair_operands): the lane pair's even / odd pixel
-            const int pe = __builtin_amdgcn_update_dpp(0, pix, 0xA0, 0xF, 0xF, false);   // quad_perm(0,0,2,2)
-            const int po = __builtin_amdgcn_update_dpp(0, pix, 0xF5, 0xF, 0xF, false);   // quad_perm(1,1,3,3)
+            // full-line loads (see cm_pair_operands): the lane pair's even / odd
+            // pixel, + the lane's 16-byte chunk.  An out-of-map pixel's OOB
+            // (2^31) plus the chunk (< 256) stays past every descriptor's range
+            // (frameext < 2^31 - 256, corr_mfma_setup), so it needs no select
+            // of its own, and the 128-byte half goes to the immediate offset.
             const unsigned ch = 16u * (unsigned)((q16 & 1) * 4 + kc);
+            const unsigned pe = (unsigned)__builtin_amdgcn_mov_dpp(pix, 0xA0, 0xF, 0xF, false) + ch;   // quad_perm(0,0,2,2)
+            const unsigned po = (unsigned)__builtin_amdgcn_mov_dpp(pix, 0xF5, 0xF, 0xF, false) + ch;   // quad_perm(1,1,3,3)
 #pragma unroll
-            for (int ks = 0; ks < 4; ks++) {
-                const unsigned b = (unsigned)((ks & 1) ? po : pe);
-                const unsigned o = b == OOB ? OOB : b + 128u * (ks >> 1) + ch;
-                a[ks] = __builtin_bit_cast(h8_t, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
-            }
+            for (int ks = 0; ks < 4; ks++)
+                a[ks] = __builtin_bit_cast(h8_t, __builtin_amdgcn_raw_buffer_load_b128(rs, ((ks & 1) ? po : pe) + 128u * (ks >> 1), 0, 0));
         };
         int clev = 0, ctl = 0, cntl = L0.ntiles;
         auto consume = [&](int t, const h8_t* a) {

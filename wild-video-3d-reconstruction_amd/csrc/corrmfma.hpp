@@ -1,7 +1,6 @@
-// corrmfma.hpp -- the matrix-core altcorr's parameters, shared by
-// corrmfma.hip (one wave per edge, windows read through the vector-memory
-// path) and corrstage.hip (target-frame windows staged in LDS; its fallback
-// edges run corr_mfma_kernel).
+// corrmfma.hpp -- the matrix-core altcorr's parameters and its bilinear
+// step (corrmfma.hip: one wave per edge, windows read through the
+// vector-memory path).
 #pragma once
 
 #include "common.hpp"
@@ -34,12 +33,11 @@ struct CorrMfmaParams {
     half_t* out;
     int64_t o_e;
     const int* order;   // optional edge visiting order (edges grouped by target frame), NULL = 0..E-1
-    const int* dev_begin;   // optional: visit order slots [*dev_begin, E) only (read on the device)
 };
 
 // The fp32 bilinear 8x8 -> 7x7 step of one output (correlation_kernel.cu:221-232's
-// four terms) as one explicit chain, so every kernel computing it (per-edge
-// and staged) rounds identically whatever the compiler would contract:
+// four terms) as one explicit chain, so it rounds the same way whatever the
+// compiler would contract:
 // w = {(1-dx)(1-dy), dx(1-dy), (1-dx)dy, dx dy}, r = the 2 x 2 products
 __device__ __forceinline__ float cm_bilinear(float w0, float w1, float w2, float w3, float r00, float r01, float r10,
                                              float r11)
@@ -47,7 +45,7 @@ __device__ __forceinline__ float cm_bilinear(float w0, float w1, float w2, float
     float v = __builtin_fmaf(w3, r11, __builtin_fmaf(w2, r10, __builtin_fmaf(w1, r01, w0 * r00)));
     // an fp32 value, rounded to fp16 by the caller's conversion: without this
     // the compiler may fuse the last fma into the conversion (v_fma_mix*_f16:
-    // one rounding instead of two -- other bits than the per-edge kernel's)
+    // one rounding instead of two)
     asm volatile("" : "+v"(v));
     return v;
 }
@@ -57,7 +55,7 @@ int corr_mfma_setup(CorrMfmaParams& p, const void* table, int64_t num_patches, c
                     const int64_t* fmap_sizes, const int64_t* fmap_strides, const float* level_scale,
                     const float* coords, const int64_t* coords_size, const int64_t* coords_stride, const int64_t* ii,
                     const int64_t* jj, void* corr, int64_t edge_stride, const int* order);
-// corr_mfma_kernel over the order's slots (p.dev_begin: from a device-side start)
+// corr_mfma_kernel over the order's slots
 int corr_mfma_launch(const CorrMfmaParams& p, hipStream_t s);
 
 }  // namespace dpvo

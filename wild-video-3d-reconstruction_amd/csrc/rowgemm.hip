@@ -1197,9 +1197,16 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
 #endif
         const bool more = tile + G < ntiles;
         // ---- GEMM1 (+ OVL: the previous tile's row epilogue, rows 16 w .. 16 w + 15
-        // in 8 batches of 2: batch b's loads after k-step L(b) = b (nk1 - 3) / 7,
-        // its arithmetic after k-step L(b) + 1 <= nk1 - 2, before the last
-        // k-step's barrier)
+        // in 8 batches of 2: batch b's loads after k-step L(b) = b (nk1 - 4) / 7,
+        // its y-tile reads and arithmetic after k-step L(b) + 1 <= nk1 - 3.
+        // Barriers come at the even k-steps only, so the last batch must finish
+        // before the barrier of k-step nk1 - 2: that barrier is the only one
+        // between a wave's last read of tile t's y rows and the other waves'
+        // acc_to_y writes of tile t + 1 after k-step nk1 - 1.  (Round 4 to 5
+        // scheduled the last batch's reads after k-step nk1 - 2, with no barrier
+        // before those writes: a wave running ahead could overwrite y-tile
+        // columns a slower wave had not read yet -- the intermittent last-bit
+        // differences of the round-5 graph-replay test.)
         {
             EpiOps2<2> st;
             int bi = 0, bd = 0;
@@ -1212,7 +1219,7 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
                     bd++;
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                if (bi < 8 && (bi * (nk1 - 3)) / 7 == ks) {
+                if (bi < 8 && (bi * (nk1 - 4)) / 7 == ks) {
                     epi_issue(etile, 16 * w + 2 * bi, st);
                     bi++;
                 }

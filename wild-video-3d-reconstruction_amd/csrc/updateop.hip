@@ -109,6 +109,41 @@ template <> struct Pair<double> {
     static __device__ __forceinline__ void store(double* p, float2_t v) { p[0] = v.x; p[1] = v.y; }
 };
 
+// Online softmax-weighted sum over rows order[i0 .. i1) for the lane's two
+// channels, in SA_UNROLL batches from i0 (sa_reduce_csr_kernel's arithmetic).
+template <typename T>
+__device__ __forceinline__ void sa_online(const T* __restrict__ f, int64_t ldf, const T* __restrict__ s, int64_t lds,
+                                          const int* order, int i0b, int i1, int cc, float2_t& m, float2_t& l,
+                                          float2_t& acc)
+{
+    for (int i0 = i0b; i0 < i1; i0 += SA_UNROLL) {
+        float2_t sv[SA_UNROLL], fv[SA_UNROLL];
+#pragma unroll
+        for (int u = 0; u < SA_UNROLL; u++) {
+            const int64_t e = order[min(i0 + u, i1 - 1)];
+            sv[u] = Pair<T>::load(s + e * lds + cc);
+            fv[u] = Pair<T>::load(f + e * ldf + cc);
+        }
+        float2_t mb = m;
+#pragma unroll
+        for (int u = 0; u < SA_UNROLL; u++)
+            if (i0 + u < i1) {
+                mb.x = fmaxf(mb.x, sv[u].x);
+                mb.y = fmaxf(mb.y, sv[u].y);
+            }
+        const float ax = __expf(m.x - mb.x), ay = __expf(m.y - mb.y);
+        l.x *= ax; l.y *= ay; acc.x *= ax; acc.y *= ay;
+#pragma unroll
+        for (int u = 0; u < SA_UNROLL; u++)
+            if (i0 + u < i1) {
+                const float px = __expf(sv[u].x - mb.x), py = __expf(sv[u].y - mb.y);
+                l.x += px; l.y += py;
+                acc.x += px * fv[u].x; acc.y += py * fv[u].y;
+            }
+        m = mb;
+    }
+}
+
 // One wave per (group, 128-channel slice).  Lane owns channels c, c+1.
 template <typename T>
 __global__ __launch_bounds__(64 * SA_WAVES) void sa_reduce_kernel(const T* __restrict__ f, int64_t ldf,
@@ -124,15 +159,24 @@ __global__ __launch_bounds__(64 * SA_WAVES) void sa_reduce_kernel(const T* __res
     const int64_t g = task / slices;
     const int c = (int)(task % slices) * 128 + 2 * lane;
     const int b = offs[g], S = offs[g + 1] - b;
+    const bool act = c < D;
+    const int cc = act ? c : 0;
+    float2_t m = {-INFINITY, -INFINITY}, l = {0.f, 0.f}, acc = {0.f, 0.f};
 
-    // ascending edge order within the group (ranks of distinct edge ids)
-    const int* order = perm + b;
+    // ascending edge order within the group (ranks of distinct edge ids).  The
+    // online pass is instantiated once per source of the order -- the wave's
+    // LDS list or global perm -- never through one pointer that may be either:
+    // such a generic pointer compiles to flat loads, and a flat load of the
+    // LDS list is not ordered after the ds_write that stored it (another lane's
+    // rank), so the pass could read a stale slot of the sorted list -- the
+    // round-5 intermittent "csr != dense" SoftAgg mismatch.
     if (S <= SA_CAP) {
         int* raw = lst[w][0];
         int* srt = lst[w][1];
         for (int i = lane; i < S; i += 64) raw[i] = perm[b + i];
-        __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         for (int i = lane; i < S; i += 64) {
             const int v = raw[i];
             int r = 0;
@@ -141,41 +185,10 @@ __global__ __launch_bounds__(64 * SA_WAVES) void sa_reduce_kernel(const T* __res
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        order = srt;
-    }
-    const bool act = c < D;
-    const int cc = act ? c : 0;
-
-    float2_t m = {-INFINITY, -INFINITY}, l = {0.f, 0.f}, acc = {0.f, 0.f};
-    for (int i0 = 0; i0 < S; i0 += SA_UNROLL) {
-        float2_t sv[SA_UNROLL], fv[SA_UNROLL];
-#pragma unroll
-        for (int u = 0; u < SA_UNROLL; u++) {
-            const int i = min(i0 + u, S - 1);
-            const int64_t e = order[i];
-            sv[u] = Pair<T>::load(s + e * lds + cc);
-            fv[u] = Pair<T>::load(f + e * ldf + cc);
-        }
-        float2_t mb = m;
-#pragma unroll
-        for (int u = 0; u < SA_UNROLL; u++) {
-            if (i0 + u < S) {
-                mb.x = fmaxf(mb.x, sv[u].x);
-                mb.y = fmaxf(mb.y, sv[u].y);
-            }
-        }
-        // rescale the running sums once per batch (exp(-inf) = 0 on the first)
-        const float ax = __expf(m.x - mb.x), ay = __expf(m.y - mb.y);
-        l.x *= ax; l.y *= ay; acc.x *= ax; acc.y *= ay;
-#pragma unroll
-        for (int u = 0; u < SA_UNROLL; u++) {
-            if (i0 + u < S) {
-                const float px = __expf(sv[u].x - mb.x), py = __expf(sv[u].y - mb.y);
-                l.x += px; l.y += py;
-                acc.x += px * fv[u].x; acc.y += py * fv[u].y;
-            }
-        }
-        m = mb;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        sa_online<T>(f, ldf, s, lds, srt, 0, S, cc, m, l, acc);
+    } else {
+        sa_online<T>(f, ldf, s, lds, perm + b, 0, S, cc, m, l, acc);
     }
     if (act) Pair<T>::store(y + g * (int64_t)D + c, float2_t{acc.x / (l.x + eps), acc.y / (l.y + eps)});
 }
@@ -493,41 +506,6 @@ __global__ __launch_bounds__(256) void sa_reduce_csr_kernel(const T* __restrict_
             m = mb;
         }
         if (act) Pair<T>::store(y + g * (int64_t)D + c, float2_t{acc.x / (l.x + eps), acc.y / (l.y + eps)});
-    }
-}
-
-// Online softmax-weighted sum over rows order[i0 .. i1) for the lane's two
-// channels, in SA_UNROLL batches from i0 (sa_reduce_csr_kernel's arithmetic).
-template <typename T>
-__device__ __forceinline__ void sa_online(const T* __restrict__ f, int64_t ldf, const T* __restrict__ s, int64_t lds,
-                                          const int* order, int i0b, int i1, int cc, float2_t& m, float2_t& l,
-                                          float2_t& acc)
-{
-    for (int i0 = i0b; i0 < i1; i0 += SA_UNROLL) {
-        float2_t sv[SA_UNROLL], fv[SA_UNROLL];
-#pragma unroll
-        for (int u = 0; u < SA_UNROLL; u++) {
-            const int64_t e = order[min(i0 + u, i1 - 1)];
-            sv[u] = Pair<T>::load(s + e * lds + cc);
-            fv[u] = Pair<T>::load(f + e * ldf + cc);
-        }
-        float2_t mb = m;
-#pragma unroll
-        for (int u = 0; u < SA_UNROLL; u++)
-            if (i0 + u < i1) {
-                mb.x = fmaxf(mb.x, sv[u].x);
-                mb.y = fmaxf(mb.y, sv[u].y);
-            }
-        const float ax = __expf(m.x - mb.x), ay = __expf(m.y - mb.y);
-        l.x *= ax; l.y *= ay; acc.x *= ax; acc.y *= ay;
-#pragma unroll
-        for (int u = 0; u < SA_UNROLL; u++)
-            if (i0 + u < i1) {
-                const float px = __expf(sv[u].x - mb.x), py = __expf(sv[u].y - mb.y);
-                l.x += px; l.y += py;
-                acc.x += px * fv[u].x; acc.y += py * fv[u].y;
-            }
-        m = mb;
     }
 }
 

@@ -75,7 +75,7 @@ def forward(poses, patches, intrinsics, target, weight, lmbda, ii, jj, kk, t0, t
     N = int(t1) - int(t0)
     flags = (1 if SPARSE else 0) | (0 if DETERMINISTIC else 2) | (4 if keep_status and status is not None else 0)
     nbytes = H.lib().dpvo_ba_workspace_bytes_ex(E, num_patches, max(N, 0), flags)
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=poses.device)
+    ws = H.empty(nbytes, dtype=torch.uint8, device=poses.device)
     deferred = status is not None
     if deferred:
         if status.dtype != torch.int32 or status.numel() < 1 or status.device != poses.device:
@@ -104,11 +104,11 @@ def neighbors(ii, jj):
     H.on_gpu(ii, jj)
     ii, jj = H.idx64(ii), H.idx64(jj)
     E = ii.numel()
-    ix = torch.empty(E, dtype=torch.int64, device=ii.device)
-    jx = torch.empty(E, dtype=torch.int64, device=ii.device)
+    ix = H.empty(E, dtype=torch.int64, device=ii.device)
+    jx = H.empty(E, dtype=torch.int64, device=ii.device)
     if E:
         nbytes = H.lib().dpvo_neighbors_workspace_bytes(E)
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=ii.device)
+        ws = H.empty(nbytes, dtype=torch.uint8, device=ii.device)
         H.check(H.lib().dpvo_neighbors(H.ptr(ii), H.ptr(jj), E, H.ptr(ix), H.ptr(jx), H.ptr(ws), nbytes,
                                        H.stream_of(ii)))
     return [ix, jx]
@@ -121,7 +121,7 @@ def reproject(poses, patches, intrinsics, ii, jj, kk):
     P = patches.shape[-1]
     ii, jj, kk = H.idx64(ii), H.idx64(jj), H.idx64(kk)
     E = ii.numel()
-    out = torch.empty((E, 2, P, P), dtype=torch.float32, device=poses.device)
+    out = H.empty((E, 2, P, P), dtype=torch.float32, device=poses.device)
     H.check(H.lib().dpvo_reproject(H.ptr(poses), H.ptr(patches), P, H.ptr(intrinsics), H.ptr(ii), H.ptr(jj),
                                    H.ptr(kk), E, H.ptr(out), H.stream_of(poses)))
     return out.view(1, E, 2, P, P)
@@ -152,8 +152,8 @@ def solve_system(J_Ginv_i, J_Ginv_j, ii, jj, res, ep, lm, freen):
         raise RuntimeError("solve_system: J_Ginv_i/J_Ginv_j must be [r, 7, 7], ii/jj [r], res [r, 7]")
     n = int(torch.maximum(ii.max(), jj.max()).item()) + 1 if r else 0
     m = 7 * n if int(freen) < 0 else min(7 * int(freen), 7 * n)
-    A = torch.empty(m, m, dtype=torch.float64, device=dev)
-    b = torch.empty(m, dtype=torch.float64, device=dev)
+    A = H.empty(m, m, dtype=torch.float64, device=dev)
+    b = H.empty(m, dtype=torch.float64, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
     H.check(H.lib().dpvo_solve_system_assemble(H.ptr(Ji), H.ptr(Jj), H.ptr(ii), H.ptr(jj), H.ptr(rr), r, m,
                                                float(ep), float(lm), H.ptr(A), H.ptr(b), H.ptr(status),

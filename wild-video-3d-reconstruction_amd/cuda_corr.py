@@ -25,7 +25,7 @@ def forward(fmap1, fmap2, coords, ii, jj, radius):
     _check_corr_args(fmap1, fmap2, coords, ii, jj)
     B, E, _, Hh, W = coords.shape
     Do = 2 * radius + 1
-    out = torch.empty((B, E, Do, Do, Hh, W), dtype=fmap1.dtype, device=fmap1.device)
+    out = H.empty((B, E, Do, Do, Hh, W), dtype=fmap1.dtype, device=fmap1.device)
     ii, jj = H.idx64(ii), H.idx64(jj)
     H.check(H.lib().dpvo_corr_forward(
         H.dtype_code(fmap1), H.ptr(fmap1), H.sizes(fmap1), H.strides(fmap1), H.ptr(fmap2), H.sizes(fmap2),
@@ -42,7 +42,7 @@ def pack(fmap1, out=None):
         raise RuntimeError("pack: fmap1 must be an fp16 [B, N1, C, 3, 3] tensor")
     nbytes = H.lib().dpvo_corr_table_bytes(H.sizes(fmap1))
     if out is None or out.numel() * out.element_size() < nbytes:
-        out = torch.empty((nbytes + 3) // 4, dtype=torch.int32, device=fmap1.device)
+        out = H.empty((nbytes + 3) // 4, dtype=torch.int32, device=fmap1.device)
     H.check(H.lib().dpvo_corr_pack(H.ptr(fmap1), H.sizes(fmap1), H.strides(fmap1), H.ptr(out), H.stream_of(fmap1)))
     return out
 
@@ -58,7 +58,7 @@ def forward_pyramid(fmap1, pyramid, coords, ii, jj, radius, scales, out=None, ta
     Do = 2 * radius + 1
     F = Do * Do * Hh * W * L
     if out is None:
-        out = torch.empty((B, E, F), dtype=fmap1.dtype, device=fmap1.device)
+        out = H.empty((B, E, F), dtype=fmap1.dtype, device=fmap1.device)
     elif (out.shape != (B, E, F) or out.dtype != fmap1.dtype or out.stride(2) != 1 or
           (B > 1 and out.stride(0) != E * out.stride(1))):
         raise RuntimeError("forward_pyramid: out must be [B, E, F] with unit feature stride")
@@ -82,7 +82,7 @@ def pack_mfma(fmap1, out=None):
         raise RuntimeError("pack_mfma: fmap1 must be an fp16 [1, N1, 128, 3, 3] tensor")
     n = fmap1.shape[1] * 9 * 128
     if out is None or out.numel() < n:
-        out = torch.empty(n, dtype=torch.float16, device=fmap1.device)
+        out = H.empty(n, dtype=torch.float16, device=fmap1.device)
     H.check(H.lib().dpvo_corr_pack_mfma(H.ptr(fmap1), H.sizes(fmap1), H.strides(fmap1), H.ptr(out),
                                         H.stream_of(fmap1)))
     return out
@@ -93,9 +93,9 @@ def edge_order(jj, num_frames):
     [0, num_frames)): the L2-friendly visiting order of forward_pyramid_mfma."""
     H.on_gpu(jj)
     jj = H.idx64(jj)
-    order = torch.empty(max(jj.numel(), 1), dtype=torch.int32, device=jj.device)
+    order = H.empty(max(jj.numel(), 1), dtype=torch.int32, device=jj.device)
     nbytes = H.lib().dpvo_edge_order_workspace_bytes(int(num_frames))
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=jj.device)
+    ws = H.empty(nbytes, dtype=torch.uint8, device=jj.device)
     H.check(H.lib().dpvo_edge_order(H.ptr(jj), jj.numel(), int(num_frames), H.ptr(order), H.ptr(ws), nbytes,
                                     H.stream_of(jj)))
     return order[:jj.numel()]
@@ -114,7 +114,7 @@ def forward_pyramid_mfma(table, num_patches, pyramid, coords, ii, jj, scales=(1,
         raise RuntimeError("forward_pyramid_mfma: coords must be float32 [1, E, 2, 3, 3]")
     E = coords.shape[1]
     if out is None:
-        out = torch.empty((1, E, 882), dtype=torch.float16, device=coords.device)
+        out = H.empty((1, E, 882), dtype=torch.float16, device=coords.device)
     elif out.shape != (1, E, 882) or out.dtype != torch.float16 or out.stride(2) != 1:
         raise RuntimeError("forward_pyramid_mfma: out must be [1, E, 882] fp16 with unit feature stride")
     ii, jj = H.idx64(ii), H.idx64(jj)
@@ -129,45 +129,6 @@ def forward_pyramid_mfma(table, num_patches, pyramid, coords, ii, jj, scales=(1,
     H.check(H.lib().dpvo_corr_pyramid_mfma(
         H.ptr(table), int(num_patches), ptrs, fs, fst, sc, H.ptr(coords), H.sizes(coords), H.strides(coords),
         H.ptr(ii), H.ptr(jj), H.ptr(out), out.stride(1) if E > 0 else 0, H.ptr(order), H.stream_of(coords)))
-    return out
-
-
-def staged_workspace(num_edges, pyramid, out=None):
-    """uint8 device workspace for forward_pyramid_staged (reused when large enough)."""
-    f1 = pyramid[0]
-    nbytes = H.lib().dpvo_corr_staged_workspace_bytes(int(num_edges), int(min(f.shape[1] for f in pyramid)),
-                                                      int(f1.shape[3]), int(f1.shape[4]))
-    if nbytes == 0:
-        raise RuntimeError("forward_pyramid_staged: too many (frame, cell) bins; use forward_pyramid_mfma")
-    if out is None or out.numel() < nbytes:
-        out = torch.empty(nbytes, dtype=torch.uint8, device=f1.device)
-    return out
-
-
-def forward_pyramid_staged(table, num_patches, pyramid, coords, ii, jj, scales=(1, 4), out=None, workspace=None):
-    """forward_pyramid_mfma's rows, bit for bit, with the target-frame windows
-    staged in LDS (csrc/corrstage.hip; see include/dpvo_hot.h).  No visiting
-    order: the edges are binned by (target frame, level-1 cell) on the device.
-    workspace (optional): staged_workspace(E, pyramid), reused across calls."""
-    H.on_gpu(table, coords, ii, jj, *pyramid)
-    if len(pyramid) != 2 or any(f.dtype != torch.float16 for f in pyramid):
-        raise RuntimeError("forward_pyramid_staged: two fp16 pyramid levels")
-    if coords.dtype != torch.float32 or coords.dim() != 5 or tuple(coords.shape[2:]) != (2, 3, 3):
-        raise RuntimeError("forward_pyramid_staged: coords must be float32 [1, E, 2, 3, 3]")
-    E = coords.shape[1]
-    if out is None:
-        out = torch.empty((1, E, 882), dtype=torch.float16, device=coords.device)
-    elif out.shape != (1, E, 882) or out.dtype != torch.float16 or out.stride(2) != 1:
-        raise RuntimeError("forward_pyramid_staged: out must be [1, E, 882] fp16 with unit feature stride")
-    ii, jj = H.idx64(ii), H.idx64(jj)
-    ws = staged_workspace(E, pyramid, workspace)
-    ptrs = (H._vp * 2)(*[f.data_ptr() for f in pyramid])
-    fs = H.i64arr([s for f in pyramid for s in f.shape])
-    fst = H.i64arr([s for f in pyramid for s in f.stride()])
-    sc = (H._fp * 2)(*[float(s) for s in scales])
-    H.check(H.lib().dpvo_corr_pyramid_staged(
-        H.ptr(table), int(num_patches), ptrs, fs, fst, sc, H.ptr(coords), H.sizes(coords), H.strides(coords),
-        H.ptr(ii), H.ptr(jj), H.ptr(out), out.stride(1) if E > 0 else 0, H.ptr(ws), ws.numel(), H.stream_of(coords)))
     return out
 
 
@@ -194,7 +155,7 @@ def patchify_forward(net, coords, radius):
     coords = coords.contiguous()
     M = coords.shape[1]
     D = 2 * radius + 2
-    out = torch.empty((B, M, C, D, D), dtype=net.dtype, device=net.device)
+    out = H.empty((B, M, C, D, D), dtype=net.dtype, device=net.device)
     H.check(H.lib().dpvo_patchify_forward(H.dtype_code(net), H.ptr(net), H.sizes(net), H.strides(net), H.ptr(coords),
                                           M, int(radius), H.ptr(out), H.stream_of(net)))
     return [out]

@@ -70,8 +70,3 @@ def corr_pyramid_mfma(table, num_patches, pyramid, coords, ii, jj, levels=(1, 4)
                                           order=order)
 
 
-def corr_pyramid_staged(table, num_patches, pyramid, coords, ii, jj, levels=(1, 4), out=None, workspace=None):
-    """corr_pyramid_mfma's rows, bit for bit, with each target frame's windows
-    staged in LDS per 8x8 cell of the level-1 map (csrc/corrstage.hip)."""
-    return cuda_corr.forward_pyramid_staged(table, num_patches, list(pyramid), coords, ii, jj, list(levels), out=out,
-                                            workspace=workspace)

@@ -56,8 +56,6 @@ _C.USE_DISTANCE_EDGES = True
 _C.BA_ITERATIONS = 2          # the reference hard-codes 2 (dpvo.py:734)
 _C.CHANNEL_LAST_FMAPS = True  # keep the feature rings channel-contiguous (altcorr fast path)
 _C.EXACT_CORR = False         # True: the bit-exact fp16-chain altcorr instead of the matrix-core kernel
-_C.STAGED_CORR = False        # True: the matrix-core altcorr with the target windows staged in LDS per
-                              # (frame, cell) -- same bits; measured no faster at C3
 _C.DEFER_BA_CHECK = True      # BA's Cholesky status read at keyframe()'s host read, not inside update()
 _C.DEFER_KEYFRAME = False     # keyframe()'s decision applied by the next __call__ (its host read overlaps that frame's encoders)
 

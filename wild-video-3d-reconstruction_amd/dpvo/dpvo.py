@@ -202,12 +202,6 @@ class DPVO:
             out = buf[:E, :CORR_DIM].unsqueeze(0)
             if not getattr(self.cfg, "EXACT_CORR", False) and getattr(self.cfg, "CHANNEL_LAST_FMAPS", True):
                 # matrix cores, fp32 accumulation (csrc/corrmfma.hip)
-                if getattr(self.cfg, "STAGED_CORR", False) and self._staged_ok(E):
-                    # the same rows with each (target frame, 8x8 cell)'s windows
-                    # staged in LDS once for all of its edges (csrc/corrstage.hip)
-                    return altcorr.corr_pyramid_staged(self._gmap_table(mfma=True), self.gmap.shape[1], self.pyramid,
-                                                       coords, ii1, jj1, out=out,
-                                                       workspace=self._corr_ws).view(1, E, -1)
                 # edges grouped by target frame: one frame's map per XCD L2 at a time
                 if order is None:
                     order = cuda_corr.edge_order(jj1, self.pmem)
@@ -216,16 +210,6 @@ class DPVO:
             table = self._gmap_table()
         return altcorr.corr_pyramid(self.gmap, self.pyramid, coords, ii1, jj1, 3, (1, 4), out=out,
                                     table=table).view(1, E, -1)
-
-    def _staged_ok(self, E):
-        """the staged kernel's workspace for E edges (cached); False when its
-        (frame, cell) bins would not fit it (rings far larger than the
-        tracker's 36 frames): DPVO.corr then runs the per-edge kernel"""
-        try:
-            self._corr_ws = cuda_corr.staged_workspace(E, self.pyramid, getattr(self, "_corr_ws", None))
-            return True
-        except RuntimeError:
-            return False
 
     def _gmap_table(self, mfma=False):
         """The gmap ring packed for altcorr (the exact kernel's scalar-operand
@@ -289,7 +273,7 @@ class DPVO:
         # place instead of concatenating the whole state (146 MB at C3)
         net = self.pg.net
         n_keep = keep.numel()
-        cap = net.new_empty(1, n_keep + self._edge_slack(), net.shape[2])
+        cap = H.new_empty(net, 1, n_keep + self._edge_slack(), net.shape[2])
         torch.index_select(net, 1, keep, out=cap[:, :n_keep])
         self._net_cap = cap
         self.pg.net = cap[:, :n_keep]
@@ -306,7 +290,7 @@ class DPVO:
         if cap is None or cur.data_ptr() != cap.data_ptr() or cap.shape[dim] < n0 + add or not cur.is_contiguous():
             size = list(src.shape)
             size[dim] = max(2 * (n0 + add), 4096)
-            cap = src.new_empty(size)
+            cap = H.new_empty(src, size)
             cap.narrow(dim, 0, n0).copy_(cur)
             caps[name] = cap
         return cap.narrow(dim, n0, add), cap.narrow(dim, 0, n0 + add)
@@ -353,16 +337,16 @@ class DPVO:
             mode = 0
         rm = m.contiguous().view(torch.uint8)
         sm = store.contiguous().view(torch.uint8) if mode == 2 else None
-        ii_k, jj_k, kk_k = (torch.empty(n_keep, dtype=torch.int64, device=self.device) for _ in range(3))
-        w_k, t_k = w.new_empty(1, n_keep, w.shape[2]), t.new_empty(1, n_keep, t.shape[2])
-        cap = net.new_empty(1, n_keep + self._edge_slack(), net.shape[2])
+        ii_k, jj_k, kk_k = (H.empty(n_keep, dtype=torch.int64, device=self.device) for _ in range(3))
+        w_k, t_k = H.new_empty(w, 1, n_keep, w.shape[2]), H.new_empty(t, 1, n_keep, t.shape[2])
+        cap = H.new_empty(net, 1, n_keep + self._edge_slack(), net.shape[2])
         tails, grown = {}, {}
         if mode:
             for name, src, dim in self._INACTIVE:
                 tails[name], grown[name] = self._inactive_reserve(name, getattr(pg, src), n_store, dim)
         tp = lambda name: tails[name].data_ptr() if mode else None
         nb = H.lib().dpvo_compact_edges_workspace_bytes(E)
-        ws = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        ws = H.empty(nb, dtype=torch.uint8, device=self.device)
         H.check(H.lib().dpvo_compact_edges(
             E, rm.data_ptr(), sm.data_ptr() if sm is not None else None, mode, pg.ii.data_ptr(), pg.jj.data_ptr(),
             pg.kk.data_ptr(), w.data_ptr(), t.data_ptr(), w.shape[2] * w.element_size(), net.data_ptr(),
@@ -443,13 +427,9 @@ class DPVO:
                 # window keys in four launches (an edge outside the window sets
                 # the deferred failure word: the next keyframe() / check_ba() raises)
                 # (+ the edges grouped by target frame: altcorr's visiting order)
-                # (the per-edge matrix-core altcorr's visiting order only when it
-                # runs: the staged kernel bins the edges itself)
-                want_order = not getattr(self.cfg, "STAGED_CORR", False)
-                ctx_idx, jslot, kk_groups, ij_groups, *rest = update_ops.window_group_by(
+                ctx_idx, jslot, kk_groups, ij_groups, order = update_ops.window_group_by(
                     self.pg.ii, self.pg.jj, self.pg.kk, self.M, self.n - 64, self.M * self.pmem, self.pmem,
-                    flag=self._ba_status if defer else self._ba_fail, jj_order=want_order)
-                order = rest[0] if want_order else None
+                    flag=self._ba_status if defer else self._ba_fail, jj_order=True)
                 slots = (ctx_idx, jslot)
             else:
                 kk_groups, ij_groups = self._kk_groups(), self._ij_groups()

@@ -58,8 +58,8 @@ def transform_fused(poses, patches, intrinsics, ii, jj, kk, depth=False, valid=F
     E, P = ii.numel(), patches.shape[-1]
     od = 3 if depth else 2
     shape = (1, E, od, P, P) if chw else (1, E, P, P, od)
-    out = torch.empty(shape, dtype=torch.float32, device=data.device)
-    v = torch.empty((1, E, P, P), dtype=torch.float32, device=data.device) if valid else None
+    out = H.empty(shape, dtype=torch.float32, device=data.device)
+    v = H.empty((1, E, P, P), dtype=torch.float32, device=data.device) if valid else None
     flags = (TF_DEPTH if depth else 0) | (TF_TONLY if tonly else 0) | (TF_CHW if chw else 0)
     H.check(H.lib().dpvo_transform(H.ptr(data), H.ptr(patches), P, H.ptr(intrinsics), H.ptr(ii), H.ptr(jj),
                                    H.ptr(kk), E, flags, H.ptr(out), H.ptr(v), H.stream_of(data)))
@@ -79,7 +79,7 @@ def pose_relative(a, b):
     """SE3 a * b^-1 for two fp32 [7] pose rows, one launch (dpvo.py:613)."""
     H.on_gpu(a, b)
     a, b = a.contiguous().float(), b.contiguous().float()
-    out = torch.empty(7, dtype=torch.float32, device=a.device)
+    out = H.empty(7, dtype=torch.float32, device=a.device)
     H.check(H.lib().dpvo_pose_relative(H.ptr(a), H.ptr(b), H.ptr(out), H.stream_of(a)))
     return SE3(out)
 
@@ -91,9 +91,9 @@ def motion_mag_pair(poses, patches, intrinsics, ii, jj, kk, i, j, beta=0.5):
     data = poses.data.contiguous()
     patches, intrinsics = patches.contiguous(), intrinsics.contiguous()
     ii, jj, kk = H.idx64(ii), H.idx64(jj), H.idx64(kk)
-    out = torch.empty(2, dtype=torch.float32, device=data.device)
+    out = H.empty(2, dtype=torch.float32, device=data.device)
     nb = H.lib().dpvo_motion_mag_workspace_bytes(ii.numel())
-    ws = torch.empty(nb, dtype=torch.uint8, device=data.device)
+    ws = H.empty(nb, dtype=torch.uint8, device=data.device)
     H.check(H.lib().dpvo_motion_mag_ws(H.ptr(data), H.ptr(patches), patches.shape[-1], H.ptr(intrinsics), H.ptr(ii),
                                        H.ptr(jj), H.ptr(kk), ii.numel(), int(i), int(j), float(beta), H.ptr(out),
                                        H.ptr(ws), nb, H.stream_of(data)))
@@ -111,11 +111,11 @@ def keyframe_masks(ii, jj, kk, ix, k, M, n, RW, mm, ba_fail, pose_k):
     if mm.dtype != torch.float32 or ba_fail.dtype != torch.int32 or pose_k.dtype != torch.float32:
         raise RuntimeError("keyframe_masks: mm / pose_k float32, ba_fail int32")
     E, dev = ii.numel(), ii.device
-    masks = torch.empty(3, E, dtype=torch.bool, device=dev)
-    idx = torch.empty(3, E, dtype=torch.int64, device=dev)
-    vals = torch.empty(7, dtype=torch.float64, device=dev)
+    masks = H.empty(3, E, dtype=torch.bool, device=dev)
+    idx = H.empty(3, E, dtype=torch.int64, device=dev)
+    vals = H.empty(7, dtype=torch.float64, device=dev)
     nb = H.lib().dpvo_keyframe_masks_workspace_bytes(E)
-    ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    ws = H.empty(nb, dtype=torch.uint8, device=dev)
     H.check(H.lib().dpvo_keyframe_masks(H.ptr(ii), H.ptr(jj), H.ptr(kk), E, H.ptr(ix), ix.numel(), int(k), int(M),
                                         int(n), int(RW), H.ptr(mm.contiguous()), H.ptr(ba_fail),
                                         H.ptr(pose_k.contiguous()), H.ptr(masks), H.ptr(idx), H.ptr(vals), H.ptr(ws),
@@ -165,7 +165,7 @@ def keyframe_flow(poses, patches, intrinsics, n, M, beta=0.5):
     data = poses.data.contiguous()
     patches, intrinsics = patches.contiguous(), intrinsics.contiguous()
     P = patches.shape[-1]
-    out = torch.empty(n, n, dtype=torch.float32, device=data.device)
+    out = H.empty(n, n, dtype=torch.float32, device=data.device)
     H.check(H.lib().dpvo_keyframe_flow(H.ptr(data), H.ptr(patches), P, H.ptr(intrinsics), int(n), int(M), float(beta),
                                        H.ptr(out), H.stream_of(data)))
     return out
@@ -213,7 +213,7 @@ def point_cloud(poses, patches, intrinsics, ix):
         patches, intrinsics = patches.contiguous(), intrinsics.contiguous()
         ix = H.idx64(ix)
         m, P = ix.numel(), patches.shape[-1]
-        out = torch.empty((1, m, P, P, 4), dtype=torch.float32, device=data.device)
+        out = H.empty((1, m, P, P, 4), dtype=torch.float32, device=data.device)
         H.check(H.lib().dpvo_point_cloud(H.ptr(data), H.ptr(patches), P, H.ptr(intrinsics), H.ptr(ix), m, 0,
                                          H.ptr(out), H.stream_of(data)))
         return out
@@ -228,7 +228,7 @@ def point_cloud_centre(poses, patches, intrinsics, ix, out=None):
     ix = H.idx64(ix)
     m, P = ix.numel(), patches.shape[-1]
     if out is None:
-        out = torch.empty((m, 3), dtype=torch.float32, device=data.device)
+        out = H.empty((m, 3), dtype=torch.float32, device=data.device)
     H.check(H.lib().dpvo_point_cloud(H.ptr(data), H.ptr(patches), P, H.ptr(intrinsics), H.ptr(ix), m, 1,
                                      H.ptr(out), H.stream_of(data)))
     return out

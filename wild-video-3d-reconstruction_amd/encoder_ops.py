@@ -105,7 +105,7 @@ class _Work:
     (l = 0 stem .. 8), or None without norm."""
 
     def __init__(self, H1, W1, H2, W2, t1, t2, stats, dev):
-        z = lambda n, c: torch.empty(n, c, dtype=torch.float16, device=dev)
+        z = lambda n, c: H.empty(n, c, dtype=torch.float16, device=dev)
         n1, n2 = H1 * W1, H2 * W2
         self.y = [z(n1, 32) for _ in range(5)]          # y0 .. y4
         self.x0, self.x1 = z(n1, 32), z(n1, 32)
@@ -161,9 +161,9 @@ class NativeEncoders:
         dev = image.device
         Hh, Ww = image.shape[1:]
         ws, (H1, W1, H2, W2) = self._ws(Hh, Ww, dev, pk)
-        fmap = fmap_out if fmap_out is not None else torch.empty(H2 * W2, 128, dtype=torch.float16, device=dev)
+        fmap = fmap_out if fmap_out is not None else H.empty(H2 * W2, 128, dtype=torch.float16, device=dev)
         M = x.numel()
-        imap = torch.empty(M, pk[1].out_dim, dtype=torch.float16, device=dev)
+        imap = H.empty(M, pk[1].out_dim, dtype=torch.float16, device=dev)
 
         def st(t):   # a producer's partials as (pointer, tiles, row length)
             if t is None or _DBG_NOSTATS:
@@ -239,9 +239,9 @@ class NativeEncoders:
         h, w = fmap.shape[-2:]
         f = fmap[0, 0]
         strides = torch.tensor([f.stride(0), f.stride(1), f.stride(2)], dtype=torch.int64)
-        gm = torch.empty(1, M, 128, 3, 3, dtype=torch.float32, device=dev)
-        im = torch.empty(1, M, dim, 1, 1, dtype=torch.float32, device=dev)
-        pt = torch.empty(1, M, 3, 3, 3, dtype=torch.float32, device=dev)
+        gm = H.empty(1, M, 128, 3, 3, dtype=torch.float32, device=dev)
+        im = H.empty(1, M, dim, 1, 1, dtype=torch.float32, device=dev)
+        pt = H.empty(1, M, 3, 3, 3, dtype=torch.float32, device=dev)
         clr = lut = img = None
         Hh = Ww = 0
         if return_color:
@@ -250,7 +250,7 @@ class NativeEncoders:
             img = image.contiguous()
             Hh, Ww = img.shape[1:]
             lut = self._lut(dev)
-            clr = torch.empty(1, M, 3, dtype=torch.float32, device=dev)
+            clr = H.empty(1, M, 3, dtype=torch.float32, device=dev)
         H.check(H.lib().dpvo_patch_gather(f.data_ptr(), strides.data_ptr(), h, w, imap.data_ptr(), dim, _ptr(img),
                                           Hh, Ww, _ptr(lut), x.data_ptr(), y.data_ptr(), M, gm.data_ptr(),
                                           im.data_ptr(), pt.data_ptr(), _ptr(clr), H.stream_of(fmap)))

@@ -116,7 +116,7 @@ def scatter_max(src, index, dim=-1, out=None, dim_size=None):
 
 def scatter_softmax(src, index, dim=-1, eps=1e-12, dim_size=None):
     dim, src3, index, outer, E, inner = _prep(src, index, dim)
-    out = torch.empty_like(src3)
+    out = H.empty(src3.shape, dtype=src3.dtype, device=src3.device)
     _check_range(index)
     if E:
         U.scatter_csr(U.SCATTER_SOFTMAX, src3, index, U.group_by(index), out, eps=eps)

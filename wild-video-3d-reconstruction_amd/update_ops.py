@@ -26,9 +26,9 @@ def softagg(f, s, group, groups, eps=1e-12):
         raise RuntimeError("softagg: rows must be channel-contiguous")
     E, D = f.shape
     group = H.idx64(group)
-    y = torch.empty(groups, D, dtype=f.dtype, device=f.device)
+    y = H.empty(groups, D, dtype=f.dtype, device=f.device)
     nbytes = H.lib().dpvo_softagg_workspace_bytes(E, groups)
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=f.device)
+    ws = H.empty(nbytes, dtype=torch.uint8, device=f.device)
     H.check(H.lib().dpvo_softagg_forward(H.dtype_code(f), H.ptr(f), f.stride(0), H.ptr(s), s.stride(0),
                                          H.ptr(group), E, D, groups, float(eps), H.ptr(y), H.ptr(ws), nbytes,
                                          H.stream_of(f)))
@@ -54,13 +54,13 @@ def group_by(key, key_bits=64, radix=False):
     key = H.idx64(key)
     n = key.numel()
     dev = key.device
-    gid = torch.empty(n, dtype=torch.int64, device=dev)
-    offs = torch.empty(n + 1, dtype=torch.int32, device=dev)
-    perm = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
-    groups = torch.empty(1, dtype=torch.int64, device=dev)
+    gid = H.empty(n, dtype=torch.int64, device=dev)
+    offs = H.empty(n + 1, dtype=torch.int32, device=dev)
+    perm = H.empty(max(n, 1), dtype=torch.int32, device=dev)
+    groups = H.empty(1, dtype=torch.int64, device=dev)
     nbytes = (H.lib().dpvo_group_by_workspace_bytes(n) if radix
               else H.lib().dpvo_group_by_workspace_bytes_for(n, int(key_bits)))
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    ws = H.empty(nbytes, dtype=torch.uint8, device=dev)
     H.check(H.lib().dpvo_group_by(H.ptr(key), n, int(key_bits), H.ptr(gid), H.ptr(offs), H.ptr(perm), H.ptr(groups),
                                   H.ptr(ws), nbytes, H.stream_of(key)))
     return gid, offs, perm, groups
@@ -73,7 +73,7 @@ def softagg_csr(f, s, offs, perm, groups, max_groups, eps=1e-12, long_groups=Fal
     if f.dim() != 2 or s.shape != f.shape or f.dtype != s.dtype or f.stride(1) != 1 or s.stride(1) != 1:
         raise RuntimeError("softagg_csr: f and s must be [E, D] with channel-contiguous rows, same dtype")
     D = f.shape[1]
-    y = torch.empty(max_groups, D, dtype=f.dtype, device=f.device)
+    y = H.empty(max_groups, D, dtype=f.dtype, device=f.device)
     fn = H.lib().dpvo_softagg_csr_long if long_groups else H.lib().dpvo_softagg_csr
     H.check(fn(H.dtype_code(f), H.ptr(f), f.stride(0), H.ptr(s), s.stride(0), H.ptr(offs), H.ptr(perm), H.ptr(groups),
                int(max_groups), D, float(eps), H.ptr(y), H.stream_of(f)))
@@ -115,9 +115,9 @@ def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=
         M = a_idx.numel()
     elif M is None:
         M = A.shape[0]
-    out32 = torch.empty(M, WIDTH, dtype=torch.float32, device=dev) if want32 else None
-    out16 = torch.empty(M, WIDTH, dtype=torch.float16, device=dev) if want16 else None
-    head_out = torch.empty(M, 4, dtype=torch.float16, device=dev) if heads is not None else None
+    out32 = H.empty(M, WIDTH, dtype=torch.float32, device=dev) if want32 else None
+    out16 = H.empty(M, WIDTH, dtype=torch.float16, device=dev) if want16 else None
+    head_out = H.empty(M, 4, dtype=torch.float16, device=dev) if heads is not None else None
     if res16_idx is not None:
         res16_idx = H.idx64(res16_idx)
     g1 = RowGemmArgs()
@@ -179,8 +179,8 @@ def neighbors_csr(jj, offs, perm, groups, max_groups):
     H.on_gpu(jj, offs, perm, groups)
     jj = H.idx64(jj)
     E = jj.numel()
-    ix = torch.empty(E, dtype=torch.int64, device=jj.device)
-    jx = torch.empty(E, dtype=torch.int64, device=jj.device)
+    ix = H.empty(E, dtype=torch.int64, device=jj.device)
+    jx = H.empty(E, dtype=torch.int64, device=jj.device)
     H.check(H.lib().dpvo_neighbors_csr(H.ptr(jj), H.ptr(offs), H.ptr(perm), H.ptr(groups), int(max_groups), E,
                                        H.ptr(ix), H.ptr(jx), H.stream_of(jj)))
     return ix, jx
@@ -195,7 +195,7 @@ def window_keys(ii, jj, kk, M, base, ring, frames, flag=None):
     E = kk.numel()
     if ii.numel() != E or jj.numel() != E:
         raise RuntimeError("window_keys: ii, jj and kk must have the same length")
-    out = torch.empty(4, E, dtype=torch.int64, device=kk.device)
+    out = H.empty(4, E, dtype=torch.int64, device=kk.device)
     H.check(H.lib().dpvo_window_keys(H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(M), int(base), int(ring), int(frames),
                                      H.ptr(out[0]), H.ptr(out[1]), H.ptr(out[2]), H.ptr(out[3]), H.ptr(flag),
                                      H.stream_of(kk)))
@@ -218,13 +218,13 @@ def window_group_by(ii, jj, kk, M, base, ring, frames, flag=None, jj_order=False
     if nbytes == 0:
         raise RuntimeError("window_group_by: 64 M above the counting-sort range")
     dev = kk.device
-    slots = torch.empty(2, E, dtype=torch.int64, device=dev)
-    gid = torch.empty(2, E, dtype=torch.int64, device=dev)
-    offs = torch.empty(2, E + 1, dtype=torch.int32, device=dev)
-    perm = torch.empty(2, max(E, 1), dtype=torch.int32, device=dev)
-    groups = torch.empty(2, 1, dtype=torch.int64, device=dev)
-    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    order = torch.empty(max(E, 1), dtype=torch.int32, device=dev) if jj_order else None
+    slots = H.empty(2, E, dtype=torch.int64, device=dev)
+    gid = H.empty(2, E, dtype=torch.int64, device=dev)
+    offs = H.empty(2, E + 1, dtype=torch.int32, device=dev)
+    perm = H.empty(2, max(E, 1), dtype=torch.int32, device=dev)
+    groups = H.empty(2, 1, dtype=torch.int64, device=dev)
+    ws = H.empty(nbytes, dtype=torch.uint8, device=dev)
+    order = H.empty(max(E, 1), dtype=torch.int32, device=dev) if jj_order else None
     H.check(H.lib().dpvo_window_group_by(
         H.ptr(ii), H.ptr(jj), H.ptr(kk), E, int(M), int(base), int(ring), int(frames), bits, H.ptr(slots[0]),
         H.ptr(slots[1]), H.ptr(flag), H.ptr(gid[0]), H.ptr(offs[0]), H.ptr(perm[0]), H.ptr(groups[0]), H.ptr(gid[1]),
@@ -245,7 +245,7 @@ def append_edges(ii, jj, kk, ix, n, M, r):
     add = H.lib().dpvo_append_edges_count(int(n), int(M), int(r))
     if add < 0:
         raise RuntimeError("append_edges: n >= 1, M >= 1 and PATCH_LIFETIME >= 1 required")
-    out = torch.empty(3, E + add, dtype=torch.int64, device=kk.device)
+    out = H.empty(3, E + add, dtype=torch.int64, device=kk.device)
     H.check(H.lib().dpvo_append_edges(H.ptr(ii), H.ptr(jj), H.ptr(kk), E, H.ptr(ix), int(n), int(M), int(r),
                                       H.ptr(out[0]), H.ptr(out[1]), H.ptr(out[2]), H.stream_of(kk)))
     return out[0], out[1], out[2]
@@ -260,8 +260,8 @@ def edge_targets(centre, delta, weight):
             delta.shape != (1, E, 2) or weight.shape != (1, E, 2) or centre.shape != (1, E, 2) or
             delta.stride(2) != 1 or weight.stride(2) != 1):
         raise RuntimeError("edge_targets: centre fp32, delta / weight fp16 [1, E, 2] with unit component stride")
-    target = torch.empty(1, E, 2, dtype=torch.float32, device=delta.device)
-    w32 = torch.empty(1, E, 2, dtype=torch.float32, device=delta.device)
+    target = H.empty(1, E, 2, dtype=torch.float32, device=delta.device)
+    w32 = H.empty(1, E, 2, dtype=torch.float32, device=delta.device)
     H.check(H.lib().dpvo_edge_targets(H.ptr(delta), delta.stride(1), H.ptr(weight), weight.stride(1), H.ptr(centre),
                                       centre.stride(1), centre.stride(2), E, H.ptr(target), H.ptr(w32),
                                       H.stream_of(delta)))
@@ -276,7 +276,7 @@ def gather_rows(x, idx, dtype=None):
         raise RuntimeError("gather_rows: x must be [R, D] with contiguous rows")
     dtype = dtype or x.dtype
     idx = H.idx64(idx)
-    out = torch.empty(idx.numel(), x.shape[1], dtype=dtype, device=x.device)
+    out = H.empty(idx.numel(), x.shape[1], dtype=dtype, device=x.device)
     H.check(H.lib().dpvo_gather_rows(H.dtype_code(x), H.ptr(x), x.stride(0), x.shape[0], H.ptr(idx), idx.numel(),
                                      x.shape[1], H.dtype_code(out), H.ptr(out), H.stream_of(x)))
     return out
@@ -384,10 +384,10 @@ def rowgemm(A, W16, b16, flags=0, a_idx=None, M=None, res32=None, res16=None, re
     elif M is None:
         M = A.shape[0]
     if want32 and out32 is None:
-        out32 = torch.empty(M, WIDTH, dtype=torch.float32, device=dev)
+        out32 = H.empty(M, WIDTH, dtype=torch.float32, device=dev)
     if want16 and out16 is None:
-        out16 = torch.empty(M, WIDTH, dtype=torch.float16, device=dev)
-    head_out = torch.empty(M, 4, dtype=torch.float16, device=dev) if heads is not None else None
+        out16 = H.empty(M, WIDTH, dtype=torch.float16, device=dev)
+    head_out = H.empty(M, 4, dtype=torch.float16, device=dev) if heads is not None else None
     if res16_idx is not None:
         res16_idx = H.idx64(res16_idx)
     a = RowGemmArgs()
@@ -435,7 +435,7 @@ def rowgemm_pair(A, Wa, ba, Wb, bb, M_dev=None):
     outs = []
     args = []
     for W, b in ((Wa, ba), (Wb, bb)):
-        o = torch.empty(M, WIDTH, dtype=torch.float16, device=dev)
+        o = H.empty(M, WIDTH, dtype=torch.float16, device=dev)
         a = RowGemmArgs()
         a.A, a.lda, a.a_idx, a.a_rows = _p(A), A.stride(0), None, M
         a.W, a.K, a.N, a.bias, a.zero_row = _p(W), Kp, WIDTH, _p(b), _p(zero_row(dev, Kp))
@@ -469,7 +469,7 @@ def rowgemm_pair_pre(a32, b16, b_idx, Wa, ba, Wb, bb, b_rows=None):
     M, dev = a32.shape[0], a32.device
     outs, args = [], []
     for W, b in ((Wa, ba), (Wb, bb)):
-        o = torch.empty(M, WIDTH, dtype=torch.float16, device=dev)
+        o = H.empty(M, WIDTH, dtype=torch.float16, device=dev)
         a = RowGemmArgs()
         z = _p(zero_row(dev, Kp))
         a.A, a.lda, a.a_idx, a.a_rows = z, Kp, None, M   # (A unused: the rows are pre's)
@@ -494,8 +494,8 @@ def rowadd_ln(a, b16=None, b_idx=None, ln=None, want32=True, want16=True, c16=No
     if a.dim() != 2 or a.shape[1] != WIDTH or a.stride(1) != 1 or a.dtype not in (torch.float16, torch.float32):
         raise RuntimeError("rowadd_ln: a must be [M, 384] fp16/fp32 with contiguous rows")
     M, dev = a.shape[0], a.device
-    out32 = torch.empty(M, WIDTH, dtype=torch.float32, device=dev) if want32 else None
-    out16 = torch.empty(M, WIDTH, dtype=torch.float16, device=dev) if want16 else None
+    out32 = H.empty(M, WIDTH, dtype=torch.float32, device=dev) if want32 else None
+    out16 = H.empty(M, WIDTH, dtype=torch.float16, device=dev) if want16 else None
     if b_idx is not None:
         b_idx = H.idx64(b_idx)
     args = RowAddArgs()
