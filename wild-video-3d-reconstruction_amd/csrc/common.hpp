@@ -76,7 +76,9 @@ __device__ __forceinline__ int wrap_add(int a, int b) { return (int)((unsigned)a
 template <int CTRL>
 __device__ __forceinline__ float dpp_rot(float v)
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+    // (no "old" operand: every lane of a row rotation is written; update_dpp
+    // with old = 0 cost a v_mov of that 0 per rotation)
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 // all-reduce over a DPP row (16 lanes): every lane of the row gets the row's sum
 __device__ __forceinline__ float row16_sum(float s)

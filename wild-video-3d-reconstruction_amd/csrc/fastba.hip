@@ -1702,11 +1702,11 @@ __device__ __forceinline__ float wave64_sum33(const float (&v)[33], int lane)
 #pragma unroll
     for (int j = 0; j < 2; j++) {   // bit 1, quad_perm [2, 3, 0, 1]
         const float send = b1 ? r[j] : r[j + 2], keep = b1 ? r[j + 2] : r[j];
-        t2[j] = keep + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), 0x4E, 0xF, 0xF, false));
+        t2[j] = keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x4E, 0xF, 0xF, false));
     }
     // bit 0, quad_perm [1, 0, 3, 2]
     const float send = b0 ? t2[0] : t2[1], keep = b0 ? t2[1] : t2[0];
-    return keep + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(send), 0xB1, 0xF, 0xF, false));
+    return keep + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0xB1, 0xF, 0xF, false));
 }
 
 __device__ __forceinline__ unsigned wave_or(unsigned v)

@@ -48,7 +48,7 @@ enum {
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v)
 {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));   // (no old operand)
 }
 // all-reduce over a DPP row (16 lanes) by rotations: every lane gets the sum
 __device__ __forceinline__ float rowsum16(float s)
