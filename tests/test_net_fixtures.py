@@ -142,7 +142,7 @@ def test_update_step_inputs_regenerate(which):
     assert int(f["iters"] if "iters" in f else 2) == C["iters"]
 
 
-@pytest.mark.parametrize("which", ["small", "c2"])
+@pytest.mark.parametrize("which", ["small", "c2", "c3"])
 def test_update_step_oracle_chain_matches_reference(monkeypatch, which):
     """the CPU restatement of the whole update() -- oracle.transform, the
     oracle's exact altcorr (F16_ACC64), the mirror Update in float64, the
