@@ -281,16 +281,18 @@ def test_fused_update_operator_context_index_is_the_gathered_context():
 
 
 @pytest.mark.parametrize("big", [False, True])
-@pytest.mark.parametrize("case", ["corr", "gather_res", "gate_ln", "gate_heads"])
+@pytest.mark.parametrize("case", ["corr", "gather_res", "gather_res16", "gate_ln", "gate_heads"])
 def test_rowchain_is_two_rowgemms(case, big):
     """dpvo_rowchain (the intermediate kept in LDS) is bit-identical to two
     rowgemm launches with the intermediate in HBM: same MFMA chunk order,
     same fp16 rounding of the intermediate.  big: more 128-row tiles than
     workgroups, so blocks run several tiles and the row pass of one tile is
-    interleaved with the next tile's first GEMM (ILV)."""
+    interleaved with the next tile's first GEMM (ILV).  gather_res: c1 / c2's
+    chain (no res16: the no-addend epilogue); gather_res16: with a gathered
+    fp16 addend (the general residual epilogue)."""
     import update_ops as U
     torch.manual_seed(3)
-    M = 1000 if case != "gather_res" else 777
+    M = 777 if case.startswith("gather_res") else 1000
     if big:
         M = 70001
     K1 = 896 if case == "corr" else 384
@@ -302,9 +304,12 @@ def test_rowchain_is_two_rowgemms(case, big):
     res32 = torch.randn(M, 384, device=dev)
     gate16 = torch.rand(M, 384, device=dev).half()
     heads = (torch.randn(4, 384, device=dev).half() * 0.05, torch.randn(4, device=dev).half())
-    a_idx = torch.randint(-1, A.shape[0], (M,), device=dev) if case == "gather_res" else None
+    a_idx = torch.randint(-1, A.shape[0], (M,), device=dev) if case.startswith("gather_res") else None
+    r16 = torch.randn(600, 384, device=dev).half()
+    ridx = torch.randint(-1, 600, (M,), device=dev)
     kw = {"corr": dict(flags=U.LN | U.LN_RELU, ln=ln),
           "gather_res": dict(flags=U.RES, res32=res32, want32=True),
+          "gather_res16": dict(flags=U.RES, res32=res32, res16=r16, res16_idx=ridx, want32=True),
           "gate_ln": dict(flags=U.GATE | U.LN, res32=res32, gate16=gate16, ln=ln, want32=True),
           "gate_heads": dict(flags=U.GATE | U.HEADS, res32=res32, gate16=gate16, heads=heads, want32=True,
                              want16=False)}[case]

@@ -928,7 +928,7 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
 {
     constexpr bool TRI = FMID != 0;
     static_assert(!(TRI && GATED), "a chain is either gated or three GEMMs long");
-    constexpr bool OVL = F2 == RG_RES;
+    constexpr bool OVL = (F2 & ~RG_NOADD) == RG_RES;
     constexpr int NSEG = (TRI || GATED) ? 3 : 2;
     constexpr int NPA = GATED ? 2 : 1;   // A passes per tile
     constexpr int nk2 = RG_BN / R5_BK;
@@ -1211,19 +1211,21 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
         // columns a slower wave had not read yet -- the intermittent last-bit
         // differences of the round-5 graph-replay test.)
         {
-            EpiOps2<2> st;
+            constexpr int OR = 2, NB = 16 / OR;   // rows per batch, batches
+            // (4-row batches: the same time, 248 registers)
+            EpiOps2<OR> st;
             int bi = 0, bd = 0;
             auto ovl = [&](int ks) __attribute__((always_inline)) {
                 if (!OVL || etile < 0) return;
                 if (bd < bi) {
                     EpiConsts2 kc;
                     load_consts2<F2>(p, lane, kc);
-                    epi_done(etile, 16 * w + 2 * bd, kc, st);
+                    epi_done(etile, 16 * w + OR * bd, kc, st);
                     bd++;
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                if (bi < 8 && (bi * (nk1 - 4)) / 7 == ks) {
-                    epi_issue(etile, 16 * w + 2 * bi, st);
+                if (bi < NB && (bi * (nk1 - 4)) / (NB - 1) == ks) {
+                    epi_issue(etile, 16 * w + OR * bi, st);
                     bi++;
                 }
             };
@@ -1332,282 +1334,6 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
     if (lane == 0)
         for (int k = 0; k < ST_SEGS; k++) dpvo_stamps[((int64_t)blockIdx.x * 8 + w) * ST_SEGS + k] = st_sum[k];
 #endif
-}
-
-// ---------------------------------------------------------------------------
-// rowchain64 (round 6): the two-GEMM chain with a 64-row tile and TWO
-// workgroups per CU, for the residual chains (c1 / c2: gathered A, ReLU, RES).
-// rowchain5's GEMM2 runs with the HBM idle (its A is the y tile and its
-// epilogue waits for the next tile's GEMM1: round-5 stamps, 13k of ~53k cycles
-// per tile); with two workgroups on a CU, one's GEMM2 overlaps the other's
-// GEMM1 + row epilogue.  Per workgroup: 8 waves as 1 (M) x 8 (N), wave tile
-// 64 x 48 (4 x 3 accumulators, <= 128 VGPRs: four waves per SIMD), a 48 KB y
-// tile, a 4 x 4 KB A ring (8 bytes per thread per k-step), the biases and the row
-// sources table in LDS: ~74 KB.  The W stream, A ring protocol (one barrier per
-// two k-steps), OVL epilogue (4 batches of 2 rows per wave inside the next
-// tile's GEMM1) and y-tile arithmetic are rowchain5's, so per output element
-// the MFMA k order and the roundings are the same: bit-identical.
-// ---------------------------------------------------------------------------
-constexpr int R6_BM = 64;
-constexpr int R6_Y = R6_BM * 768;              // 48 KB
-constexpr int R6_ASLOT = R6_BM * R5_BK * 2;    // 4 KB
-constexpr int R6_BIAS = R6_Y + 4 * R6_ASLOT;   // two biases, 768 B each
-constexpr int R6_IDX = R6_BIAS + 2 * RG_BN * 2;
-constexpr int R6_IDX_TILES = 16;               // tiles per block whose row sources sit in LDS
-constexpr int R6_LDS = R6_IDX + R6_IDX_TILES * R6_BM * 8;
-
-template <int F2, int F1, bool OVL, int NW = 2>
-__global__ __launch_bounds__(R5_THREADS) __attribute__((amdgpu_waves_per_eu(4, 4))) void rowchain64_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p)
-{
-    static_assert((F2 & ~(RG_RES | RG_LN | RG_NOADD)) == 0 && (F2 & RG_RES), "rowchain64: residual epilogues");
-    static_assert(F1 >= 0, "rowchain64: compile-time first activation");
-    constexpr int nk2 = RG_BN / R5_BK;
-    __shared__ __attribute__((aligned(16))) char smem[R6_LDS];
-    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int fr = lane & 15, fq = lane >> 4;
-    const int nk1 = p1.K / R5_BK;
-    const int64_t Mrows = p1.M_dev ? min(*p1.M_dev, p1.M) : p1.M;
-    const int64_t ntiles = (Mrows + R6_BM - 1) / R6_BM;
-    if ((int64_t)blockIdx.x >= ntiles) return;
-    const unsigned G = gridDim.x;
-    const int64_t my_tiles = (ntiles - 1 - blockIdx.x) / G + 1;
-    const int64_t total_a = my_tiles * nk1;
-    const int64_t total_w = my_tiles * (nk1 + nk2);
-    const YMapChunk ym;
-    const half_t* __restrict__ zero = (const half_t*)p1.zero_row;
-    // ---- the row sources (rowchain5's table: the first tile's read directly,
-    // the later tiles' after the prologue's loads are issued)
-    int64_t* idx_lds = (int64_t*)(smem + R6_IDX);
-    const bool idx_tab = p1.a_idx != nullptr, idx_early = idx_tab && nk1 < 4;
-    auto idx_fill = [&](int i0) __attribute__((always_inline)) {
-        for (int i = i0 + threadIdx.x; i < (int)my_tiles * R6_BM; i += blockDim.x) {
-            const int64_t m = ((int64_t)blockIdx.x + (int64_t)(i / R6_BM) * G) * R6_BM + i % R6_BM;
-            idx_lds[i] = m < Mrows ? p1.a_idx[m] : -1;
-        }
-    };
-    if (idx_early) {
-        idx_fill(0);
-        __syncthreads();
-    }
-    // ---- A staging by all 8 waves: thread x holds row x >> 3, 8-byte chunk x & 7
-    typedef _Float16 a4_t __attribute__((ext_vector_type(4)));
-    const int ar = threadIdx.x >> 3, ac = threadIdx.x & 7;
-    int64_t a_tile = -1;
-    int a_lt = -1;
-    const half_t* arow = zero;
-    auto a_set = [&](int64_t m, int64_t src) __attribute__((always_inline)) {
-        const half_t* row = zero;
-        if (m < Mrows && src >= 0 && src < p1.a_rows) row = (const half_t*)p1.A + src * p1.lda;
-        arow = row + 4 * ac;
-    };
-    if (idx_tab && !idx_early) {
-        a_tile = blockIdx.x;
-        a_lt = 0;
-        const int64_t m0 = a_tile * R6_BM + ar;
-        a_set(m0, m0 < Mrows ? p1.a_idx[m0] : -1);
-    }
-    auto a_row = [&](int64_t t) __attribute__((always_inline)) {
-        if (t == a_tile) return;
-        a_tile = t;
-        a_lt++;
-        const int64_t m = t * R6_BM + ar;
-        a_set(m, !idx_tab ? m : idx_lds[a_lt * R6_BM + ar]);
-    };
-    a4_t areg[2];
-    auto load_a = [&](const R5Cursor& c) __attribute__((always_inline)) -> a4_t {
-        a_row(c.t);
-        return *(const a4_t*)(arow + c.k * R5_BK);
-    };
-    const int aw_off = ar * 64 + 16 * ((ac >> 1) ^ rc_sw(ar)) + 8 * (ac & 1);
-    // ---- W: segment 0 = W1, 1 = W2; fragments at column 48 w + 16 nt + fr
-    const half_t* Ws0 = (const half_t*)p1.W;
-    const half_t* Ws1 = (const half_t*)p.W;
-    // (NW = 1: one W register set, loaded one k-step ahead -- the other three
-    // waves of the SIMD cover its latency)
-    h8_t wreg[NW][3];
-    const int wcol = (48 * w + fr) * R5_BK + 8 * fq;
-    auto load_w = [&](const R5WCursor& c, h8_t (&r)[3]) __attribute__((always_inline)) {
-        const half_t* src = (c.s == 0 ? Ws0 : Ws1) + (int64_t)c.k * (RG_BN * R5_BK) + wcol;
-#pragma unroll
-        for (int nt = 0; nt < 3; nt++) r[nt] = *(const h8_t*)(src + nt * 16 * R5_BK);
-    };
-    if (threadIdx.x < 2 * 96) {
-        const int b = threadIdx.x / 96, c = 4 * (threadIdx.x % 96);
-        *(h4_t*)(smem + R6_BIAS + b * RG_BN * 2 + 2 * c) = *(const h4_t*)((const half_t*)(b ? p.bias : p1.bias) + c);
-    }
-    f4_t acc[4][3];
-    auto zero_acc = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++)
-#pragma unroll
-            for (int nt = 0; nt < 3; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
-    };
-    const int ar_off = fr * 64 + 16 * (fq ^ rc_sw(fr));   // + 1024 mt: row 16 mt + fr
-    auto sync = [&]() __attribute__((always_inline)) {
-        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
-        __builtin_amdgcn_s_barrier();
-    };
-    auto acc_to_y = [&](int bi, bool relu, bool sigm) __attribute__((always_inline)) {
-#pragma unroll
-        for (int nt = 0; nt < 3; nt++) {
-            const int col = 48 * w + 16 * nt + 4 * fq;
-            const h4_t b = *(const h4_t*)(smem + R6_BIAS + bi * RG_BN * 2 + 2 * col);
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++) {
-                h4_t y;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    half_t v = (half_t)(acc[mt][nt][r] + (float)b[r]);
-                    if (relu) v = v > (half_t)0 ? v : (half_t)0;
-                    if (sigm) v = (half_t)fast_sigmoid((float)v);
-                    y[r] = v;
-                }
-                *(h4_t*)(smem + ym.off(16 * mt + fr, col * 2)) = y;
-            }
-        }
-    };
-    const unsigned bid = blockIdx.x;
-    R5Cursor ca{0, (int64_t)bid, 0, 0};
-    R5WCursor cw{0, (int64_t)bid, 0, 0};
-    auto wnext = [&]() __attribute__((always_inline)) { cw.next(total_w, nk1, nk2, 0, 2, G); };
-    auto anext = [&]() __attribute__((always_inline)) { ca.next(total_a, nk1, 1, G); };
-    // one A-step g, PH = g & 1 (rowchain5's step_a on a 64-row slot)
-    int ga = 0;
-    auto step_a = [&](auto ph) __attribute__((always_inline)) {
-        constexpr int PH = decltype(ph)::value;
-        if (PH == 0) sync();
-        const char* sa = smem + R6_Y + (ga & 3) * R6_ASLOT;
-        h8_t a[4];
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(sa + ar_off + 1024 * mt);
-#pragma unroll
-        for (int nt = 0; nt < 3; nt++)
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++)
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wreg[PH % NW][nt], a[mt], acc[mt][nt], 0, 0, 0);
-        load_w(cw, wreg[PH % NW]);
-        wnext();
-        __builtin_amdgcn_sched_barrier(0);
-        *(a4_t*)(smem + R6_Y + ((ga + 2) & 3) * R6_ASLOT + aw_off) = areg[PH];
-        areg[PH] = load_a(ca);
-        anext();
-        ga++;
-    };
-    auto step_y = [&](auto ph, int ks) __attribute__((always_inline)) {
-        constexpr int PH = decltype(ph)::value;
-        h8_t a[4];
-#pragma unroll
-        for (int mt = 0; mt < 4; mt++) a[mt] = *(const h8_t*)(smem + ym.off(16 * mt + fr, (ks * 4 + fq) * 16));
-#pragma unroll
-        for (int nt = 0; nt < 3; nt++)
-#pragma unroll
-            for (int mt = 0; mt < 4; mt++)
-                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wreg[PH % NW][nt], a[mt], acc[mt][nt], 0, 0, 0);
-        load_w(cw, wreg[PH % NW]);
-        wnext();
-    };
-    auto epi_issue = [&](int64_t et, int lr, auto& o) __attribute__((always_inline)) {
-        constexpr int R = sizeof(o.add) / sizeof(o.add[0][0]) / 3 * 2;
-        epi2_load<F2, R>(p, Mrows, et * R6_BM + lr, lane, o);
-    };
-    auto epi_done = [&](int64_t et, int lr, const EpiConsts2& kc, const auto& o) __attribute__((always_inline)) {
-        constexpr int R = sizeof(o.add) / sizeof(o.add[0][0]) / 3 * 2;
-        const int hh = lane >> 5, ss = lane & 31;
-        epi2_finish<F2, R>(
-            p, Mrows,
-            [&](int i, int j) { return *(const ep_h4*)(smem + ym.off(lr + 2 * i + hh, (128 * j + 4 * ss) * 2)); },
-            et * R6_BM + lr, lane, kc, o);
-    };
-
-    // ---- prologue (rowchain5's): W-steps 0, 1; A stages 0, 1 in slots, 2, 3 in registers
-#pragma unroll
-    for (int r = 0; r < NW; r++) {
-        load_w(cw, wreg[r]);
-        wnext();
-    }
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
-        *(a4_t*)(smem + R6_Y + r * R6_ASLOT + aw_off) = load_a(ca);
-        anext();
-    }
-#pragma unroll
-    for (int r = 0; r < 2; r++) {
-        areg[r] = load_a(ca);
-        anext();
-    }
-    if (idx_tab && !idx_early) idx_fill(R6_BM);
-    // OVL needs the 4 batches' loads at distinct k-steps <= nk1 - 4
-    const bool ovl_ok = OVL && nk1 >= 8;
-    int64_t etile = -1;
-    for (int64_t tile = bid; tile < ntiles; tile += G) {
-        const bool more = tile + G < ntiles;
-        // ---- GEMM1 (+ the previous tile's rows 8 w .. 8 w + 7 in 4 batches of
-        // 2: batch b's loads after k-step b (nk1 - 4) / 3, its y-tile reads and
-        // arithmetic one k-step later, <= nk1 - 3 -- before the barrier of
-        // k-step nk1 - 2, the last one ahead of this tile's acc_to_y writes)
-        {
-            EpiOps2<2> st;
-            int bi = 0, bd = 0;
-            auto ovl = [&](int ks) __attribute__((always_inline)) {
-                if (!OVL || etile < 0) return;
-                if (bd < bi) {
-                    EpiConsts2 kc;
-                    load_consts2<F2>(p, lane, kc);
-                    epi_done(etile, 8 * w + 2 * bd, kc, st);
-                    bd++;
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                if (bi < 4 && (bi * (nk1 - 4)) / 3 == ks) {
-                    epi_issue(etile, 8 * w + 2 * bi, st);
-                    bi++;
-                }
-            };
-            zero_acc();
-#pragma unroll 1
-            for (int ks = 0; ks < nk1; ks += 2) {
-                step_a(std::integral_constant<int, 0>{});
-                ovl(ks);
-                step_a(std::integral_constant<int, 1>{});
-                ovl(ks + 1);
-            }
-        }
-        etile = -1;
-        acc_to_y(0, (F1 & RG_RELU) != 0, (F1 & RG_SIGMOID) != 0);
-        sync();
-        zero_acc();
-#pragma unroll 1
-        for (int ks = 0; ks < nk2; ks += 2) {
-            step_y(std::integral_constant<int, 0>{}, ks);
-            step_y(std::integral_constant<int, 1>{}, ks + 1);
-        }
-        sync();   // every wave is done reading the y tile
-        acc_to_y(1, F2 & RG_RELU, F2 & RG_SIGMOID);
-        sync();
-        if (more && ovl_ok) {
-            etile = tile;   // runs inside the next tile's GEMM1
-            continue;
-        }
-        EpiConsts2 kc;
-        load_consts2<F2>(p, lane, kc);
-        if constexpr (OVL) {   // (only the last tile: one batch live)
-#pragma unroll 1
-            for (int q0 = 0; q0 < 8; q0 += 4) {
-                EpiOps2<4> st;
-                epi_issue(tile, 8 * w + q0, st);
-                epi_done(tile, 8 * w + q0, kc, st);
-            }
-        } else {
-#pragma unroll 1
-            for (int q0 = 0; q0 < 8; q0 += 2) {
-                EpiOps2<2> st;
-                epi_issue(tile, 8 * w + q0, st);
-                epi_done(tile, 8 * w + q0, kc, st);
-            }
-        }
-        // (the next tile's y-tile writes follow its GEMM1 k-steps' barriers)
-    }
 }
 
 // v = a32[row] (+ b16[idx[row]]) -> [LayerNorm] -> out32 / out16
@@ -1903,17 +1629,16 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
         DPVO_CHECK_LAUNCH();
         return 0;
     }
-#ifdef DPVO_CHAIN64
-    if (f == DPVO_RG_RES && relu1 && !g2->res16) {
-        const int64_t nt64 = (g1->M + R6_BM - 1) / R6_BM;
-        const unsigned grid64 =
-            (unsigned)std::max<int64_t>(std::min<int64_t>(nt64, 2 * g_num_cus), (nt64 + R6_IDX_TILES - 1) / R6_IDX_TILES);
-        hipLaunchKernelGGL((rowchain64_kernel<DPVO_RG_RES | RG_NOADD, RG_RELU, DPVO_CHAIN64 >= 2, DPVO_CHAIN64 == 3 ? 1 : 2>), dim3(grid64), dim3(R5_THREADS), 0,
-                           as_stream(stream), *g1, a2);
+    if (f == DPVO_RG_RES && !g2->res16) {   // (c1 / c2: no addend loads, + 0 in their place)
+        if (relu1)
+            hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | RG_NOADD, false, 0, RG_RELU>), dim3(grid),
+                               dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, a2);
+        else
+            hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | RG_NOADD>), dim3(grid), dim3(R5_THREADS), 0,
+                               as_stream(stream), *g1, a2, a2);
         DPVO_CHECK_LAUNCH();
         return 0;
     }
-#endif
     switch (f) {
 #define RCH_CASE(F)                                                                                                   \
     case (F):                                                                                                         \
