@@ -1,7 +1,9 @@
 #!/bin/bash
-# A/B of rowchain experiment builds (scripts/build_exp.sh) on c1 / c2's chain
-# at C3's shape: the chain tests and the whole-update pins on each build, then
-# timings interleaved twice.  LIBS= the exp/<name> builds, TESTS=0 skips tests.
+# A/B of update-operator experiment builds (scripts/build_exp.sh) at C3's
+# shape: the GEMM tests and the whole-update pins on each build, then timings
+# interleaved twice (TIMER= the timing script: exp_chain_time.py, c1 / c2's
+# chain, or exp_pair_time.py, SoftAgg's GEMM pairs).  LIBS= the exp/<name>
+# builds, TESTS=0 skips tests.
 set -u
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -19,9 +21,9 @@ fi
 for r in 1 2; do
   for lib in product ${LIBS:-c64}; do
     if [ "$lib" = product ]; then
-      timeout -k 10 300 python -u scripts/exp_chain_time.py --tag product >> "$out" 2>&1 || exit $?
+      timeout -k 10 300 python -u scripts/${TIMER:-exp_chain_time.py} --tag product >> "$out" 2>&1 || exit $?
     else
-      DPVO_DIAG=1 DPVO_HOT_LIB=exp/$lib/libdpvo_hot.so timeout -k 10 300 python -u scripts/exp_chain_time.py --tag $lib >> "$out" 2>&1 || exit $?
+      DPVO_DIAG=1 DPVO_HOT_LIB=exp/$lib/libdpvo_hot.so timeout -k 10 300 python -u scripts/${TIMER:-exp_chain_time.py} --tag $lib >> "$out" 2>&1 || exit $?
     fi
     tail -1 "$out"
   done

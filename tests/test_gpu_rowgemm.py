@@ -168,6 +168,18 @@ def test_kblocked_w_is_bit_identical(M, flags):
     assert same(out[:h], want[:h]) and bool((out[h:] == 7.0).all())
     f, g = U.rowgemm_pair(A, U.kblock(Wa), ba, U.kblock(Wb), bb)
     assert same(f, U.rowgemm(A, Wa, ba)[1]) and same(g, U.rowgemm(A, Wb, bb)[1])
+    # the pair with the A tile resident (K = 384) under a device row count, and
+    # the ring-streamed pair (K = 896 and K = 64: the tile does not fit, or is
+    # shorter than the staging depth)
+    f2, g2 = U.rowgemm_pair(A, U.kblock(Wa), ba, U.kblock(Wb), bb, M_dev=Md)
+    assert same(f2[:h], f[:h]) and same(g2[:h], g[:h])
+    W16b, b16b = U.pack_linear(*lin(K, 10))
+    f, g = U.rowgemm_pair(buf, U.kblock(W16), b16, U.kblock(W16b), b16b)
+    assert same(f, U.rowgemm(buf, W16, b16)[1]) and same(g, U.rowgemm(buf, W16b, b16b)[1])
+    (W64a, b64a), (W64b, b64b) = U.pack_linear(*lin(64, 11)), U.pack_linear(*lin(64, 12))
+    A64 = A[:, :64]
+    f, g = U.rowgemm_pair(A64, U.kblock(W64a), b64a, U.kblock(W64b), b64b)
+    assert same(f, U.rowgemm(A64, W64a, b64a)[1]) and same(g, U.rowgemm(A64, W64b, b64b)[1])
     with pytest.raises(RuntimeError):
         U.rowgemm(A, U.kblock(Wa), ba, flags=U.RES, res32=torch.zeros(M, D, device="cuda"))
 

@@ -612,15 +612,11 @@ __device__ __forceinline__ h8_t r5_cvt(const R5PreRaw& x)
     return y;
 }
 
-template <int FLAGS, bool DUAL, bool PRE = false>
-__global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_args p, dpvo_rowgemm_args p2,
-                                                                 dpvo_rowadd_args pre)
+template <int FLAGS, bool DUAL>
+__global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_args p, dpvo_rowgemm_args p2)
 {
     static_assert((FLAGS & ~(RG_RELU | RG_SIGMOID)) == 0, "v5: plain GEMMs only");
-    // (PRE: the addend-source table, then both passes' biases -- in LDS, not
-    // registers: the staged fp32 + fp16 A register sets leave none to spare)
-    constexpr int PRE_BIAS = R5_LDS + R5_PRE_IDX_TILES * RG_BM * 8;
-    __shared__ __attribute__((aligned(16))) char smem[R5_LDS + (PRE ? R5_PRE_IDX_TILES * RG_BM * 8 + 2 * RG_BN * 2 : 0)];
+    __shared__ __attribute__((aligned(16))) char smem[R5_LDS];
     typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -634,68 +630,30 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     const YMapChunk ym;
     const int fr = lane & 15, fq = lane >> 4;
     const half_t* __restrict__ zero = (const half_t*)p.zero_row;
-    // PRE: the addend rows' sources -- the first tile's read directly in the
-    // prologue, the block's later tiles' from an LDS table filled after the
-    // prologue's loads are issued (published by the first k-step's barrier),
-    // so that crossing into the next tile inside the k-loop waits on LDS, not
-    // (vmcnt 0) on every load in flight; the host sizes the grid so that a
-    // block has <= R5_PRE_IDX_TILES tiles
-    int64_t* idx_lds = (int64_t*)(smem + R5_LDS);
-    auto pre_src = [&](int64_t m) __attribute__((always_inline)) -> int64_t {
-        return (m < Mrows && pre.b16) ? (pre.b_idx ? pre.b_idx[m] : m) : -1;
-    };
     // ---- A staging: lane holds row 16 w + (lane >> 2), logical chunk lane & 3
     const int ar = 16 * w + (lane >> 2), ac = lane & 3;
 
     int64_t a_tile = -1;
-    int a_lt = -1;                   // PRE: the block-local index of a_tile
     const half_t* arow = zero;
-    const float* arow32 = nullptr;   // PRE
-    auto pre_set = [&](int64_t t, int64_t s) __attribute__((always_inline)) {
-        const int64_t m = t * RG_BM + ar;
-        // rows past M read row 0 (finite; their outputs are never stored)
-        arow32 = (const float*)pre.a + (m < Mrows ? m : 0) * pre.lda + 8 * ac;
-        const half_t* b = (const half_t*)g_pre_negzero.v;
-        if (s >= 0 && s < pre.b_rows) b = (const half_t*)pre.b16 + s * RG_BN;
-        arow = b + 8 * ac;
-    };
-    if constexpr (PRE) {   // the first tile, from global (the table is filled after the prologue)
-        a_tile = blockIdx.x;
-        a_lt = 0;
-        pre_set(a_tile, pre_src(a_tile * RG_BM + ar));
-    }
     auto a_row = [&](int64_t t) __attribute__((always_inline)) {
         if (t == a_tile) return;
         a_tile = t;
         const int64_t m = t * RG_BM + ar;
-        if constexpr (PRE) {
-            a_lt++;
-            pre_set(t, idx_lds[a_lt * RG_BM + ar]);
-        } else {
-            const half_t* row = zero;
-            if (p.a_idx) {   // (the index load's wait inside the branch, not at the join)
-                if (m < Mrows) {
-                    const int64_t src = p.a_idx[m];
-                    if (src >= 0 && src < p.a_rows) row = (const half_t*)p.A + src * p.lda;
-                }
-            } else if (m < Mrows && m < p.a_rows) {
-                row = (const half_t*)p.A + m * p.lda;
+        const half_t* row = zero;
+        if (p.a_idx) {   // (the index load's wait inside the branch, not at the join)
+            if (m < Mrows) {
+                const int64_t src = p.a_idx[m];
+                if (src >= 0 && src < p.a_rows) row = (const half_t*)p.A + src * p.lda;
             }
-            arow = row + 8 * ac;
+        } else if (m < Mrows && m < p.a_rows) {
+            row = (const half_t*)p.A + m * p.lda;
         }
+        arow = row + 8 * ac;
     };
-    r5_areg_t<PRE> areg[2];
-    auto load_a = [&](const R5Cursor& c) __attribute__((always_inline)) -> r5_areg_t<PRE> {
+    h8_t areg[2];
+    auto load_a = [&](const R5Cursor& c) __attribute__((always_inline)) -> h8_t {
         a_row(c.t);
-        if constexpr (PRE) {
-            R5PreRaw x;
-            x.lo = *(const f4_t*)(arow32 + c.k * R5_BK);
-            x.hi = *(const f4_t*)(arow32 + c.k * R5_BK + 4);
-            x.b = *(const h8_t*)(arow + c.k * R5_BK);
-            return x;
-        } else {
-            return *(const h8_t*)(arow + c.k * R5_BK);
-        }
+        return *(const h8_t*)(arow + c.k * R5_BK);
     };
     // slot image: row r, physical chunk ac ^ rc_sw(r) holds logical chunk ac
     const int aw_off = ar * 64 + 16 * (ac ^ rc_sw(ar));
@@ -709,21 +667,13 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) r[nt] = *(const h8_t*)(src + nt * 16 * R5_BK);
     };
-    // ---- biases of this wave's columns, both passes (PRE: staged in LDS here,
-    // read by the epilogues, which follow the k-loop's barriers)
-    h4_t bias[PRE ? 1 : NP][3];
-    if constexpr (PRE) {
-        if (threadIdx.x < NP * 96) {
-            const int b = threadIdx.x / 96, c = 4 * (threadIdx.x % 96);
-            *(h4_t*)(smem + PRE_BIAS + b * RG_BN * 2 + 2 * c) = *(const h4_t*)((const half_t*)(b ? p2.bias : p.bias) + c);
-        }
-    } else {
+    // ---- biases of this wave's columns, both passes
+    h4_t bias[NP][3];
 #pragma unroll
-        for (int q = 0; q < NP; q++)
+    for (int q = 0; q < NP; q++)
 #pragma unroll
-            for (int nt = 0; nt < 3; nt++)
-                bias[q][nt] = *(const h4_t*)((const half_t*)(q ? p2.bias : p.bias) + 48 * w + 16 * nt + 4 * fq);
-    }
+        for (int nt = 0; nt < 3; nt++)
+            bias[q][nt] = *(const h4_t*)((const half_t*)(q ? p2.bias : p.bias) + 48 * w + 16 * nt + 4 * fq);
     f4_t acc[8][3];
 #pragma unroll
     for (int mt = 0; mt < 8; mt++)
@@ -737,11 +687,7 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
 #pragma unroll
         for (int nt = 0; nt < 3; nt++) {
             const int col = 48 * w + 16 * nt + 4 * fq;
-            h4_t bq;
-            if constexpr (PRE)
-                bq = *(const h4_t*)(smem + PRE_BIAS + q * RG_BN * 2 + 2 * col);
-            else
-                bq = bias[q][nt];
+            const h4_t bq = bias[q][nt];
 #pragma unroll
             for (int mt = 0; mt < 8; mt++) {
                 h4_t y;
@@ -802,7 +748,7 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     }
 #pragma unroll
     for (int r = 0; r < 2; r++) {
-        const h8_t x = r5_cvt(load_a(ca));
+        const h8_t x = load_a(ca);
         *(h8_t*)(smem + R5_Y + r * R5_ASLOT + aw_off) = x;
         ca.next(total, nks, NP, G);
     }
@@ -810,10 +756,6 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     for (int r = 0; r < 2; r++) {
         areg[r] = load_a(ca);
         ca.next(total, nks, NP, G);
-    }
-    if constexpr (PRE) {   // (stages 0-3 are the first tile's: NP nks >= 4, K % 64 == 0)
-        for (int i = RG_BM + threadIdx.x; i < (int)my_tiles * RG_BM; i += blockDim.x)
-            idx_lds[i] = pre_src(((int64_t)blockIdx.x + (int64_t)(i / RG_BM) * G) * RG_BM + i % RG_BM);
     }
 #ifdef DPVO_STAMPS
     unsigned long long st_sum[ST_SEGS] = {};
@@ -853,7 +795,7 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
         load_w(cw, wreg[PR]);                                                  // W stage f + 2
         cw.next(total, nks, NP, G);
         __builtin_amdgcn_sched_barrier(0);
-        *(h8_t*)(smem + R5_Y + ((PH + 2) & 3) * R5_ASLOT + aw_off) = r5_cvt(areg[PR]);   // stage f + 2
+        *(h8_t*)(smem + R5_Y + ((PH + 2) & 3) * R5_ASLOT + aw_off) = areg[PR];   // stage f + 2
         areg[PR] = load_a(ca);                                                         // stage f + 4
         ca.next(total, nks, NP, G);
         RC_STAMP(s3)
@@ -879,6 +821,261 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowgemm5_kernel(dpvo_rowgemm_ar
     if (lane == 0)
         for (int k = 0; k < ST_SEGS; k++) dpvo_stamps[((int64_t)blockIdx.x * 8 + w) * ST_SEGS + k] = st_sum[k];
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// rowpair6 (round 6): SoftAgg's f / g pair (rowgemm5 DUAL, K <= 384) with the
+// whole A tile resident in LDS.  rowgemm5 streams A through a 4-slot ring and
+// reads it twice, once per pass; the second read comes back from past L2 (the
+// round-5 counters: 152 MB fetched for agg_kk's 73 MB operand, 345 MB for
+// pair_pre's).  Here pass 0 stages every k-step of the tile into its own 8 KB
+// slot (96 KB at K = 384), pass 1 runs on those slots with no loads and no
+// barriers, and each pass's row epilogue goes out through half a y tile (48 KB,
+// 64 rows at a time).  During pass 1 the next tile's first two A stages load
+// into the registers the ring protocol uses; they reach slots 0 / 1 after pass
+// 1's epilogue.  Same MFMA operands in the same k order, the same epilogue
+// arithmetic: bit-identical to rowgemm5.
+// ---------------------------------------------------------------------------
+constexpr int P6_MAXK = 12;                                      // k-steps (K <= 384)
+constexpr int P6_YH = P6_MAXK * R5_ASLOT;                        // half y tile after the A tile
+constexpr int P6_IDX = P6_YH + 64 * 768;                         // PRE: addend sources
+constexpr int P6_BIAS = P6_IDX + R5_PRE_IDX_TILES * RG_BM * 8;   // PRE: both passes' biases
+constexpr int P6_LDS = P6_BIAS + 2 * RG_BN * 2;                  // 153.5 KB
+
+template <bool PRE>
+__global__ __launch_bounds__(R5_THREADS, 1) void rowpair6_kernel(dpvo_rowgemm_args p, dpvo_rowgemm_args p2,
+                                                                 dpvo_rowadd_args pre)
+{
+    __shared__ __attribute__((aligned(16))) char smem[P6_LDS];
+    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nks = p.K / R5_BK;   // even, 4 .. 12 (host-checked)
+    const int64_t Mrows = p.M_dev ? min(*p.M_dev, p.M) : p.M;
+    const int64_t ntiles = (Mrows + RG_BM - 1) / RG_BM;
+    if ((int64_t)blockIdx.x >= ntiles) return;
+    const unsigned G = gridDim.x;
+    const int64_t my_tiles = (ntiles - 1 - blockIdx.x) / G + 1;
+    const int64_t total_w = my_tiles * 2 * nks;
+    const YMapChunk ym;
+    const int fr = lane & 15, fq = lane >> 4;
+    const half_t* __restrict__ zero = (const half_t*)p.zero_row;
+    int64_t* idx_lds = (int64_t*)(smem + P6_IDX);
+    auto pre_src = [&](int64_t m) __attribute__((always_inline)) -> int64_t {
+        return (m < Mrows && pre.b16) ? (pre.b_idx ? pre.b_idx[m] : m) : -1;
+    };
+    // ---- A staging (rowgemm5's): lane holds row 16 w + (lane >> 2), chunk lane & 3
+    const int ar = 16 * w + (lane >> 2), ac = lane & 3;
+    int64_t a_tile = -1;
+    int a_lt = -1;
+    const half_t* arow = zero;
+    const float* arow32 = nullptr;
+    auto pre_set = [&](int64_t t, int64_t s) __attribute__((always_inline)) {
+        const int64_t m = t * RG_BM + ar;
+        arow32 = (const float*)pre.a + (m < Mrows ? m : 0) * pre.lda + 8 * ac;
+        const half_t* b = (const half_t*)g_pre_negzero.v;
+        if (s >= 0 && s < pre.b_rows) b = (const half_t*)pre.b16 + s * RG_BN;
+        arow = b + 8 * ac;
+    };
+    if constexpr (PRE) {
+        a_tile = blockIdx.x;
+        a_lt = 0;
+        pre_set(a_tile, pre_src(a_tile * RG_BM + ar));
+    }
+    auto a_row = [&](int64_t t) __attribute__((always_inline)) {
+        if (t == a_tile) return;
+        a_tile = t;
+        const int64_t m = t * RG_BM + ar;
+        if constexpr (PRE) {
+            a_lt++;
+            pre_set(t, idx_lds[a_lt * RG_BM + ar]);
+        } else {
+            const half_t* row = zero;
+            if (p.a_idx) {
+                if (m < Mrows) {
+                    const int64_t src = p.a_idx[m];
+                    if (src >= 0 && src < p.a_rows) row = (const half_t*)p.A + src * p.lda;
+                }
+            } else if (m < Mrows && m < p.a_rows) {
+                row = (const half_t*)p.A + m * p.lda;
+            }
+            arow = row + 8 * ac;
+        }
+    };
+    r5_areg_t<PRE> areg[2];
+    auto load_a = [&](int64_t t, int k) __attribute__((always_inline)) -> r5_areg_t<PRE> {
+        a_row(t);
+        if constexpr (PRE) {
+            R5PreRaw x;
+            x.lo = *(const f4_t*)(arow32 + k * R5_BK);
+            x.hi = *(const f4_t*)(arow32 + k * R5_BK + 4);
+            x.b = *(const h8_t*)(arow + k * R5_BK);
+            return x;
+        } else {
+            return *(const h8_t*)(arow + k * R5_BK);
+        }
+    };
+    const int aw_off = ar * 64 + 16 * (ac ^ rc_sw(ar));
+    auto put_a = [&](int slot, const r5_areg_t<PRE>& x) __attribute__((always_inline)) {
+        *(h8_t*)(smem + slot * R5_ASLOT + aw_off) = r5_cvt(x);
+    };
+    // ---- W fragments (rowgemm5's flat (tile, pass, k-step) stream, two ahead)
+    h8_t wreg[2][3];
+    const half_t* W1 = (const half_t*)p.W;
+    const half_t* W2 = (const half_t*)p2.W;
+    const int wcol = (48 * w + fr) * R5_BK + 8 * fq;
+    auto load_w = [&](const R5Cursor& c, h8_t (&r)[3]) __attribute__((always_inline)) {
+        const half_t* src = (c.q ? W2 : W1) + (int64_t)c.k * (RG_BN * R5_BK) + wcol;
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) r[nt] = *(const h8_t*)(src + nt * 16 * R5_BK);
+    };
+    h4_t bias[PRE ? 1 : 2][3];
+    if constexpr (PRE) {
+        if (threadIdx.x < 2 * 96) {
+            const int b = threadIdx.x / 96, c = 4 * (threadIdx.x % 96);
+            *(h4_t*)(smem + P6_BIAS + b * RG_BN * 2 + 2 * c) = *(const h4_t*)((const half_t*)(b ? p2.bias : p.bias) + c);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+            for (int nt = 0; nt < 3; nt++)
+                bias[q][nt] = *(const h4_t*)((const half_t*)(q ? p2.bias : p.bias) + 48 * w + 16 * nt + 4 * fq);
+    }
+    f4_t acc[8][3];
+#pragma unroll
+    for (int mt = 0; mt < 8; mt++)
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+    const int ar_off = fr * 64 + 16 * (fq ^ rc_sw(fr));   // + 1024 mt: row 16 mt + fr
+    auto sync = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+        __builtin_amdgcn_s_barrier();
+    };
+    // pass q's rows out, 64 at a time through the half y tile (rowgemm5's
+    // conversion and whole-row stores); ends on a barrier
+    auto epilogue = [&](int64_t t, auto qc) __attribute__((always_inline)) {
+        constexpr int q = decltype(qc)::value;
+        const dpvo_rowgemm_args& pe = q ? p2 : p;
+        half_t* out = (half_t*)pe.out16;
+        const bool al16 = ((uintptr_t)out & 15) == 0 && (pe.ldo16 & 7) == 0;
+#pragma unroll
+        for (int hh = 0; hh < 2; hh++) {
+#pragma unroll
+            for (int nt = 0; nt < 3; nt++) {
+                const int col = 48 * w + 16 * nt + 4 * fq;
+                h4_t bq;
+                if constexpr (PRE)
+                    bq = *(const h4_t*)(smem + P6_BIAS + q * RG_BN * 2 + 2 * col);
+                else
+                    bq = bias[q][nt];
+#pragma unroll
+                for (int m4 = 0; m4 < 4; m4++) {
+                    const int mt = 4 * hh + m4;
+                    h4_t y;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) y[r] = (half_t)(acc[mt][nt][r] + (float)bq[r]);
+                    acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+                    *(h4_t*)(smem + P6_YH + ym.off(16 * m4 + fr, col * 2)) = y;
+                }
+            }
+            sync();
+            const int64_t row0 = t * RG_BM + 64 * hh;
+            if (al16) {   // wave w: rows 8 w .. 8 w + 7 of the half, one 768-byte row per instruction
+                if (lane < 48) {
+#pragma unroll 4
+                    for (int i = 0; i < 8; i++) {
+                        const int lr = 8 * w + i;
+                        const h8_t v = *(const h8_t*)(smem + P6_YH + ym.off(lr, 16 * lane));
+                        if (row0 + lr < Mrows) *(h8_t*)(out + (row0 + lr) * pe.ldo16 + 8 * lane) = v;
+                    }
+                }
+            } else {   // 8-byte aligned rows: two rows per pass
+                const int h = lane >> 5, s = lane & 31;
+#pragma unroll 2
+                for (int i = 0; i < 4; i++) {
+                    const int lr = 8 * w + 2 * i + h;
+                    ep_h4 v[3];
+#pragma unroll
+                    for (int j = 0; j < 3; j++) v[j] = *(const ep_h4*)(smem + P6_YH + ym.off(lr, (128 * j + 4 * s) * 2));
+                    if (row0 + lr < Mrows) {
+#pragma unroll
+                        for (int j = 0; j < 3; j++) *(ep_h4*)(out + (row0 + lr) * pe.ldo16 + 128 * j + 4 * s) = v[j];
+                    }
+                }
+            }
+            sync();
+        }
+    };
+
+    // ---- prologue: W steps 0, 1; the first tile's A stages 0, 1 in slots 0, 1, 2, 3 in registers
+    R5Cursor cw{0, (int64_t)blockIdx.x, 0, 0};
+    auto wnext = [&]() __attribute__((always_inline)) { cw.next(total_w, nks, 2, G); };
+    load_w(cw, wreg[0]);
+    wnext();
+    load_w(cw, wreg[1]);
+    wnext();
+    put_a(0, load_a(blockIdx.x, 0));
+    put_a(1, load_a(blockIdx.x, 1));
+    areg[0] = load_a(blockIdx.x, 2);
+    areg[1] = load_a(blockIdx.x, 3);
+    if constexpr (PRE) {
+        for (int i = RG_BM + threadIdx.x; i < (int)my_tiles * RG_BM; i += blockDim.x)
+            idx_lds[i] = pre_src(((int64_t)blockIdx.x + (int64_t)(i / RG_BM) * G) * RG_BM + i % RG_BM);
+    }
+    auto mfmas = [&](int slot, const h8_t (&wr)[3]) __attribute__((always_inline)) {
+        const char* sa = smem + slot * R5_ASLOT;
+        h8_t a[8];
+#pragma unroll
+        for (int mt = 0; mt < 8; mt++) a[mt] = *(const h8_t*)(sa + ar_off + 1024 * mt);
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++)
+#pragma unroll
+            for (int mt = 0; mt < 8; mt++)
+                acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[nt], a[mt], acc[mt][nt], 0, 0, 0);
+    };
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
+        const bool more = tile + G < ntiles;
+        // ---- pass 0: k-step ks reads slot ks, then stage ks + 2 goes from its
+        // register set into slot ks + 2 and stage ks + 4 is loaded; one barrier
+        // per two k-steps makes stages ks, ks + 1 visible (no slot is reused
+        // within the tile, so no barrier guards a rewrite)
+#pragma unroll 1
+        for (int ks = 0; ks < nks; ks += 2) {
+            bd_steps<0, 2>::run([&](auto pc) __attribute__((always_inline)) {
+                constexpr int PH = decltype(pc)::value;
+                const int k = ks + PH;
+                if (PH == 0) sync();
+                mfmas(k, wreg[PH]);
+                load_w(cw, wreg[PH]);
+                wnext();
+                __builtin_amdgcn_sched_barrier(0);
+                if (k + 2 < nks) {
+                    put_a(k + 2, areg[PH]);
+                    if (k + 4 < nks) areg[PH] = load_a(tile, k + 4);
+                }
+            });
+        }
+        epilogue(tile, std::integral_constant<int, 0>{});
+        // ---- pass 1 on the resident tile; the next tile's stages 0, 1 load meanwhile
+#pragma unroll 1
+        for (int ks = 0; ks < nks; ks += 2) {
+            bd_steps<0, 2>::run([&](auto pc) __attribute__((always_inline)) {
+                constexpr int PH = decltype(pc)::value;
+                mfmas(ks + PH, wreg[PH]);
+                load_w(cw, wreg[PH]);
+                wnext();
+                if (ks == 0 && more) areg[PH] = load_a(tile + G, PH);
+            });
+        }
+        epilogue(tile, std::integral_constant<int, 1>{});
+        if (more) {   // (every wave is past its pass-1 reads: the epilogue's barriers)
+            put_a(0, areg[0]);
+            put_a(1, areg[1]);
+            areg[0] = load_a(tile + G, 2);
+            areg[1] = load_a(tile + G, 3);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1492,9 +1689,11 @@ extern "C" int dpvo_rowgemm_pair(const dpvo_rowgemm_args* a, const dpvo_rowgemm_
     if (ensure_num_cus()) return -1;
     const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
     const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
-    if (a->flags & DPVO_RG_WKB)
-        hipLaunchKernelGGL((rowgemm5_kernel<0, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b,
+    if ((a->flags & DPVO_RG_WKB) && a->K / R5_BK <= P6_MAXK && a->K / R5_BK >= 4)   // (the A tile fits LDS)
+        hipLaunchKernelGGL((rowpair6_kernel<false>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b,
                            dpvo_rowadd_args{});
+    else if (a->flags & DPVO_RG_WKB)
+        hipLaunchKernelGGL((rowgemm5_kernel<0, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b);
     else
         hipLaunchKernelGGL((rowgemm3_kernel<0, true>), dim3(grid), dim3(RG_THREADS), 0, as_stream(stream), *a, *b);
     DPVO_CHECK_LAUNCH();
@@ -1521,8 +1720,7 @@ extern "C" int dpvo_rowgemm_pair_pre(const dpvo_rowgemm_args* a, const dpvo_rowg
     // (at least ntiles / R5_PRE_IDX_TILES blocks: a block's addend sources fit its LDS table)
     const unsigned grid =
         (unsigned)std::max<int64_t>(std::min<int64_t>(ntiles, g_num_cus), (ntiles + R5_PRE_IDX_TILES - 1) / R5_PRE_IDX_TILES);
-    hipLaunchKernelGGL((rowgemm5_kernel<0, true, true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b,
-                       *pre);
+    hipLaunchKernelGGL((rowpair6_kernel<true>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, *b, *pre);
     DPVO_CHECK_LAUNCH();
     return 0;
 }
@@ -1539,7 +1737,7 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
 #define R5_CASE(F)                                                                                                  \
     case (F) | DPVO_RG_WKB:                                                                                         \
         hipLaunchKernelGGL((rowgemm5_kernel<(F), false>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, \
-                           *a, dpvo_rowadd_args{});                                                                 \
+                           *a);                                                                                     \
         break;
         R5_CASE(0)
         R5_CASE(DPVO_RG_RELU)
