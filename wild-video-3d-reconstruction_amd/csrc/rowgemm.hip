@@ -1034,8 +1034,18 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowpair6_kernel(dpvo_rowgemm_ar
             for (int mt = 0; mt < 8; mt++)
                 acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wr[nt], a[mt], acc[mt][nt], 0, 0, 0);
     };
+#ifdef DPVO_STAMPS
+    // segments: 0 pass-0 barrier waits, 1 pass-0 k-steps otherwise, 2 pass-0
+    // epilogue, 3 pass 1, 4 pass-1 epilogue + next stages, 10 total, 11 tiles
+    unsigned long long st_sum[ST_SEGS] = {};
+    RC_STAMP(p_begin)
+#endif
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += G) {
         const bool more = tile + G < ntiles;
+#ifdef DPVO_STAMPS
+        st_sum[11] += 1;
+        RC_STAMP(q0)
+#endif
         // ---- pass 0: k-step ks reads slot ks, then stage ks + 2 goes from its
         // register set into slot ks + 2 and stage ks + 4 is loaded; one barrier
         // per two k-steps makes stages ks, ks + 1 visible (no slot is reused
@@ -1045,7 +1055,10 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowpair6_kernel(dpvo_rowgemm_ar
             bd_steps<0, 2>::run([&](auto pc) __attribute__((always_inline)) {
                 constexpr int PH = decltype(pc)::value;
                 const int k = ks + PH;
+                RC_STAMP(b0)
                 if (PH == 0) sync();
+                RC_STAMP(b1)
+                RC_ACC(0, b0, b1)
                 mfmas(k, wreg[PH]);
                 load_w(cw, wreg[PH]);
                 wnext();
@@ -1056,7 +1069,15 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowpair6_kernel(dpvo_rowgemm_ar
                 }
             });
         }
+#ifdef DPVO_STAMPS
+        RC_STAMP(q1)
+        st_sum[1] += q1 - q0;
+#endif
         epilogue(tile, std::integral_constant<int, 0>{});
+#ifdef DPVO_STAMPS
+        RC_STAMP(q2)
+        RC_ACC(2, q1, q2)
+#endif
         // ---- pass 1 on the resident tile; the next tile's stages 0, 1 load meanwhile
 #pragma unroll 1
         for (int ks = 0; ks < nks; ks += 2) {
@@ -1068,6 +1089,10 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowpair6_kernel(dpvo_rowgemm_ar
                 if (ks == 0 && more) areg[PH] = load_a(tile + G, PH);
             });
         }
+#ifdef DPVO_STAMPS
+        RC_STAMP(q3)
+        RC_ACC(3, q2, q3)
+#endif
         epilogue(tile, std::integral_constant<int, 1>{});
         if (more) {   // (every wave is past its pass-1 reads: the epilogue's barriers)
             put_a(0, areg[0]);
@@ -1075,7 +1100,18 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowpair6_kernel(dpvo_rowgemm_ar
             areg[0] = load_a(tile + G, 2);
             areg[1] = load_a(tile + G, 3);
         }
+#ifdef DPVO_STAMPS
+        RC_STAMP(q4)
+        RC_ACC(4, q3, q4)
+#endif
     }
+#ifdef DPVO_STAMPS
+    RC_STAMP(p_end)
+    st_sum[1] -= st_sum[0];   // (segment 1 held the whole pass 0)
+    st_sum[10] += p_end - p_begin;
+    if (lane == 0)
+        for (int k = 0; k < ST_SEGS; k++) dpvo_stamps[((int64_t)blockIdx.x * 8 + w) * ST_SEGS + k] = st_sum[k];
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1625,6 +1661,108 @@ __global__ __launch_bounds__(256) void rowadd_ln_kernel(dpvo_rowadd_args p)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Narrow tiles (round 6) for the device-counted GEMMs -- SoftAgg's h Linear
+// on the groups (`rowgemm(y, *ph, M_dev=G)`, net.py): G (~4.4k patch groups,
+// a few hundred frame-pair groups at C3) is known only on the device, so
+// rowgemm5 launched for the upper bound put it on 35 / 4 busy workgroups of
+// 128 rows: 15 us a launch, bound by each workgroup's L1 traffic (the whole
+// 288 KB W per tile).  Here a workgroup takes 32 rows x 192 columns (two per
+// row tile; 4 waves x 48 columns, 2 x 3 accumulators): the A tile is loaded
+// once into LDS (XOR-swizzled 16-byte chunks: conflict-free fragment reads),
+// each wave streams its W fragments from L2 two k-steps ahead, and each lane
+// stores its 4 columns of each row.  Same 16 x 16 x 32 blocks in the same k
+// order, the same epilogue rounding: bit-identical to rowgemm5.
+// ---------------------------------------------------------------------------
+#ifndef DPVO_RN_WD
+#define DPVO_RN_WD 2
+#endif
+constexpr int RN_BM = 32, RN_THREADS = 256, RN_MAXK = 896, RN_WD = DPVO_RN_WD;   // W k-steps in flight
+
+template <int FLAGS, int KC>   // KC = K / 64: the A chunks each thread stages
+__global__ __launch_bounds__(RN_THREADS) void rowgemm_narrow_kernel(dpvo_rowgemm_args p)
+{
+    static_assert((FLAGS & ~(RG_RELU | RG_SIGMOID)) == 0, "narrow: plain GEMMs only");
+    __shared__ __attribute__((aligned(16))) char sA[RN_BM * RN_MAXK * 2];
+    typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int fr = lane & 15, fq = lane >> 4;
+    constexpr int K = 64 * KC, nks = K / R5_BK, rowb = 2 * K;
+    static_assert(K <= RN_MAXK && K % 128 == 0, "narrow: the A tile's swizzle needs K % 128 == 0");
+    static_assert(nks % RN_WD == 0, "narrow: whole groups of W k-steps");
+    const int64_t Mrows = p.M_dev ? min(*p.M_dev, p.M) : p.M;
+    const int64_t ntiles = (Mrows + RN_BM - 1) / RN_BM;
+    const int c0 = 192 * (blockIdx.x & 1) + 48 * w;   // this wave's first column
+    const half_t* __restrict__ W = (const half_t*)p.W + (c0 + fr) * R5_BK + 8 * fq;
+    half_t* out = (half_t*)p.out16;
+    auto soff = [&](int r, int c) __attribute__((always_inline)) { return r * rowb + ((c ^ (r & 15)) << 4); };
+    h4_t bias[3];
+#pragma unroll
+    for (int nt = 0; nt < 3; nt++) bias[nt] = *(const h4_t*)((const half_t*)p.bias + c0 + 16 * nt + 4 * fq);
+    const int ar = threadIdx.x >> 3, ac = threadIdx.x & 7;   // staging: row ar, chunks ac + 8 j
+    for (int64_t t = blockIdx.x >> 1; t < ntiles; t += gridDim.x >> 1) {
+        // ---- the A tile into LDS: all KC loads of a thread in flight together
+        const int64_t m = t * RN_BM + ar;
+        const half_t* row = (const half_t*)p.zero_row;
+        if (m < Mrows) {
+            const int64_t src = p.a_idx ? p.a_idx[m] : m;
+            if (src >= 0 && src < p.a_rows) row = (const half_t*)p.A + src * p.lda;
+        }
+        h8_t st[KC];
+#pragma unroll
+        for (int j = 0; j < KC; j++) st[j] = *(const h8_t*)(row + 8 * (ac + 8 * j));
+#pragma unroll
+        for (int j = 0; j < KC; j++) *(h8_t*)(sA + soff(ar, ac + 8 * j)) = st[j];
+        __syncthreads();
+        f4_t acc[2][3];
+#pragma unroll
+        for (int mt = 0; mt < 2; mt++)
+#pragma unroll
+            for (int nt = 0; nt < 3; nt++) acc[mt][nt] = f4_t{0.f, 0.f, 0.f, 0.f};
+        h8_t wf[RN_WD][3];
+        auto load_w = [&](int ks, h8_t (&wr)[3]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int nt = 0; nt < 3; nt++) wr[nt] = *(const h8_t*)(W + (int64_t)ks * (RG_BN * R5_BK) + nt * 16 * R5_BK);
+        };
+#pragma unroll
+        for (int d = 0; d < RN_WD; d++) load_w(d, wf[d]);
+#pragma unroll 1
+        for (int ks = 0; ks < nks; ks += RN_WD) {
+            bd_steps<0, RN_WD>::run([&](auto pc) __attribute__((always_inline)) {
+                constexpr int S = decltype(pc)::value;
+                h8_t a[2];
+#pragma unroll
+                for (int mt = 0; mt < 2; mt++) a[mt] = *(const h8_t*)(sA + soff(16 * mt + fr, 4 * (ks + S) + fq));
+#pragma unroll
+                for (int nt = 0; nt < 3; nt++)
+#pragma unroll
+                    for (int mt = 0; mt < 2; mt++)
+                        acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[S][nt], a[mt], acc[mt][nt], 0, 0, 0);
+                load_w(min(ks + S + RN_WD, nks - 1), wf[S]);   // (unconditional: exact wait counts)
+            });
+        }
+#pragma unroll
+        for (int nt = 0; nt < 3; nt++) {
+            const int col = c0 + 16 * nt + 4 * fq;
+#pragma unroll
+            for (int mt = 0; mt < 2; mt++) {
+                h4_t y;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    half_t v = (half_t)(acc[mt][nt][r] + (float)bias[nt][r]);
+                    if (FLAGS & RG_RELU) v = v > (half_t)0 ? v : (half_t)0;
+                    if (FLAGS & RG_SIGMOID) v = (half_t)fast_sigmoid((float)v);
+                    y[r] = v;
+                }
+                const int64_t row = t * RN_BM + 16 * mt + fr;
+                if (row < Mrows) *(h4_t*)(out + row * p.ldo16 + col) = y;
+            }
+        }
+        __syncthreads();   // (every wave's A reads before the next tile's writes)
+    }
+}
+
 int g_num_cus = 0;
 
 }  // namespace
@@ -1733,11 +1871,22 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
     if (ensure_num_cus()) return -1;
     const int64_t ntiles = (a->M + RG_BM - 1) / RG_BM;
     const unsigned grid = (unsigned)std::min<int64_t>(ntiles, g_num_cus);
+    // a device row count (the SoftAgg group GEMMs: G rows of an upper bound M,
+    // G << M) takes the narrow 32-row tiles
+    const unsigned grid_n = 2 * (unsigned)std::min<int64_t>((a->M + RN_BM - 1) / RN_BM, 2 * (int64_t)g_num_cus);
+    const bool narrow = a->M_dev && (a->K == 384 || a->K == 896);
     switch (f) {
-#define R5_CASE(F)                                                                                                  \
-    case (F) | DPVO_RG_WKB:                                                                                         \
-        hipLaunchKernelGGL((rowgemm5_kernel<(F), false>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, \
-                           *a);                                                                                     \
+#define R5_CASE(F)                                                                                                    \
+    case (F) | DPVO_RG_WKB:                                                                                           \
+        if (narrow && a->K == 384)                                                                                    \
+            hipLaunchKernelGGL((rowgemm_narrow_kernel<(F), 6>), dim3(grid_n), dim3(RN_THREADS), 0, as_stream(stream), \
+                               *a);                                                                                   \
+        else if (narrow)                                                                                              \
+            hipLaunchKernelGGL((rowgemm_narrow_kernel<(F), 14>), dim3(grid_n), dim3(RN_THREADS), 0,                   \
+                               as_stream(stream), *a);                                                                \
+        else                                                                                                          \
+            hipLaunchKernelGGL((rowgemm5_kernel<(F), false>), dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *a, \
+                               *a);                                                                                   \
         break;
         R5_CASE(0)
         R5_CASE(DPVO_RG_RELU)
