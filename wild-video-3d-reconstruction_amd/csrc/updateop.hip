@@ -697,8 +697,18 @@ __global__ __launch_bounds__(256) void wg_hist_kernel(const int64_t* __restrict_
                                                       int* __restrict__ slot_ij, uint32_t* __restrict__ key_kk,
                                                       uint32_t* __restrict__ key_ij)
 {
+    // the (ii, jj) keys: a patch's edges go to different frame pairs, so a
+    // wave's lanes rarely share one and ~500 bins took every edge's atomic; a
+    // workgroup ranks its edges in an LDS histogram instead and reserves each
+    // touched bin's range with one global atomic (the slots within a bin are
+    // ordered by wg_fix afterwards, as before).  The kk keys come in runs (a
+    // patch's edges are adjacent): one atomic per run, cb_run_slot.
+    constexpr int BIJ = 1 << WG_IJ_BITS;
+    __shared__ int lh[BIJ];
     const int lane = threadIdx.x & 63;
     for (int64_t e0 = blockIdx.x * (int64_t)blockDim.x; e0 < E; e0 += (int64_t)gridDim.x * blockDim.x) {
+        for (int i = threadIdx.x; i < BIJ; i += blockDim.x) lh[i] = 0;
+        __syncthreads();
         const int64_t e = e0 + threadIdx.x;   // uniform trip count: whole waves stay converged
         const bool valid = e < E;
         uint32_t kk_k = 0xffffffffu, ij_k = 0xffffffffu;
@@ -706,7 +716,7 @@ __global__ __launch_bounds__(256) void wg_hist_kernel(const int64_t* __restrict_
             const int64_t k = kk[e], j = jj[e];
             const int64_t a = ii[e] - base, b = j - base, kr = k - M * base;
             kk_k = (uint32_t)kr & mask_kk;
-            ij_k = (uint32_t)(a * 64 + b) & ((1u << WG_IJ_BITS) - 1);
+            ij_k = (uint32_t)(a * 64 + b) & (BIJ - 1);
             if (flag && (a < 0 || a >= 64 || b < 0 || b >= 64 || kr < 0 || kr >= 64 * M)) atomicCAS(flag, 0, -2);
             const int64_t r = k % ring, f = j % frames;
             ctx[e] = r < 0 ? r + ring : r;
@@ -715,11 +725,18 @@ __global__ __launch_bounds__(256) void wg_hist_kernel(const int64_t* __restrict_
             key_ij[e] = ij_k;
         }
         const int s_kk = cb_run_slot(kk_k, valid, lane, hist_kk);
-        const int s_ij = cb_run_slot(ij_k, valid, lane, hist_ij);
+        const int l_ij = valid ? atomicAdd(&lh[ij_k], 1) : 0;   // rank within this workgroup's share
+        __syncthreads();
+        for (int i = threadIdx.x; i < BIJ; i += blockDim.x) {
+            const int c = lh[i];
+            if (c) lh[i] = atomicAdd(&hist_ij[i], c);   // the workgroup's base in bin i
+        }
+        __syncthreads();
         if (valid) {
             slot_kk[e] = s_kk;
-            slot_ij[e] = s_ij;
+            slot_ij[e] = lh[ij_k] + l_ij;
         }
+        __syncthreads();   // (lh is cleared for the next round)
     }
 }
 
@@ -727,6 +744,7 @@ __global__ __launch_bounds__(256) void wg_hist_kernel(const int64_t* __restrict_
 // bin, the group count and offs[G] = E.  8192 bins per round: thread t loads
 // bins 8t .. 8t+7 (two 16-byte loads, coalesced), scans them in registers,
 // one block scan of the thread sums, 64-byte coalesced stores of the results.
+// (16 bins per thread, C3's 16384 kk bins in one round: 11.8 vs 11.4 us.)
 __global__ __launch_bounds__(1024) void wg_scan_kernel(const int* __restrict__ hist, int Bkk, int64_t* __restrict__ pre_kk,
                                                        int64_t* __restrict__ pre_ij, int* __restrict__ offs_kk,
                                                        int* __restrict__ offs_ij, int64_t* __restrict__ groups_kk,
@@ -771,21 +789,24 @@ __global__ __launch_bounds__(1024) void wg_scan_kernel(const int* __restrict__ h
     const int* h = ij ? hist + Bkk : hist;
     int64_t* pre = ij ? pre_ij : pre_kk;
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    constexpr int PT = 8;   // bins per thread
     int64_t carry = 0;
-    for (int base = 0; base < B; base += 8192) {
-        const int b0 = base + 8 * t;
-        int c[8];
-        if (b0 + 8 <= B && ((uintptr_t)(h + b0) & 15) == 0) {
-            const int4 x = *(const int4*)(h + b0), y = *(const int4*)(h + b0 + 4);
-            c[0] = x.x; c[1] = x.y; c[2] = x.z; c[3] = x.w;
-            c[4] = y.x; c[5] = y.y; c[6] = y.z; c[7] = y.w;
+    for (int base = 0; base < B; base += 1024 * PT) {
+        const int b0 = base + PT * t;
+        int c[PT];
+        if (b0 + PT <= B && ((uintptr_t)(h + b0) & 15) == 0) {
+#pragma unroll
+            for (int q = 0; q < PT / 4; q++) {
+                const int4 x = *(const int4*)(h + b0 + 4 * q);
+                c[4 * q] = x.x; c[4 * q + 1] = x.y; c[4 * q + 2] = x.z; c[4 * q + 3] = x.w;
+            }
         } else {
 #pragma unroll
-            for (int j = 0; j < 8; j++) c[j] = b0 + j < B ? h[b0 + j] : 0;
+            for (int j = 0; j < PT; j++) c[j] = b0 + j < B ? h[b0 + j] : 0;
         }
-        int64_t loc[8], s = 0;
+        int64_t loc[PT], s = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < PT; j++) {
             loc[j] = s;
             s += CbCombine()(c[j]);
         }
@@ -806,7 +827,7 @@ __global__ __launch_bounds__(1024) void wg_scan_kernel(const int* __restrict__ h
         }
         const int64_t ex = off + x - s;
 #pragma unroll
-        for (int j = 0; j < 8; j++)
+        for (int j = 0; j < PT; j++)
             if (b0 + j < B) pre[b0 + j] = ex + loc[j];
         carry += tot;
         __syncthreads();   // wsum is rewritten next round
