@@ -1,7 +1,9 @@
 """Where the c1 / c2 chain's time goes (rowchain5_kernel<RES>, csrc/rowgemm.hip,
 DPVO_STAMPS build in diag/libdpvo_hot.so): per tile, cycles in the GEMM1
 k-loop (with the previous tile's residual epilogue overlapped), the GEMM1 ->
-y tile write, GEMM2, the y-tile write, at C3 shapes (E = 95,424 gathered rows)."""
+y tile write, GEMM2, the y-tile write, at C3 shapes (E = 95,424 gathered rows).
+--tri: the corr chain instead (dpvo_rowchain3: K1 = 896, GEMM2 -> LayerNorm ->
+GEMM3 on the y tile, then the RES | LN epilogue with the gathered inp rows)."""
 import ctypes
 import os
 import sys
@@ -17,20 +19,31 @@ import _dpvo_hot as H  # noqa: E402
 import update_ops as U  # noqa: E402
 
 
-def main(E=95424):
+def main(E=95424, tri=False):
     g = torch.Generator(device="cuda").manual_seed(0)
     n16 = (0.5 * torch.randn(E, 384, generator=g, device="cuda")).half()
     n32 = torch.randn(E, 384, generator=g, device="cuda")
     nb = torch.randint(-1, E, (E,), generator=g, device="cuda")
     W = [U.kblock((torch.randn(384, 384, generator=g, device="cuda") / 20).half()) for _ in range(2)]
     b = torch.zeros(384, device="cuda").half()
+    if tri:
+        corr = (0.5 * torch.randn(E, 896, generator=g, device="cuda")).half()
+        W1 = U.kblock((torch.randn(384, 896, generator=g, device="cuda") / 30).half())
+        ring = torch.randn(192 * 36, 384, generator=g, device="cuda").half()
+        ridx = torch.randint(0, 192 * 36, (E,), generator=g, device="cuda")
+        ln = (torch.ones(384, device="cuda"), torch.zeros(384, device="cuda"), 1e-3)
+        fn = lambda: U.rowchain(corr, W1, b, W[1], b, flags1=U.RELU, mid=(W[0], b, ln), flags=U.RES | U.LN,  # noqa: E731
+                                res32=n32, res16=ring, res16_idx=ridx, ln=ln, want32=True)
+    else:
+        fn = lambda: U.rowchain(n16, W[0], b, W[1], b, flags1=U.RELU, a_idx=nb, flags=U.RES, res32=n32,  # noqa: E731
+                                want32=True)
     for _ in range(3):
-        U.rowchain(n16, W[0], b, W[1], b, flags1=U.RELU, a_idx=nb, flags=U.RES, res32=n32, want32=True)
+        fn()
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record()
     for _ in range(10):
-        U.rowchain(n16, W[0], b, W[1], b, flags1=U.RELU, a_idx=nb, flags=U.RES, res32=n32, want32=True)
+        fn()
     ev[1].record()
     torch.cuda.synchronize()
     print(f"chain: {ev[0].elapsed_time(ev[1]) / 10 * 1e3:.1f} us per launch (stamps inflate it)")
@@ -44,11 +57,11 @@ def main(E=95424):
     tiles = st[:, 0, 11]
     print(f"{nblk} blocks, tiles / block {tiles.mean():.2f} (max {tiles.max():.0f})")
     names = {0: "GEMM1 k-loop (+ OVL epilogue)", 1: "GEMM1 acc -> y tile + sync", 2: "GEMM2 + sync",
-             3: "GEMM2 + y-tile write + sync", 4: "row epilogue (non-OVL)", 10: "total"}
+             3: "GEMM2 (+ LN + GEMM3) + y-tile write + sync", 4: "row epilogue (non-OVL)", 10: "total"}
     for k, n in names.items():
         per = st[:, :, k].sum(0) / tiles.sum() if k != 10 else st[:, :, k].mean(0)
         print(f"  {n:32s} {per.mean():10.0f} cycles {'per tile' if k != 10 else 'per wave'}  (waves {np.round(per)})")
 
 
 if __name__ == "__main__":
-    main()
+    main(tri="--tri" in sys.argv)

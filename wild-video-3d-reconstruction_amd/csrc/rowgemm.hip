@@ -1161,6 +1161,9 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
 {
     constexpr bool TRI = FMID != 0;
     static_assert(!(TRI && GATED), "a chain is either gated or three GEMMs long");
+    // (RES | LN overlapped the same way -- the corr chain, the gated LN chain --
+    // measured 188 -> 197 us and 150 -> 150 us: its batches' loads queue ahead
+    // of the A stream's in the in-order vmcnt; profiles/r6/experiments/)
     constexpr bool OVL = (F2 & ~RG_NOADD) == RG_RES;
     constexpr int NSEG = (TRI || GATED) ? 3 : 2;
     constexpr int NPA = GATED ? 2 : 1;   // A passes per tile
@@ -1955,18 +1958,21 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
         a2.gate16 = nullptr;
         a2.res16 = nullptr;
         switch (f) {
+// (no res16 in a gated chain: the addend loads compiled out, RG_NOADD)
+#define RCG_NA RG_NOADD
 #define RCG_CASE(F)                                                                                                   \
     case (F):                                                                                                         \
         if (relu1)                                                                                                    \
-            hipLaunchKernelGGL((rowchain5_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES, true, 0, RG_RELU>), dim3(grid), \
-                               dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, *gate);                               \
+            hipLaunchKernelGGL((rowchain5_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES | RCG_NA, true, 0, RG_RELU>),    \
+                               dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, *gate);                   \
         else                                                                                                          \
-            hipLaunchKernelGGL((rowchain5_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES, true>), dim3(grid),             \
+            hipLaunchKernelGGL((rowchain5_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES | RCG_NA, true>), dim3(grid),    \
                                dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, *gate);                               \
         break;
             RCG_CASE(DPVO_RG_GATE | DPVO_RG_LN)
             RCG_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
 #undef RCG_CASE
+#undef RCG_NA
         default:
             set_error("dpvo_rowchain_gated: unsupported epilogue flag combination " + std::to_string(f));
             return -1;
