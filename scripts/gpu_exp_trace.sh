@@ -13,6 +13,7 @@ for lib in product ${LIBS}; do
   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/prof_${TAG}_$lib -o run -- python3 scripts/${TIMER} --tag $lib \
     > gpurun_out/${TAG}_$lib.log 2>&1 || exit $?
   python3 scripts/kstats_db.py gpurun_out/prof_${TAG}_$lib "${PAT:-}" > gpurun_out/${TAG}_$lib.txt
+  rm -rf gpurun_out/prof_${TAG}_$lib   # (the traces would exceed the copy-back cap)
   grep '^{' gpurun_out/${TAG}_$lib.log | tail -1
   cat gpurun_out/${TAG}_$lib.txt
 done
