@@ -176,6 +176,13 @@ def test_kblocked_w_is_bit_identical(M, flags):
     W16b, b16b = U.pack_linear(*lin(K, 10))
     f, g = U.rowgemm_pair(buf, U.kblock(W16), b16, U.kblock(W16b), b16b)
     assert same(f, U.rowgemm(buf, W16, b16)[1]) and same(g, U.rowgemm(buf, W16b, b16b)[1])
+    # the resident-A pair at its shortest tiles (K = 128: four k-steps, the
+    # prologue's whole staging depth; K = 256), several tiles per block
+    for Kr in (128, 256):
+        Ar = torch.randn(70001, Kr, device="cuda").half()
+        (Wra, bra), (Wrb, brb) = U.pack_linear(*lin(Kr, 13)), U.pack_linear(*lin(Kr, 14))
+        f, g = U.rowgemm_pair(Ar, U.kblock(Wra), bra, U.kblock(Wrb), brb)
+        assert same(f, U.rowgemm(Ar, Wra, bra)[1]) and same(g, U.rowgemm(Ar, Wrb, brb)[1])
     (W64a, b64a), (W64b, b64b) = U.pack_linear(*lin(64, 11)), U.pack_linear(*lin(64, 12))
     A64 = A[:, :64]
     f, g = U.rowgemm_pair(A64, U.kblock(W64a), b64a, U.kblock(W64b), b64b)
