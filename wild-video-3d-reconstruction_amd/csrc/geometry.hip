@@ -21,24 +21,54 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 
 using G3 = lie::SE3<float>;
 
-__global__ __launch_bounds__(256) void transform_kernel(const float* poses, const float* patches, int P,
-                                                       const float* intr, const int64_t* ii, const int64_t* jj,
-                                                       const int64_t* kk, int64_t E, int flags, float* coords,
-                                                       float* valid)
+// PC: the patch size as a compile-time constant (3, every tracker preset) or
+// 0 for a run-time P.  The operands are __restrict__ (coords / valid never
+// alias the inputs) and, with PC, every patch value and both intrinsics are
+// loaded before the first store: the previous loop, with possible aliasing,
+// reloaded them after each pixel's stores -- a dependent L2 round trip per
+// pixel (17 us at C3).
+template <int PC>
+__global__ __launch_bounds__(256) void transform_kernel(const float* __restrict__ poses,
+                                                       const float* __restrict__ patches, int P,
+                                                       const float* __restrict__ intr, const int64_t* __restrict__ ii,
+                                                       const int64_t* __restrict__ jj, const int64_t* __restrict__ kk,
+                                                       int64_t E, int flags, float* __restrict__ coords,
+                                                       float* __restrict__ valid)
 {
     const bool depth = flags & DPVO_TF_DEPTH, tonly = flags & DPVO_TF_TONLY, chw = flags & DPVO_TF_CHW;
     const int od = depth ? 3 : 2;
-    const int64_t PP = (int64_t)P * P;
+    const int64_t PP = PC ? PC * PC : (int64_t)P * P;
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < E; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = ii[e], j = jj[e];
-        // Gij = poses[jj] * poses[ii].inv()   (projective_ops.py:60)
-        G3 g = G3::load(poses + j * 7).mul(G3::load(poses + i * 7).inv());
+        const int64_t i = ii[e], j = jj[e], k = kk[e];   // (the three index loads together)
+        __builtin_amdgcn_sched_barrier(0);
+        const float* pa = patches + k * 3 * PP;
+        // Gij = poses[jj] * poses[ii].inv()   (projective_ops.py:60); raw pose
+        // words first (G3::load normalizes: arithmetic on the loaded values)
+        float rj[7], ri[7];
+#pragma unroll
+        for (int t = 0; t < 7; t++) {
+            rj[t] = poses[j * 7 + t];
+            ri[t] = poses[i * 7 + t];
+        }
+        float ki[4], kj[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            ki[t] = intr[i * 4 + t];
+            kj[t] = intr[j * 4 + t];
+        }
+        float pv[3][PC ? PC * PC : 1];
+        if constexpr (PC > 0) {
+#pragma unroll
+            for (int c = 0; c < 3; c++)
+#pragma unroll
+                for (int q = 0; q < PC * PC; q++) pv[c][q] = pa[c * PC * PC + q];
+        }
+        __builtin_amdgcn_sched_barrier(0);   // (every operand load issued before the arithmetic)
+        G3 g = G3::load(rj).mul(G3::load(ri).inv());
         if (tonly) { g.so3.q.x = 0.f; g.so3.q.y = 0.f; g.so3.q.z = 0.f; g.so3.q.w = 1.f; }
-        const float *ki = intr + i * 4, *kj = intr + j * 4;
-        const float* pa = patches + kk[e] * 3 * PP;
-        for (int64_t q = 0; q < PP; q++) {
+        auto pixel = [&](int64_t q, float px, float py, float pd) __attribute__((always_inline)) {
             // iproj (projective_ops.py:19-29)
-            const float X0[4] = {(pa[q] - ki[2]) / ki[0], (pa[PP + q] - ki[3]) / ki[1], 1.0f, pa[2 * PP + q]};
+            const float X0[4] = {(px - ki[2]) / ki[0], (py - ki[3]) / ki[1], 1.0f, pd};
             float X1[4];
             g.act4(X0, X1);
             // proj with Z clamped to >= 0.1 (projective_ops.py:32-50)
@@ -55,28 +85,47 @@ __global__ __launch_bounds__(256) void transform_kernel(const float* poses, cons
                 if (depth) coords[(e * PP + q) * od + 2] = d;
             }
             if (valid) valid[e * PP + q] = X1[2] > 0.2f ? 1.0f : 0.0f;
+        };
+        if constexpr (PC > 0) {
+#pragma unroll
+            for (int q = 0; q < PC * PC; q++) pixel(q, pv[0][q], pv[1][q], pv[2][q]);
+        } else {
+            for (int64_t q = 0; q < PP; q++) pixel(q, pa[q], pa[PP + q], pa[2 * PP + q]);
         }
     }
 }
 
-__global__ __launch_bounds__(256) void point_cloud_kernel(const float* poses, const float* patches, int P,
-                                                         const float* intr, const int64_t* ix, int64_t m,
-                                                         int centre_only, float* out)
+__global__ __launch_bounds__(256) void point_cloud_kernel(const float* __restrict__ poses,
+                                                         const float* __restrict__ patches, int P,
+                                                         const float* __restrict__ intr,
+                                                         const int64_t* __restrict__ ix, int64_t m, int centre_only,
+                                                         float* __restrict__ out)
 {
     const int64_t PP = (int64_t)P * P, centre = (P / 2) * P + P / 2;
     for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < m; k += (int64_t)gridDim.x * blockDim.x) {
         const int64_t f = ix[k];
-        const G3 g = G3::load(poses + f * 7).inv();
         const float* K = intr + f * 4;
         const float* pa = patches + k * 3 * PP;
         if (centre_only) {
-            const float X0[4] = {(pa[centre] - K[2]) / K[0], (pa[PP + centre] - K[3]) / K[1], 1.0f, pa[2 * PP + centre]};
+            // every operand load issued before the arithmetic (G3::load normalizes)
+            float rp[7], kv[4], c[3];
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 0; t < 7; t++) rp[t] = poses[f * 7 + t];
+#pragma unroll
+            for (int t = 0; t < 4; t++) kv[t] = K[t];
+#pragma unroll
+            for (int t = 0; t < 3; t++) c[t] = pa[t * PP + centre];
+            __builtin_amdgcn_sched_barrier(0);
+            const G3 g = G3::load(rp).inv();
+            const float X0[4] = {(c[0] - kv[2]) / kv[0], (c[1] - kv[3]) / kv[1], 1.0f, c[2]};
             float X1[4];
             g.act4(X0, X1);
             out[k * 3 + 0] = X1[0] / X1[3];
             out[k * 3 + 1] = X1[1] / X1[3];
             out[k * 3 + 2] = X1[2] / X1[3];
         } else {
+            const G3 g = G3::load(poses + f * 7).inv();
             for (int64_t q = 0; q < PP; q++) {
                 const float X0[4] = {(pa[q] - K[2]) / K[0], (pa[PP + q] - K[3]) / K[1], 1.0f, pa[2 * PP + q]};
                 g.act4(X0, out + (k * PP + q) * 4);
@@ -584,8 +633,12 @@ extern "C" int dpvo_transform(const float* poses, const float* patches, int P, c
     DPVO_CHECK_ARG(P >= 1, "bad patch size");
     if (num_edges == 0) return 0;
     DPVO_CHECK_ARG(poses && patches && intrinsics && ii && jj && kk && coords, "null operand");
-    hipLaunchKernelGGL(transform_kernel, dim3(grid_for(num_edges, 256)), dim3(256), 0, as_stream(stream), poses,
-                       patches, P, intrinsics, ii, jj, kk, num_edges, flags, coords, valid);
+    if (P == 3)
+        hipLaunchKernelGGL(transform_kernel<3>, dim3(grid_for(num_edges, 256)), dim3(256), 0, as_stream(stream), poses,
+                           patches, P, intrinsics, ii, jj, kk, num_edges, flags, coords, valid);
+    else
+        hipLaunchKernelGGL(transform_kernel<0>, dim3(grid_for(num_edges, 256)), dim3(256), 0, as_stream(stream), poses,
+                           patches, P, intrinsics, ii, jj, kk, num_edges, flags, coords, valid);
     DPVO_CHECK_LAUNCH();
     return 0;
 }
