@@ -481,6 +481,19 @@ int dpvo_rowadd_ln(const dpvo_rowadd_args* args, void* stream);
 int dpvo_rowgemm_pair_pre(const dpvo_rowgemm_args* a, const dpvo_rowgemm_args* b, const dpvo_rowadd_args* pre,
                           void* stream);
 
+/* dpvo_rowchain_gated whose residual rows are not read from second->res32
+ * but formed in the row epilogue: base = LayerNorm(pre->a + pre->b16[b_idx]
+ * + pre->c16[c_idx]; pre->ln_g, ln_b, ln_eps) with dpvo_rowadd_ln's fp32
+ * arithmetic in its order -- the first GRU's `norm(net + agg_kk + agg_ij)`
+ * residual (net.py:90-92) without rowadd_ln's fp32 output rows: bit-identical
+ * to dpvo_rowadd_ln(pre with out32) followed by dpvo_rowchain_gated with
+ * res32 = those rows.  second: flags DPVO_RG_GATE | DPVO_RG_LN, res32 and
+ * res16 NULL; first: a ReLU first GEMM; pre: fp32 a (lda >= 384, 16-byte
+ * aligned), M = first->M (no M_dev), ln_g / ln_b required, out32 / out16
+ * ignored. */
+int dpvo_rowchain_gated_pre(const dpvo_rowgemm_args* gate, const dpvo_rowgemm_args* first,
+                            const dpvo_rowgemm_args* second, const dpvo_rowadd_args* pre, void* stream);
+
 /* The tracker's per-update edge keys in one launch (DPVO.update / DPVO.corr,
  * dpvo.py:326-327,718 and the SoftAgg group keys of net.py:86-88):
  * key_kk[e] = kk[e] - M base, key_ij[e] = (ii[e] - base) * 64 + (jj[e] - base),

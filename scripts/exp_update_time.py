@@ -24,7 +24,15 @@ def main():
     ap.add_argument("--tag", default=os.environ.get("DPVO_HOT_LIB", "product"))
     ap.add_argument("--preset", default="dpvo_2k")
     ap.add_argument("--buffer", type=int, default=2048)
+    ap.add_argument("--set", action="append", default=[],
+                    help="NAME=0|1: a class-level switch of dpvo.net.Update (e.g. FUSE_GRU_RES=0)")
     args = ap.parse_args()
+    from dpvo.net import Update
+    for kv in args.set:
+        k, v = kv.split("=")
+        assert hasattr(Update, k), k
+        setattr(Update, k, bool(int(v)))
+        args.tag += f" {k}={v}"
     from dpvo.synthetic import steady_state_tracker
     slam = steady_state_tracker(args.preset, buffer=args.buffer, seed=0)
     with torch.no_grad():

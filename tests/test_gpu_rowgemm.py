@@ -396,6 +396,40 @@ def test_rowchain_gated_is_gate_gemm_plus_chain(M, last):
         U.rowchain(A, W1, b1, W2, b2, flags1=U.RELU, gate16=g16, gate=(Wg, bg), **kw)
 
 
+@pytest.mark.parametrize("M", [1, 1000, 70001])
+def test_rowchain_gated_pre_is_rowadd_then_chain(M):
+    """dpvo_rowchain_gated_pre (the residual rows LayerNorm(a + b16[b_idx] +
+    c16[c_idx]) formed in the row epilogue) is bit-identical to rowadd_ln
+    writing them as out32 followed by dpvo_rowchain_gated with res32 = those
+    rows: the first GRU chain after `norm(net + agg_kk + agg_ij)` (net.py:90-92),
+    including absent / out-of-range addend indices and rows past M."""
+    import update_ops as U
+    torch.manual_seed(6)
+    dev = "cuda"
+    G1, G2 = 700, 300
+    a32 = torch.randn(M, 384, device=dev)
+    b16 = torch.randn(G1, 384, device=dev).half()
+    c16 = torch.randn(G2, 384, device=dev).half()
+    bidx = torch.randint(-1, G1 + 5, (M,), device=dev)
+    cidx = torch.randint(-1, G2 + 5, (M,), device=dev)
+    ln0 = (torch.rand(384, device=dev) + 0.5, torch.randn(384, device=dev) * 0.1, 1e-3)
+    ln1 = (torch.rand(384, device=dev) + 0.5, torch.randn(384, device=dev) * 0.1, 1e-3)
+    lin_ = lambda s: U.pack_linear(torch.randn(384, 384, device=dev) / s, torch.randn(384, device=dev) * 0.1)
+    (Wg, bg), (W1, b1), (W2, b2) = lin_(20.0), lin_(20.0), lin_(20.0)
+    r32, r16 = U.rowadd_ln(a32, b16, bidx, ln0, c16=c16, c_idx=cidx)
+    _, p16 = U.rowadd_ln(a32, b16, bidx, ln0, c16=c16, c_idx=cidx, want32=False)
+    assert same(r16, p16)
+    kw = dict(flags=U.GATE | U.LN, ln=ln1, want32=True, gate=(Wg, bg))
+    ref = U.rowchain(r16, W1, b1, W2, b2, flags1=U.RELU, res32=r32, **kw)
+    got = U.rowchain(p16, W1, b1, W2, b2, flags1=U.RELU, pre=(a32, b16, bidx, c16, cidx, ln0), **kw)
+    for r, g in zip(ref, got):
+        assert (r is None) == (g is None)
+        if r is not None:
+            assert same(r, g)
+    with pytest.raises(RuntimeError):   # res32 and pre together
+        U.rowchain(p16, W1, b1, W2, b2, flags1=U.RELU, res32=r32, pre=(a32, b16, bidx, c16, cidx, ln0), **kw)
+
+
 @pytest.mark.parametrize("M", [1, 1000, 95424])
 @pytest.mark.parametrize("gathered", [False, True])
 def test_rowchain3_is_chain_plus_rowgemm(M, gathered):

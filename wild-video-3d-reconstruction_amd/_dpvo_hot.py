@@ -86,6 +86,7 @@ _SIGNATURES = {
     "dpvo_rowchain": (_ip, [_vp, _vp, _vp]),
     "dpvo_rowchain3": (_ip, [_vp, _vp, _vp, _vp]),
     "dpvo_rowchain_gated": (_ip, [_vp, _vp, _vp, _vp]),
+    "dpvo_rowchain_gated_pre": (_ip, [_vp, _vp, _vp, _vp, _vp]),
     "dpvo_rowadd_ln": (_ip, [_vp, _vp]),
     "dpvo_append_edges_count": (_i64, [_i64, _i64, _i64]),
     "dpvo_append_edges": (_ip, [_vp, _vp, _vp, _i64, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp]),

@@ -1132,6 +1132,76 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowpair6_kernel(dpvo_rowgemm_ar
 // spill.)  Per output element the MFMA k order and the epilogue arithmetic are
 // rowgemm3's: bit-identical to the unchained launches.
 // ---------------------------------------------------------------------------
+// PRELN's row operands: R rows (R / 2 row pairs, half a wave per row, lane s
+// of the half at columns 4 s + 128 j: rowadd_ln's and epi2's layout)
+template <int R>
+struct PreOps {
+    ep_f4 a[R / 2][3];
+    ep_h4 b[R / 2][3], c[R / 2][3];
+};
+template <int R>
+__device__ __forceinline__ void preln_issue(const dpvo_rowadd_args& pre, int64_t M, int64_t row0, int lane, PreOps<R>& o)
+{
+    const int h = lane >> 5, s = lane & 31;
+    const half_t* negzero = (const half_t*)g_pre_negzero.v;
+#pragma unroll
+    for (int i = 0; i < R / 2; i++) {
+        const int64_t rr = row0 + 2 * i + h;
+        const int64_t row = rr < M ? rr : M - 1;   // clamped for loads; stores skip rows >= M
+        const int64_t sb = pre.b_idx ? pre.b_idx[row] : row;
+        const int64_t sc = pre.c_idx ? pre.c_idx[row] : row;
+        const half_t* b = pre.b16 && sb >= 0 && sb < pre.b_rows ? (const half_t*)pre.b16 + sb * RG_BN : negzero;
+        const half_t* c = pre.c16 && sc >= 0 && sc < pre.c_rows ? (const half_t*)pre.c16 + sc * RG_BN : negzero;
+        const float* a = (const float*)pre.a + row * pre.lda;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int col = 128 * j + 4 * s;
+            o.a[i][j] = *(const ep_f4*)(a + col);
+            o.b[i][j] = *(const ep_h4*)(b + col);
+            o.c[i][j] = *(const ep_h4*)(c + col);
+        }
+    }
+}
+// base = rowadd_ln(a, b16, c16, LN)'s out32 rows, operation for operation:
+// ((a + b) + c), the 12 values of a lane summed in order, half-wave sums,
+// then (v - mean) * rstd * g + beta
+template <int R>
+__device__ __forceinline__ void preln_rows(const dpvo_rowadd_args& pre, int lane, const PreOps<R>& o, EpiOps2<R>& e)
+{
+    const int s = lane & 31;
+#pragma unroll
+    for (int i = 0; i < R / 2; i++) {
+        float v[12];
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) v[4 * j + t] = o.a[i][j][t];
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) v[4 * j + t] += (float)o.b[i][j][t];
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int t = 0; t < 4; t++) v[4 * j + t] += (float)o.c[i][j][t];
+        float sm = 0.f;
+#pragma unroll
+        for (int j = 0; j < 12; j++) sm += v[j];
+        const float mean = half_sum(sm) * (1.f / RG_BN);
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < 12; j++) q += (v[j] - mean) * (v[j] - mean);
+        const float rstd = rsqrtf(half_sum(q) * (1.f / RG_BN) + pre.ln_eps);
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const ep_f4 g = *(const ep_f4*)(pre.ln_g + 128 * j + 4 * s);
+            const ep_f4 bt = *(const ep_f4*)(pre.ln_b + 128 * j + 4 * s);
+#pragma unroll
+            for (int t = 0; t < 4; t++) e.base[i][j][t] = (v[4 * j + t] - mean) * rstd * g[t] + bt[t];
+        }
+    }
+}
+
 constexpr int R5_IDX_TILES = 8;   // rowchain5: tiles per block whose row sources sit in LDS
 
 struct R5WCursor {   // (tile, segment, k-step) of the flat W-step sequence
@@ -1155,10 +1225,17 @@ struct R5WCursor {   // (tile, segment, k-step) of the flat W-step sequence
 // the update operator), or -1 to read it from p1.flags.  With the runtime
 // flags the y-tile conversion evaluates the sigmoid (exp + rcp per element)
 // beside the ReLU and selects: ~10k cycles per tile, an eighth of a c1 tile.
-template <int F2, bool GATED = false, int FMID = 0, int F1 = -1>
+// PRELN (the first GRU's gated chain, dpvo_rowchain_gated_pre): the
+// residual base is not read from res32 but formed in the row epilogue as
+// LayerNorm(pre.a + pre.b16[b_idx] + pre.c16[c_idx]) with rowadd_ln's fp32
+// arithmetic in its order (preln_rows below) -- the rows rowadd_ln would have
+// written as out32 (net.py:90-91: net + agg_kk + agg_ij -> norm), without
+// their 147 MB write and re-read.
+template <int F2, bool GATED = false, int FMID = 0, int F1 = -1, bool PRELN = false>
 __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_args p1, dpvo_rowgemm_args p,
-                                                                  dpvo_rowgemm_args pg)
+                                                                  dpvo_rowgemm_args pg, dpvo_rowadd_args pre)
 {
+    static_assert(!PRELN || (GATED && (F2 & RG_NOADD) && (F2 & RG_LN)), "PRELN: the gated LN chain");
     constexpr bool TRI = FMID != 0;
     static_assert(!(TRI && GATED), "a chain is either gated or three GEMMs long");
     // (RES | LN overlapped the same way -- the corr chain, the gated LN chain --
@@ -1550,6 +1627,16 @@ __global__ __launch_bounds__(R5_THREADS, 1) void rowchain5_kernel(dpvo_rowgemm_a
                 epi_issue(tile, 16 * w + q0, st);
                 epi_done(tile, 16 * w + q0, kc, st);
             }
+        } else if constexpr (PRELN) {
+            PreOps<4> st[2];
+            preln_issue<4>(pre, Mrows, tile * RG_BM + 16 * w, lane, st[0]);
+            bd_steps<0, 4>::run([&](auto bc) __attribute__((always_inline)) {
+                constexpr int b = decltype(bc)::value;
+                if constexpr (b + 1 < 4) preln_issue<4>(pre, Mrows, tile * RG_BM + 16 * w + 4 * (b + 1), lane, st[(b + 1) & 1]);
+                EpiOps2<4> o;
+                preln_rows<4>(pre, lane, st[b & 1], o);
+                epi_done(tile, 16 * w + 4 * b, kc, o);
+            });
         } else {
             EpiOps2<4> st[2];
             epi_issue(tile, 16 * w, st[0]);
@@ -1916,7 +2003,7 @@ extern "C" int dpvo_rowgemm(const dpvo_rowgemm_args* a, void* stream)
 }
 
 static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args* g2, const dpvo_rowgemm_args* gate,
-                           void* stream)
+                           void* stream, const dpvo_rowadd_args* pre = nullptr)
 {
     DPVO_CHECK_ARG(g1 != nullptr && g2 != nullptr, "null args");
     DPVO_CHECK_ARG(g1->N == RG_BN && g2->N == RG_BN, "rowchain: output widths must be 384");
@@ -1953,6 +2040,16 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
     a2.M = g1->M;
     a2.M_dev = g1->M_dev;
     const bool relu1 = g1->flags == DPVO_RG_RELU;   // (the compile-time activation)
+    if (pre) {   // the first GRU chain: the residual base is LayerNorm(pre rows), formed in the epilogue
+        DPVO_CHECK_ARG(gate && f == (DPVO_RG_GATE | DPVO_RG_LN) && relu1,
+                       "rowchain_gated_pre: a gated GATE | LN chain with a ReLU first GEMM");
+        a2.gate16 = nullptr;
+        a2.res16 = nullptr;
+        hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | DPVO_RG_LN | RG_NOADD, true, 0, RG_RELU, true>), dim3(grid),
+                           dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, *gate, *pre);
+        DPVO_CHECK_LAUNCH();
+        return 0;
+    }
     if (gate) {
         // the gated y goes through the RES epilogue (res16 none): x + fp16(gate * y)
         a2.gate16 = nullptr;
@@ -1964,10 +2061,10 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
     case (F):                                                                                                         \
         if (relu1)                                                                                                    \
             hipLaunchKernelGGL((rowchain5_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES | RCG_NA, true, 0, RG_RELU>),    \
-                               dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, *gate);                   \
+                               dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, *gate, dpvo_rowadd_args{});                   \
         else                                                                                                          \
             hipLaunchKernelGGL((rowchain5_kernel<((F) & ~DPVO_RG_GATE) | DPVO_RG_RES | RCG_NA, true>), dim3(grid),    \
-                               dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, *gate);                               \
+                               dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, *gate, dpvo_rowadd_args{});                               \
         break;
             RCG_CASE(DPVO_RG_GATE | DPVO_RG_LN)
             RCG_CASE(DPVO_RG_GATE | DPVO_RG_HEADS)
@@ -1983,10 +2080,10 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
     if (f == DPVO_RG_RES && !g2->res16) {   // (c1 / c2: no addend loads, + 0 in their place)
         if (relu1)
             hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | RG_NOADD, false, 0, RG_RELU>), dim3(grid),
-                               dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, a2);
+                               dim3(R5_THREADS), 0, as_stream(stream), *g1, a2, a2, dpvo_rowadd_args{});
         else
             hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | RG_NOADD>), dim3(grid), dim3(R5_THREADS), 0,
-                               as_stream(stream), *g1, a2, a2);
+                               as_stream(stream), *g1, a2, a2, dpvo_rowadd_args{});
         DPVO_CHECK_LAUNCH();
         return 0;
     }
@@ -1995,10 +2092,10 @@ static int rowchain_launch(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_args*
     case (F):                                                                                                         \
         if (relu1)                                                                                                    \
             hipLaunchKernelGGL((rowchain5_kernel<(F), false, 0, RG_RELU>), dim3(grid), dim3(R5_THREADS), 0,           \
-                               as_stream(stream), *g1, a2, a2);                                                       \
+                               as_stream(stream), *g1, a2, a2, dpvo_rowadd_args{});                                   \
         else                                                                                                          \
             hipLaunchKernelGGL(rowchain5_kernel<(F)>, dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a2,   \
-                               a2);                                                                                   \
+                               a2, dpvo_rowadd_args{});                                                               \
         break;
         RCH_CASE(DPVO_RG_LN | DPVO_RG_LN_RELU)
         RCH_CASE(DPVO_RG_RES)
@@ -2057,10 +2154,10 @@ extern "C" int dpvo_rowchain3(const dpvo_rowgemm_args* g1, const dpvo_rowgemm_ar
     a3.M_dev = g1->M_dev;
     if (g1->flags == DPVO_RG_RELU)
         hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | DPVO_RG_LN, false, DPVO_RG_LN | DPVO_RG_LN_RELU, RG_RELU>),
-                           dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a3, *g2);
+                           dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a3, *g2, dpvo_rowadd_args{});
     else
         hipLaunchKernelGGL((rowchain5_kernel<DPVO_RG_RES | DPVO_RG_LN, false, DPVO_RG_LN | DPVO_RG_LN_RELU>),
-                           dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a3, *g2);
+                           dim3(grid), dim3(R5_THREADS), 0, as_stream(stream), *g1, a3, *g2, dpvo_rowadd_args{});
     DPVO_CHECK_LAUNCH();
     return 0;
 }
@@ -2070,6 +2167,25 @@ extern "C" int dpvo_rowchain_gated(const dpvo_rowgemm_args* gate, const dpvo_row
 {
     DPVO_CHECK_ARG(gate != nullptr, "rowchain_gated: gate args missing");
     return rowchain_launch(g1, g2, gate, stream);
+}
+
+extern "C" int dpvo_rowchain_gated_pre(const dpvo_rowgemm_args* gate, const dpvo_rowgemm_args* g1,
+                                       const dpvo_rowgemm_args* g2, const dpvo_rowadd_args* pre, void* stream)
+{
+    DPVO_CHECK_ARG(gate != nullptr && pre != nullptr, "rowchain_gated_pre: gate / pre args missing");
+    DPVO_CHECK_ARG(pre->a && !pre->a_f16 && pre->lda >= RG_BN && pre->lda % 4 == 0 && ((uintptr_t)pre->a & 15) == 0,
+                   "rowchain_gated_pre: pre.a must be fp32 rows of >= 384 (16-byte aligned)");
+    DPVO_CHECK_ARG(pre->ln_g && pre->ln_b && ((uintptr_t)pre->ln_g & 15) == 0 && ((uintptr_t)pre->ln_b & 15) == 0,
+                   "rowchain_gated_pre: pre.ln_g / ln_b (16-byte aligned) are required");
+    DPVO_CHECK_ARG((!pre->b16 || ((uintptr_t)pre->b16 & 7) == 0) && (!pre->c16 || ((uintptr_t)pre->c16 & 7) == 0),
+                   "rowchain_gated_pre: pre.b16 / c16 must be 8-byte aligned");
+    DPVO_CHECK_ARG(!pre->c16 || pre->b16, "rowchain_gated_pre: c16 needs b16");
+    DPVO_CHECK_ARG(pre->M == g1->M && !g1->M_dev, "rowchain_gated_pre: pre.M must be the chain's row count");
+    DPVO_CHECK_ARG(!g2->res32 && !g2->res16, "rowchain_gated_pre: the residual comes from pre (res32 / res16 NULL)");
+    dpvo_rowgemm_args b2 = *g2;
+    b2.res32 = pre->a;   // (rowchain_launch's residual check; the kernel reads pre)
+    b2.ldr = pre->lda;
+    return rowchain_launch(g1, &b2, gate, stream, pre);
 }
 
 #ifdef DPVO_STAMPS

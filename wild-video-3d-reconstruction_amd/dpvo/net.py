@@ -40,6 +40,9 @@ class Update(nn.Module):
     FUSED = True  # inference under fp16 autocast runs the fused HIP path (class-level switch for A/B tests)
     CORR_CHAIN3 = True  # the corr MLP + first LayerNorm as one three-GEMM launch (False: two launches)
     FUSE_AGG_ADD = True  # the agg_kk row add inside agg_ij's f / g launch (False: a rowadd_ln pass; same bits)
+    # the first GRU chain forms its residual norm(net + agg_kk + agg_ij) in its
+    # epilogue (rowadd_ln writes only the fp16 rows; False: the fp32 rows too; same bits)
+    FUSE_GRU_RES = True
 
     # ------------------------------------------------------------ fused path
     def _packed(self):
@@ -146,6 +149,9 @@ class Update(nn.Module):
                 if not self.FUSE_AGG_ADD:
                     _, n16 = U.rowadd_ln(n32, hy, gid, want32=False)
                 kk_add = (hy, gid)
+            elif self.FUSE_GRU_RES:
+                _, n16 = U.rowadd_ln(n32, *kk_add, c16=hy, c_idx=gid, ln=ln, want32=False)
+                gru_pre = (n32, kk_add[0], kk_add[1], hy, gid, ln)
             else:
                 n32, n16 = U.rowadd_ln(n32, *kk_add, c16=hy, c_idx=gid, ln=ln)
         # gru = LN0 (fused above), GatedResidual, LN1, GatedResidual; then the d / w heads
@@ -155,6 +161,9 @@ class Update(nn.Module):
             if last:
                 n32, _, heads = U.rowchain(n16, *pr1, *pr2, flags1=U.RELU, flags=U.GATE | U.HEADS, res32=n32,
                                            gate=pgate, heads=pk["heads"], want32=True, want16=False)
+            elif self.FUSE_GRU_RES:
+                n32, n16, _ = U.rowchain(n16, *pr1, *pr2, flags1=U.RELU, flags=U.GATE | U.LN, gate=pgate, ln=ln1,
+                                         want32=True, pre=gru_pre)
             else:
                 n32, n16, _ = U.rowchain(n16, *pr1, *pr2, flags1=U.RELU, flags=U.GATE | U.LN, res32=n32,
                                          gate=pgate, ln=ln1, want32=True)

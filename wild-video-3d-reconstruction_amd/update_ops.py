@@ -81,7 +81,8 @@ def softagg_csr(f, s, offs, perm, groups, max_groups, eps=1e-12, long_groups=Fal
 
 
 def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=None, res16=None, res16_idx=None,
-             gate16=None, ln=None, heads=None, want32=False, want16=True, M_dev=None, gate=None, mid=None):
+             gate16=None, ln=None, heads=None, want32=False, want16=True, M_dev=None, gate=None, mid=None,
+             pre=None):
     """rowgemm(rowgemm(A, W1, b1, flags1, a_idx).y16, W2, b2, flags, ...) in one
     launch, the 384-wide intermediate kept on chip (dpvo_rowchain).
     gate = (Wg, bg) with GATE in flags: gate16 = rowgemm(A, Wg, bg, SIGMOID)
@@ -90,6 +91,10 @@ def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=
     output LayerNorm'd and ReLU'd on chip (dpvo_rowchain3; flags must be
     RES | LN): rowgemm(rowchain(A, W1, b1, Wm, bm, LN | LN_RELU).out16, W2, b2,
     flags, ...) in one launch.
+    pre = (a32, b16, b_idx, c16, c_idx, (ln_g, ln_b, eps)) with gate and res32
+    None: the residual rows are rowadd_ln(a32, b16, b_idx, ln, c16=c16,
+    c_idx=c_idx)'s out32, formed in the row epilogue instead of read
+    (dpvo_rowchain_gated_pre, bit-identical).
     Weights may be given as [384, Kp] (re-laid out per call) or already
     k-blocked by kblock() (what the kernel reads; the fused Update caches them).
     Returns (out32, out16, head_out) of the last GEMM."""
@@ -155,7 +160,25 @@ def rowchain(A, W1, b1, W2, b2, flags1=None, flags=0, a_idx=None, M=None, res32=
             raise RuntimeError("rowchain: pass either gate16 or gate, not both")
         gg = RowGemmArgs()
         gg.W, gg.K, gg.N, gg.bias = _p(Wg), Kp, WIDTH, _p(bg)
-        H.check(H.lib().dpvo_rowchain_gated(_ct.byref(gg), _ct.byref(g1), _ct.byref(g2), H.stream_of(A)))
+        if pre is not None:
+            a32, pb16, pbi, pc16, pci, pln = pre
+            H.on_gpu(a32, pb16, pc16, pln[0], pln[1])
+            if res32 is not None or a32.dtype != torch.float32 or a32.dim() != 2 or a32.shape != (M, WIDTH) \
+                    or a32.stride(1) != 1:
+                raise RuntimeError("rowchain: pre's a32 must be fp32 [M, 384] row-contiguous, res32 None")
+            for t in (pb16, pc16):
+                if t.dtype != torch.float16 or not t.is_contiguous() or t.shape[-1] != WIDTH:
+                    raise RuntimeError("rowchain: pre's b16 / c16 must be contiguous fp16 [*, 384]")
+            pbi, pci = H.idx64(pbi), H.idx64(pci)
+            pa = RowAddArgs()
+            pa.a, pa.a_f16, pa.lda, pa.M = _p(a32), 0, a32.stride(0), M
+            pa.b16, pa.b_idx, pa.b_rows = _p(pb16), _p(pbi), pb16.shape[0]
+            pa.c16, pa.c_idx, pa.c_rows = _p(pc16), _p(pci), pc16.shape[0]
+            pa.ln_g, pa.ln_b, pa.ln_eps = _p(pln[0]), _p(pln[1]), float(pln[2])
+            H.check(H.lib().dpvo_rowchain_gated_pre(_ct.byref(gg), _ct.byref(g1), _ct.byref(g2), _ct.byref(pa),
+                                                    H.stream_of(A)))
+        else:
+            H.check(H.lib().dpvo_rowchain_gated(_ct.byref(gg), _ct.byref(g1), _ct.byref(g2), H.stream_of(A)))
     elif mid is not None:
         Wm, bm, lnm = mid
         H.on_gpu(Wm, bm, lnm[0], lnm[1])
