@@ -15,7 +15,8 @@ Both are the L2's memory-side counters (Infinity-Cache hits included).
 Records, per kernel: dispatches, bytes per dispatch; and the two groups the
 bench line uses:
   corr      = edge_hist + edge_scatter + corr_mfma (one altcorr phase per update)
-  update_op = rowgemm / rowchain / rowadd_ln / sa_reduce / nb_csr kernels,
+  update_op = rowgemm (incl. the narrow GEMM) / rowpair / rowchain / rowadd_ln /
+              sa_reduce / nb_csr kernels,
               bytes per update() (total / corr_mfma dispatches: every update,
               and every phase_breakdown repetition, runs altcorr once)
 plus the sha of the HIP sources (bench.py uses the record only when they match).
@@ -33,7 +34,7 @@ REPO = os.path.dirname(HERE)
 sys.path.insert(0, REPO)
 
 CORR = re.compile(r"corr_mfma_kernel|edge_hist_kernel|edge_scatter_kernel")
-UPD = re.compile(r"rowgemm\d?_kernel|rowchain\d?_kernel|rowadd_ln_kernel|sa_reduce_csr|nb_csr_kernel")
+UPD = re.compile(r"rowgemm\w*_kernel|rowpair\d?_kernel|rowchain\d?_kernel|rowadd_ln_kernel|sa_reduce_csr|nb_csr_kernel")
 
 
 def short(name):
